@@ -1,0 +1,483 @@
+// kh_capi.cpp — C ABI implementation (include/kmer_hash_amd.h): table lifetime, device buffers,
+// HIP streams/events, and the host-side orchestration of the kernels in kh_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/kmer_hash_amd.h"
+#include "kh_codec.hpp"
+#include "kh_internal.hpp"
+#include "kh_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define KH_HIP(call)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(KH_ERR_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),     \
+                        __FILE__, __LINE__);                                                  \
+    } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    uint64_t bytes = 0;
+    int ensure(uint64_t want) {
+        if (want <= bytes && p) return KH_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (want == 0) want = 16;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(KH_ERR_NOMEM, "hipMalloc(%llu) failed: %s", (unsigned long long)want,
+                        hipGetErrorString(e));
+        }
+        bytes = want;
+        return KH_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+}  // namespace
+
+void kh_set_error_internal(const char* msg) { g_err = msg ? msg : ""; }
+
+struct kh_table {
+    int device = 0;
+    kh::KParams kp{};
+    uint64_t cap = 0;       // slots
+    uint64_t n_kmers = 0;   // k-mers the table was created for
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+
+    DevBuf slots, starts, ctr, stats;
+    DevBuf mask, mask_off, scratch;          // per insert batch
+    DevBuf stage;                            // host-API staging of records / keys
+    DevBuf stage2, stage3;
+    DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text;
+    uint64_t starts_cap = 0;                 // start entries the starts buffer holds
+    uint64_t chunk_cap = 0;
+
+    uint64_t n_inserted = 0;                 // host-side count (what was submitted)
+    uint64_t last_contigs = 0;               // n_starts seen by the last assemble
+    bool assembled = false;
+
+    hipEvent_t ev_ins0 = nullptr, ev_ins1 = nullptr, ev_ins2 = nullptr;
+    hipEvent_t ev_walk0 = nullptr, ev_walk1 = nullptr, ev_mat1 = nullptr;
+    bool ins_timed = false, walk_timed = false;
+};
+
+namespace {
+
+int set_device(const kh_table* t) {
+    KH_HIP(hipSetDevice(t->device));
+    return KH_OK;
+}
+
+kh::TableView view(const kh_table* t) { return kh::TableView{t->slots.as<uint64_t>(), t->cap}; }
+
+int ensure_starts(kh_table* t, uint64_t need) {
+    if (need <= t->starts_cap) return KH_OK;
+    const uint64_t W = (uint64_t)t->kp.W;
+    uint64_t newcap = need < 1024 ? 1024 : need;
+    DevBuf nb;
+    int rc = nb.ensure(newcap * W * 8);
+    if (rc) return rc;
+    if (t->starts.p && t->starts_cap)
+        KH_HIP(hipMemcpyAsync(nb.p, t->starts.p, t->starts_cap * W * 8, hipMemcpyDeviceToDevice,
+                              t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    t->starts.release();
+    t->starts = nb;
+    t->starts_cap = newcap;
+    return KH_OK;
+}
+
+int read_ctr(kh_table* t, int idx, uint64_t* v) {
+    unsigned long long x = 0;
+    KH_HIP(hipMemcpyAsync(&x, t->ctr.as<unsigned long long>() + idx, sizeof x,
+                          hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    *v = x;
+    return KH_OK;
+}
+
+// First device-side error, as a status code.
+int check_stats(kh_table* t) {
+    unsigned long long st[kh::ST_NUM];
+    KH_HIP(hipMemcpyAsync(st, t->stats.p, sizeof st, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    if (st[kh::ST_FULL]) return fail(KH_ERR_FULL, "table full: %llu probes wrapped", st[kh::ST_FULL]);
+    if (st[kh::ST_DUP]) return fail(KH_ERR_DUPLICATE, "%llu duplicate k-mers inserted", st[kh::ST_DUP]);
+    if (st[kh::ST_BAD_EXT])
+        return fail(KH_ERR_BAD_BASE, "%llu extension bytes outside {A,C,G,T,F}", st[kh::ST_BAD_EXT]);
+    if (st[kh::ST_MISSING])
+        return fail(KH_ERR_NOT_FOUND, "Error: k-mer not found in hash map (%llu walks)",
+                    st[kh::ST_MISSING]);
+    if (st[kh::ST_CYCLE]) return fail(KH_ERR_CYCLE, "%llu walks exceeded the table size", st[kh::ST_CYCLE]);
+    if (st[kh::ST_SPIN]) return fail(KH_ERR_HIP, "%llu inserts timed out on a slot", st[kh::ST_SPIN]);
+    if (st[kh::ST_CHUNK_OVF]) return fail(KH_ERR_NOMEM, "walker chunk pool overflow");
+    return KH_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int kh_abi_version(void) { return KH_ABI_VERSION; }
+int kh_packed_size(int k) { return (k >= 1 && k <= KH_K_MAX) ? (k + 3) / 4 : KH_ERR_ARG; }
+int kh_record_size(int k) { return (k >= 1 && k <= KH_K_MAX) ? (k + 3) / 4 + 2 : KH_ERR_ARG; }
+const char* kh_last_error(void) { return g_err.c_str(); }
+
+int kh_device_count(int* n) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *n = 0;
+        return fail(KH_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *n = c;
+    return KH_OK;
+}
+
+int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int device) {
+    if (!out) return fail(KH_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (k < 1 || k > KH_K_MAX) return fail(KH_ERR_ARG, "k=%d outside [1,%d]", k, KH_K_MAX);
+    if (!(load_factor > 0.0 && load_factor < 1.0))
+        return fail(KH_ERR_ARG, "load factor %g outside (0,1)", load_factor);
+    kh_table* t = new (std::nothrow) kh_table();
+    if (!t) return fail(KH_ERR_NOMEM, "host allocation failed");
+    t->device = device;
+    t->kp = kh::make_params(k);
+    t->n_kmers = n_kmers;
+    double c = (double)(n_kmers ? n_kmers : 1) / load_factor;
+    t->cap = (uint64_t)c;
+    if ((double)t->cap < c) t->cap++;
+    if (t->cap < 2) t->cap = 2;
+    int rc = KH_OK;
+    auto bail = [&](int r) {
+        kh_destroy(t);
+        return r;
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return bail(fail(KH_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)));
+    if (hipStreamCreateWithFlags(&t->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(KH_ERR_HIP, "hipStreamCreate failed"));
+    t->stream = t->own_stream;
+    hipEvent_t* evs[] = {&t->ev_ins0, &t->ev_ins1, &t->ev_ins2, &t->ev_walk0, &t->ev_walk1, &t->ev_mat1};
+    for (auto* ev : evs)
+        if (hipEventCreate(ev) != hipSuccess) return bail(fail(KH_ERR_HIP, "hipEventCreate failed"));
+    if ((rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8))) return bail(rc);
+    if ((rc = t->ctr.ensure(kh::CT_NUM * 8))) return bail(rc);
+    if ((rc = t->stats.ensure(kh::ST_NUM * 8))) return bail(rc);
+    if ((rc = kh_clear(t))) return bail(rc);
+    if (hipStreamSynchronize(t->stream) != hipSuccess) return bail(fail(KH_ERR_HIP, "sync failed"));
+    *out = t;
+    return KH_OK;
+}
+
+int kh_destroy(kh_table* t) {
+    if (!t) return KH_OK;
+    (void)hipSetDevice(t->device);
+    if (t->stream) (void)hipStreamSynchronize(t->stream);
+    DevBuf* bufs[] = {&t->slots, &t->starts, &t->ctr, &t->stats, &t->mask, &t->mask_off,
+                      &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
+                      &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text};
+    for (auto* b : bufs) b->release();
+    hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1};
+    for (auto ev : evs)
+        if (ev) (void)hipEventDestroy(ev);
+    if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
+    delete t;
+    return KH_OK;
+}
+
+int kh_clear(kh_table* t) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(hipMemsetAsync(t->slots.p, 0xff, t->cap * (uint64_t)t->kp.W * 8, t->stream));
+    KH_HIP(hipMemsetAsync(t->ctr.p, 0, kh::CT_NUM * 8, t->stream));
+    KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
+    t->n_inserted = 0;
+    t->assembled = false;
+    return KH_OK;
+}
+
+int kh_set_stream(kh_table* t, void* s) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    t->stream = s ? (hipStream_t)s : t->own_stream;
+    return KH_OK;
+}
+
+int kh_sync(kh_table* t) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(hipStreamSynchronize(t->stream));
+    return check_stats(t);
+}
+
+uint64_t kh_capacity(const kh_table* t) { return t ? t->cap : 0; }
+
+int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (n == 0) return KH_OK;
+    if (!dev_recs) return fail(KH_ERR_ARG, "null records");
+    if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
+    if (t->n_inserted + n > t->n_kmers)
+        return fail(KH_ERR_FULL, "inserting %llu k-mers into a table created for %llu (%llu in)",
+                    (unsigned long long)n, (unsigned long long)t->n_kmers,
+                    (unsigned long long)t->n_inserted);
+    if (int rc = set_device(t)) return rc;
+    int rc;
+    const uint64_t nw = (n + 63) / 64;
+    if ((rc = t->mask.ensure(nw * 8))) return rc;
+    if ((rc = t->mask_off.ensure(nw * 8))) return rc;
+    if ((rc = t->scratch.ensure(kh::scan_scratch_words(nw > n ? nw : n) * 8 + 64))) return rc;
+    if ((rc = ensure_starts(t, t->n_inserted + n))) return rc;
+    KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
+    KH_HIP(kh::launch_insert(t->kp, (const uint8_t*)dev_recs, n, view(t), t->mask.as<uint64_t>(),
+                             t->stats.as<unsigned long long>(), t->stream));
+    KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
+    KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
+                                     t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                     t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(),
+                                     t->stream));
+    KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
+    t->ins_timed = true;
+    t->n_inserted += n;
+    t->assembled = false;
+    return KH_OK;
+}
+
+int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (n == 0) return KH_OK;
+    if (!host_recs) return fail(KH_ERR_ARG, "null records");
+    if (int rc = set_device(t)) return rc;
+    const uint64_t bytes = n * (uint64_t)t->kp.R;
+    if (int rc = t->stage.ensure(bytes)) return rc;
+    KH_HIP(hipMemcpyAsync(t->stage.p, host_recs, bytes, hipMemcpyHostToDevice, t->stream));
+    if (int rc = kh_insert_dev(t, t->stage.p, n)) return rc;
+    KH_HIP(hipStreamSynchronize(t->stream));
+    return check_stats(t);
+}
+
+int kh_find_dev(kh_table* t, const void* dev_keys, uint64_t n, void* dev_out, void* dev_found) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (n == 0) return KH_OK;
+    if (!dev_keys || !dev_out || !dev_found) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_find(t->kp, (const uint8_t*)dev_keys, n, view(t), (uint8_t*)dev_out,
+                           (uint8_t*)dev_found, t->stream));
+    return KH_OK;
+}
+
+int kh_find(kh_table* t, const uint8_t* keys, uint64_t n, uint8_t* out, uint8_t* found) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (n == 0) return KH_OK;
+    if (!keys || !out || !found) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    const uint64_t kb = n * (uint64_t)t->kp.P, rb = n * (uint64_t)t->kp.R;
+    int rc;
+    if ((rc = t->stage.ensure(kb))) return rc;
+    if ((rc = t->stage2.ensure(rb))) return rc;
+    if ((rc = t->stage3.ensure(n))) return rc;
+    KH_HIP(hipMemcpyAsync(t->stage.p, keys, kb, hipMemcpyHostToDevice, t->stream));
+    if ((rc = kh_find_dev(t, t->stage.p, n, t->stage2.p, t->stage3.p))) return rc;
+    KH_HIP(hipMemcpyAsync(out, t->stage2.p, rb, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipMemcpyAsync(found, t->stage3.p, n, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    return KH_OK;
+}
+
+int kh_set_starts(kh_table* t, const uint8_t* recs, uint64_t n) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (n && !recs) return fail(KH_ERR_ARG, "null records");
+    if (int rc = set_device(t)) return rc;
+    int rc;
+    if ((rc = ensure_starts(t, n))) return rc;
+    const uint64_t bytes = n * (uint64_t)t->kp.R;
+    if ((rc = t->stage.ensure(bytes))) return rc;
+    if (n) KH_HIP(hipMemcpyAsync(t->stage.p, recs, bytes, hipMemcpyHostToDevice, t->stream));
+    KH_HIP(kh::launch_load_starts(t->kp, t->stage.as<uint8_t>(), n, t->starts.as<uint64_t>(),
+                                  t->ctr.as<unsigned long long>(), t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    t->assembled = false;
+    return KH_OK;
+}
+
+int kh_assemble_dev(kh_table* t) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (int rc = set_device(t)) return rc;
+    int rc;
+    uint64_t ns = 0;
+    // The start count decides buffer sizes and the grid (the reference also knows
+    // start_nodes.size() on the host before walking, kmer_hash.cpp:41).
+    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
+    const uint64_t n = t->n_inserted > ns ? t->n_inserted : ns;
+    const uint64_t chunk_cap = n / kh::CHUNK_BASES + ns + 64;
+    if ((rc = t->contig_len.ensure((ns + 1) * 4))) return rc;
+    if ((rc = t->contig_off.ensure((ns + 1) * 8))) return rc;
+    if ((rc = t->chunk_data.ensure(chunk_cap * kh::CHUNK_WORDS * 8))) return rc;
+    if ((rc = t->chunk_owner.ensure(chunk_cap * 4))) return rc;
+    if ((rc = t->chunk_seq.ensure(chunk_cap * 4))) return rc;
+    if ((rc = t->text.ensure(n + ns * ((uint64_t)t->kp.K + 1) + 64))) return rc;
+    if ((rc = t->scratch.ensure(kh::scan_scratch_words(ns) * 8 + 64))) return rc;
+    t->chunk_cap = chunk_cap;
+    kh::WalkBuffers wb;
+    wb.starts = t->starts.as<uint64_t>();
+    wb.n_starts = ns;
+    wb.contig_len = t->contig_len.as<uint32_t>();
+    wb.chunk_data = t->chunk_data.as<uint64_t>();
+    wb.chunk_owner = t->chunk_owner.as<uint32_t>();
+    wb.chunk_seq = t->chunk_seq.as<uint32_t>();
+    wb.chunk_cap = chunk_cap;
+    wb.max_steps = n;
+    unsigned long long* ctr = t->ctr.as<unsigned long long>();
+    KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
+    KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
+    KH_HIP(kh::launch_walk(t->kp, view(t), wb, ctr, t->stats.as<unsigned long long>(), 0, t->stream));
+    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
+    KH_HIP(kh::launch_materialize(t->kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                  t->text.as<char>(), ctr, t->stream));
+    KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
+    t->walk_timed = true;
+    t->last_contigs = ns;
+    t->assembled = true;
+    return KH_OK;
+}
+
+int kh_assemble(kh_table* t, uint64_t* n_contigs, uint64_t* out_bytes) {
+    if (int rc = kh_assemble_dev(t)) return rc;
+    KH_HIP(hipStreamSynchronize(t->stream));
+    if (int rc = check_stats(t)) return rc;
+    uint64_t ob = 0;
+    if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
+    if (n_contigs) *n_contigs = t->last_contigs;
+    if (out_bytes) *out_bytes = ob;
+    return KH_OK;
+}
+
+int kh_contigs_text_dev(kh_table* t, const char** dev_text, uint64_t* bytes) {
+    if (!t || !dev_text || !bytes) return fail(KH_ERR_ARG, "null argument");
+    if (!t->assembled) return fail(KH_ERR_STATE, "no assemble since the last insert/clear");
+    uint64_t ob = 0;
+    if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
+    *dev_text = t->text.as<const char>();
+    *bytes = t->last_contigs ? ob : 0;
+    return KH_OK;
+}
+
+int kh_contigs_text(kh_table* t, char* out, uint64_t cap) {
+    const char* d = nullptr;
+    uint64_t b = 0;
+    if (int rc = kh_contigs_text_dev(t, &d, &b)) return rc;
+    if (cap < b) return fail(KH_ERR_ARG, "buffer of %llu bytes < %llu", (unsigned long long)cap,
+                             (unsigned long long)b);
+    if (b) KH_HIP(hipMemcpy(out, d, b, hipMemcpyDeviceToHost));
+    return KH_OK;
+}
+
+int kh_contigs_offsets(kh_table* t, uint64_t* out, uint64_t n) {
+    if (!t || (!out && n)) return fail(KH_ERR_ARG, "null argument");
+    if (!t->assembled) return fail(KH_ERR_STATE, "no assemble since the last insert/clear");
+    if (n > t->last_contigs) return fail(KH_ERR_ARG, "asked for %llu offsets of %llu contigs",
+                                         (unsigned long long)n, (unsigned long long)t->last_contigs);
+    if (n) {
+        KH_HIP(hipStreamSynchronize(t->stream));
+        KH_HIP(hipMemcpy(out, t->contig_off.p, n * 8, hipMemcpyDeviceToHost));
+    }
+    return KH_OK;
+}
+
+int kh_get_stats(kh_table* t, kh_stats* s) {
+    if (!t || !s) return fail(KH_ERR_ARG, "null argument");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(hipStreamSynchronize(t->stream));
+    unsigned long long st[kh::ST_NUM], ct[kh::CT_NUM];
+    KH_HIP(hipMemcpy(st, t->stats.p, sizeof st, hipMemcpyDeviceToHost));
+    KH_HIP(hipMemcpy(ct, t->ctr.p, sizeof ct, hipMemcpyDeviceToHost));
+    std::memset(s, 0, sizeof *s);
+    s->capacity = t->cap;
+    s->n_inserted = t->n_inserted;
+    s->n_starts = ct[kh::CT_N_STARTS];
+    if (t->assembled) {
+        s->n_contigs = t->last_contigs;
+        s->out_bytes = ct[kh::CT_OUT_BYTES];
+        // bytes = sum(K + len) -> lookups = sum(len - 1) = bytes - contigs * (K + 1)
+        s->n_lookups = s->out_bytes - s->n_contigs * ((uint64_t)t->kp.K + 1);
+        s->n_chunks = ct[kh::CT_CHUNK_NEXT] < t->chunk_cap ? ct[kh::CT_CHUNK_NEXT] : t->chunk_cap;
+    }
+    s->n_dup = st[kh::ST_DUP];
+    s->n_full = st[kh::ST_FULL];
+    s->n_bad_ext = st[kh::ST_BAD_EXT];
+    s->n_missing = st[kh::ST_MISSING];
+    s->n_cycle = st[kh::ST_CYCLE];
+    s->n_spin = st[kh::ST_SPIN];
+    s->n_chunk_ovf = st[kh::ST_CHUNK_OVF];
+    float ms = 0.f;
+    if (t->ins_timed) {
+        if (hipEventElapsedTime(&ms, t->ev_ins0, t->ev_ins2) == hipSuccess) s->ms_insert = ms;
+        if (hipEventElapsedTime(&ms, t->ev_ins0, t->ev_ins1) == hipSuccess) s->ms_insert_kernel = ms;
+    }
+    if (t->walk_timed) {
+        if (hipEventElapsedTime(&ms, t->ev_walk0, t->ev_walk1) == hipSuccess) s->ms_walk = ms;
+        if (hipEventElapsedTime(&ms, t->ev_walk1, t->ev_mat1) == hipSuccess) s->ms_materialize = ms;
+    }
+    return KH_OK;
+}
+
+// ---- device memory helpers -------------------------------------------------------------------
+int kh_dev_malloc(void** p, uint64_t bytes, int device) {
+    if (!p) return fail(KH_ERR_ARG, "null out pointer");
+    KH_HIP(hipSetDevice(device));
+    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+    if (e != hipSuccess) return fail(KH_ERR_NOMEM, "hipMalloc(%llu): %s", (unsigned long long)bytes,
+                                     hipGetErrorString(e));
+    return KH_OK;
+}
+int kh_dev_free(void* p) {
+    if (p) KH_HIP(hipFree(p));
+    return KH_OK;
+}
+int kh_memcpy_htod(void* dst, const void* src, uint64_t bytes) {
+    if (bytes) KH_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return KH_OK;
+}
+int kh_memcpy_dtoh(void* dst, const void* src, uint64_t bytes) {
+    if (bytes) KH_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return KH_OK;
+}
+
+}  // extern "C"

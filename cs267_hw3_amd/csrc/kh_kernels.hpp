@@ -1,0 +1,83 @@
+// kh_kernels.hpp — launch wrappers for the gfx950 k-mer table / contig walker kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kh_codec.hpp"
+
+namespace kh {
+
+// Device-side error / event counters (one 64-bit word each).
+enum StatIdx : int {
+    ST_DUP = 0,        // duplicate key on insert (input contract: keys unique, README.md:35)
+    ST_FULL = 1,       // probe wrapped the whole table
+    ST_BAD_EXT = 2,    // extension byte not in {A,C,G,T,F}
+    ST_MISSING = 3,    // walk: next k-mer absent (kmer_hash.cpp:47-49 throws)
+    ST_CYCLE = 4,      // walk: more steps than k-mers in the table (no 'F' terminator)
+    ST_SPIN = 5,       // insert: gave up waiting for a half-published 16 B slot
+    ST_CHUNK_OVF = 6,  // walk: contig chunk pool exhausted (sized as an upper bound; never expected)
+    ST_NUM = 8
+};
+
+// Device counters used by the host-side orchestration.
+enum CtrIdx : int {
+    CT_N_STARTS = 0,   // start k-mers collected so far (all insert calls)
+    CT_WALK_NEXT = 1,  // walker work-queue head
+    CT_CHUNK_NEXT = 2, // chunk allocator head
+    CT_OUT_BYTES = 3,  // total contig bytes (incl. '\n')
+    CT_NUM = 8
+};
+
+// Chunk of appended bases: 8 words x 32 bases (2 bits each) = 256 bases.
+static constexpr int CHUNK_WORDS = 8;
+static constexpr int CHUNK_BASES = 256;
+
+struct TableView {
+    uint64_t* slots;   // W words per slot, cap slots
+    uint64_t cap;
+};
+
+// Insert records (reference kmer_pair layout, R bytes each, 16-B aligned base) into the table.
+// Writes one start bit per record (bwd == 'F') into start_mask[i/64].
+hipError_t launch_insert(const KParams& p, const uint8_t* recs, uint64_t n, TableView t,
+                         uint64_t* start_mask, unsigned long long* stats, hipStream_t s);
+
+// Append start k-mers of a batch, in record order, to starts (W words each) at
+// ctr[CT_N_STARTS]. scratch must hold >= scan_scratch_words(ceil(n/64)) words.
+hipError_t launch_collect_starts(const KParams& p, const uint8_t* recs, uint64_t n,
+                                 const uint64_t* start_mask, uint64_t* mask_offsets,
+                                 uint64_t* scratch, uint64_t* starts, unsigned long long* ctr,
+                                 hipStream_t s);
+
+// Explicit start list (caller's start_nodes): R-byte records -> start words, sets CT_N_STARTS.
+hipError_t launch_load_starts(const KParams& p, const uint8_t* recs, uint64_t n, uint64_t* starts,
+                              unsigned long long* ctr, hipStream_t s);
+
+// Batched find: keys are PACKED bytes each; out gets R-byte records, found 0/1.
+hipError_t launch_find(const KParams& p, const uint8_t* keys, uint64_t n, TableView t, uint8_t* out,
+                       uint8_t* found, hipStream_t s);
+
+struct WalkBuffers {
+    const uint64_t* starts;
+    uint64_t n_starts;
+    uint32_t* contig_len;     // k-mers per contig (>= 1)
+    uint64_t* chunk_data;     // chunk_cap * CHUNK_WORDS
+    uint32_t* chunk_owner;    // contig id of each chunk
+    uint32_t* chunk_seq;      // chunk index within its contig
+    uint64_t chunk_cap;
+    uint64_t max_steps;
+};
+
+// Persistent per-lane walker (single GPU): every lane walks whole contigs, pulling start k-mers
+// from a wave-batched work queue.
+hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
+                       unsigned long long* stats, int grid_blocks, hipStream_t s);
+
+// Contig bytes: offsets = exclusive scan of (K + len) (K + len-1 bases + '\n'), then write chars.
+hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
+                              uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s);
+
+// Scratch words needed by the scans for m elements.
+uint64_t scan_scratch_words(uint64_t m);
+
+}  // namespace kh

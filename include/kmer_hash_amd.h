@@ -1,0 +1,147 @@
+/* kmer_hash_amd.h — C ABI of the MI355X-native k-mer hash table + contig walker.
+ *
+ * Drop-in boundary for the hot path of fractalclockwork/CS267_HW3 (hash_map.hpp / kmer_hash.cpp).
+ * Plain C: pointers and sizes only, no C++ or torch types, no exceptions across the boundary.
+ * Every entry point returns KH_OK (0) or a negative KH_ERR_*; kh_last_error() gives a message
+ * (thread-local). A handle is not thread-safe; use one per host thread / process.
+ *
+ * Record formats (byte-identical to the reference types, align 1):
+ *   key    = pkmer_t   : PACKED = (k+3)/4 bytes, 2 bits/base MSB-first, A=0 C=1 G=2 T=3,
+ *                        'A'-padded tail                          (pkmer_t.hpp:6, packing.hpp:77-92)
+ *   record = kmer_pair : PACKED key bytes + fb_ext[2] = {backward, forward} chars in {A,C,G,T,F}
+ *                        sizeof = PACKED + 2 = 7 (k=19) / 15 (k=51)          (kmer_t.hpp:6-8,43-45)
+ *   contig text        : one contig per line, extract_contig() bytes + '\n', in start-node order
+ *                        = the bytes of test_<rank>.dat                (read_kmers.hpp:81-92,
+ *                                                                       kmer_hash.cpp:60-68)
+ * Reference entry points replaced (see INTEGRATION.md for the bindings):
+ *   kh_create      <- DistributedHashMap(size, rank, world)  hash_map.hpp:50-52; HashMap(size)
+ *   kh_insert*     <- DistributedHashMap::insert_all        hash_map.hpp:55-80; HashMap::insert
+ *                     + start-node collection               kmer_hash.cpp:21-33
+ *   kh_find*       <- DistributedHashMap::find              hash_map.hpp:83-107; HashMap::find
+ *   kh_assemble*   <- assemble_contigs                      kmer_hash.cpp:38-55
+ *   kh_contigs_*   <- extract_contig + output_results       read_kmers.hpp:81-92, kmer_hash.cpp:60-68
+ *   kh_pack_text   <- read_kmers line parsing               read_kmers.hpp:54-79
+ */
+#ifndef KMER_HASH_AMD_H
+#define KMER_HASH_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KH_ABI_VERSION 1
+#define KH_K_MAX 60
+
+enum {
+    KH_OK = 0,
+    KH_ERR_ARG = -1,        /* bad argument / unsupported k / misaligned device pointer */
+    KH_ERR_HIP = -2,        /* HIP runtime error (message has the hipError string) */
+    KH_ERR_NOMEM = -3,      /* device or host allocation failed */
+    KH_ERR_FULL = -4,       /* more k-mers than the table was created for / probe wrapped */
+    KH_ERR_NOT_FOUND = -5,  /* walk: next k-mer missing (kmer_hash.cpp:47-49 throws) */
+    KH_ERR_DUPLICATE = -6,  /* insert: key already present (input contract: unique k-mers) */
+    KH_ERR_CYCLE = -7,      /* walk: chain longer than the table (no 'F' end) */
+    KH_ERR_BAD_BASE = -8,   /* extension byte outside {A,C,G,T,F} */
+    KH_ERR_STATE = -9       /* call order (e.g. contigs requested before assemble) */
+};
+
+typedef struct kh_table kh_table;
+
+typedef struct kh_stats {
+    uint64_t capacity;       /* table slots */
+    uint64_t n_inserted;     /* records inserted since create/clear */
+    uint64_t n_starts;       /* start k-mers collected (bwd == 'F') or set explicitly */
+    uint64_t n_contigs;      /* contigs produced by the last assemble (= n_starts) */
+    uint64_t n_lookups;      /* successful walk lookups of the last assemble = sum(len - 1) */
+    uint64_t out_bytes;      /* contig text bytes of the last assemble, '\n' included */
+    uint64_t n_chunks;       /* 256-base chunks used by the walker */
+    uint64_t n_dup, n_full, n_bad_ext, n_missing, n_cycle, n_spin, n_chunk_ovf;
+    double ms_insert;        /* device ms, last insert call (table insert + start compaction) */
+    double ms_insert_kernel; /* device ms, k_insert alone, last insert call */
+    double ms_walk;          /* device ms, k_walk, last assemble */
+    double ms_materialize;   /* device ms, offsets scan + contig text, last assemble */
+} kh_stats;
+
+/* ---- sizes / info --------------------------------------------------------------------------*/
+int kh_abi_version(void);
+int kh_packed_size(int k);   /* sizeof(pkmer_t)   */
+int kh_record_size(int k);   /* sizeof(kmer_pair) */
+const char* kh_last_error(void);
+int kh_device_count(int* n);
+
+/* ---- table lifetime --------------------------------------------------------------------------
+ * Capacity = ceil(n_kmers / load_factor) slots (kmer_hash.cpp:108-109 uses load 0.5 -> 2n).
+ * Device memory: capacity * (8 B if k <= 29 else 16 B) for the table, plus walker buffers.
+ * All work is enqueued on the table's stream (its own, or one set with kh_set_stream). */
+int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int device);
+int kh_destroy(kh_table* t);
+int kh_clear(kh_table* t);                       /* empty table + start list (async) */
+int kh_set_stream(kh_table* t, void* hip_stream); /* NULL = back to the table's own stream */
+int kh_sync(kh_table* t);                        /* wait for the stream; report device errors */
+uint64_t kh_capacity(const kh_table* t);
+int kh_get_stats(kh_table* t, kh_stats* out);    /* syncs */
+
+/* ---- insert: records in kmer_pair layout. Start k-mers (bwd == 'F') of every batch are appended
+ * to the table's start list in record order (kmer_hash.cpp:27-31). --------------------------*/
+int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n);   /* synchronous */
+int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n);   /* async, 16-B aligned */
+
+/* ---- find: keys in pkmer_t layout; out gets kmer_pair records, found[i] = 0/1 ----------------*/
+int kh_find(kh_table* t, const uint8_t* host_keys, uint64_t n, uint8_t* host_recs_out,
+            uint8_t* host_found);
+int kh_find_dev(kh_table* t, const void* dev_keys, uint64_t n, void* dev_recs_out,
+                void* dev_found);
+
+/* ---- assemble --------------------------------------------------------------------------------
+ * Walks every start k-mer (collected by the inserts, or replaced by kh_set_starts) until its
+ * forward extension is 'F', producing the contig text in start-node order on the device. */
+int kh_set_starts(kh_table* t, const uint8_t* host_start_recs, uint64_t n);
+int kh_assemble_dev(kh_table* t);                 /* async */
+int kh_assemble(kh_table* t, uint64_t* n_contigs, uint64_t* out_bytes);  /* sync + checks */
+int kh_contigs_text(kh_table* t, char* host_out, uint64_t cap);          /* D2H of the text */
+int kh_contigs_text_dev(kh_table* t, const char** dev_text, uint64_t* bytes);
+int kh_contigs_offsets(kh_table* t, uint64_t* host_offsets, uint64_t n); /* line starts */
+
+/* ---- device memory helpers (for hosts without an allocator of their own) --------------------*/
+int kh_dev_malloc(void** p, uint64_t bytes, int device);
+int kh_dev_free(void* p);
+int kh_memcpy_htod(void* dst, const void* src, uint64_t bytes);
+int kh_memcpy_dtoh(void* dst, const void* src, uint64_t bytes);
+
+/* ---- host codec helpers --------------------------------------------------------------------*/
+/* read_kmers.hpp:62-76: fixed-width "KMER BF\n" lines (k+4 bytes) -> kmer_pair records. */
+int kh_pack_text(int k, const char* text, uint64_t len, uint8_t* recs_out, uint64_t* n_out);
+/* packing.hpp:77-107 */
+int kh_pack_kmer(int k, const char* kmer, uint8_t* packed_out);
+int kh_unpack_kmer(int k, const uint8_t* packed, char* kmer_out);
+/* pkmer_t.hpp:31-37 djb2 (API parity; the table places keys with its own mixer) */
+uint64_t kh_djb2(int k, const uint8_t* packed);
+/* kmer_t.hpp:51-53 next_kmer of a record, as packed bytes */
+int kh_next_kmer(int k, const uint8_t* rec, uint8_t* packed_out);
+
+/* ---- synthetic dataset generator ------------------------------------------
+ * n k-mers cut from independent uniform-random contigs of len_min..len_max k-mers (plus
+ * single_permille / 1000 single-k-mer contigs), every k-mer unique (contigs containing a repeated
+ * k-mer are re-drawn), records shuffled by a seeded bijection. Deterministic in all arguments
+ * except `threads`. */
+typedef struct kh_gen kh_gen;
+int kh_gen_create(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
+                  uint32_t single_permille, uint64_t seed, int shuffle, int threads);
+int kh_gen_destroy(kh_gen* g);
+uint64_t kh_gen_num_contigs(const kh_gen* g);
+/* records at output positions [pos_begin, pos_end) in kmer_pair layout (block split of
+ * read_kmers.hpp:55-58 = positions [r*ceil(n/P), ...)) */
+int kh_gen_records(const kh_gen* g, uint64_t pos_begin, uint64_t pos_end, uint8_t* out);
+/* ground-truth contig text of the contigs whose start k-mer lies in [pos_begin, pos_end), in
+ * start-node order (= expected test_<rank>.dat bytes); bytes_out gets the size. out may be NULL
+ * to query the size. */
+int kh_gen_truth(const kh_gen* g, uint64_t pos_begin, uint64_t pos_end, char* out, uint64_t cap,
+                 uint64_t* bytes_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMER_HASH_AMD_H */

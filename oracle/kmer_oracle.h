@@ -1,0 +1,55 @@
+/* kmer_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference's serial k-mer path (fractalclockwork/CS267_HW3) used as
+ * the parity CHECKER for the HIP product. Nothing in cs267_hw3_amd/ links or calls this code;
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may.
+ *
+ * Pinned by: (1) the codec KATs produced by compiling the reference's own packing.hpp /
+ * pkmer_t.hpp / kmer_t.hpp / read_kmers.hpp (oracle/ref_harness.cpp -> oracle/_ref/), committed
+ * as tests/golden/kat.json; (2) golden contig files produced by that reference-codec harness on
+ * committed inputs (tests/golden/*.txt -> *_test_0.dat). See DESIGN.md "Oracle".
+ */
+#ifndef KMER_ORACLE_H
+#define KMER_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* packing.hpp:77-92 packKmer: K chars -> (K+3)/4 bytes, MSB-first, 'A'-padded tail. */
+void ko_pack(int K, const char* kmer, uint8_t* packed);
+/* packing.hpp:94-107 unpackKmer, but writes exactly K chars (no 1-byte overflow). */
+void ko_unpack(int K, const uint8_t* packed, char* kmer);
+/* pkmer_t.hpp:31-37 djb2 over the packed bytes. */
+uint64_t ko_djb2(int K, const uint8_t* packed);
+/* kmer_t.hpp:51-53 next_kmer via the string round trip: kmer[1:] + fwd, repacked. */
+void ko_next_kmer(int K, const uint8_t* rec, uint8_t* next_packed);
+
+/* read_kmers.hpp:54-79 fixed-width lines "KMER BF\n" (K+4 bytes) -> kmer_pair records
+ * (P packed bytes + fb_ext[2]). Returns number of records parsed. */
+size_t ko_parse_text(int K, const char* text, size_t len, uint8_t* recs);
+
+/* Serial assembly with the upstream stock HashMap semantics (README.md:95,99; restated by
+ * test/distributed_hashmap_test.cpp:34-65): slot = (djb2 + probe) % (2n), linear probing.
+ * kmer_hash.cpp:21-55 control flow: insert all, collect start nodes (bwd=='F') in input order,
+ * walk each until fwd=='F'. Output: contigs (read_kmers.hpp:81-92 extract_contig) joined by '\n'
+ * in start-node order = the bytes of test_0.dat (kmer_hash.cpp:60-68).
+ * Returns 0 on success, -1 missing k-mer, -2 table full, -3 cycle guard, -4 alloc.
+ * *out is malloc'd; caller frees with ko_free. */
+int ko_assemble(int K, const uint8_t* recs, size_t n, char** out, size_t* out_len,
+                size_t* n_contigs, size_t* n_lookups, double* t_insert, double* t_walk);
+void ko_free(void* p);
+
+/* Stock table, exposed for find()/insert() unit parity. */
+typedef struct ko_table ko_table;
+ko_table* ko_table_new(int K, size_t size);
+void ko_table_free(ko_table* t);
+int ko_table_insert(ko_table* t, const uint8_t* rec);               /* 1 ok, 0 full */
+int ko_table_find(const ko_table* t, const uint8_t* key, uint8_t* rec); /* 1 found, 0 not */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

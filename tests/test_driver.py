@@ -1,0 +1,42 @@
+"""The drop-in C++ driver (tools/kmer_hash_<K>) reproduces the reference's test_<rank>.dat and
+stdout contract (kmer_hash.cpp:60-79,143-148), and check_it.sh's sort-and-diff passes."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,k", [("tiny19", 19), ("verysmall19", 19), ("small51", 51)])
+def test_driver_test_mode(tmp_path, name, k):
+    exe = os.path.join(ROOT, "tools", f"kmer_hash_{k}")
+    r = subprocess.run([exe, os.path.join(GOLDEN, f"{name}.txt"), "test", "out"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = open(tmp_path / "out_0.dat", "rb").read()
+    want = open(os.path.join(GOLDEN, f"{name}_test_0.dat"), "rb").read()
+    assert got == want
+    assert sorted(got.splitlines()) == sorted(want.splitlines())  # check_it.sh semantics
+
+
+@pytest.mark.gpu
+def test_driver_timing_lines(tmp_path):
+    exe = os.path.join(ROOT, "tools", "kmer_hash_19")
+    r = subprocess.run([exe, os.path.join(GOLDEN, "mixed19.txt")], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0].startswith("Finished inserting in ") and lines[0].endswith(" sec")
+    assert lines[1].startswith("Assembled in ") and lines[1].endswith(" total")
+
+
+def test_driver_rejects_wrong_k(tmp_path):
+    exe = os.path.join(ROOT, "tools", "kmer_hash_51")
+    if not os.path.exists(exe):
+        pytest.skip("driver not built")
+    r = subprocess.run([exe, os.path.join(GOLDEN, "tiny19.txt")], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "19-mers" in r.stderr

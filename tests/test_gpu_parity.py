@@ -1,0 +1,193 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference-harness golden files, the
+oracle, and the generator's ground truth. Integer/byte work -> every comparison is bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cs267_hw3_amd as kh
+from cs267_hw3_amd import _lib
+import oracle_bind as ob
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+
+
+def golden(name):
+    m = MANIFEST[name]
+    recs = kh.pack_text(m["k"], open(os.path.join(GOLDEN, f"{name}.txt"), "rb").read())
+    want = open(os.path.join(GOLDEN, f"{name}_test_0.dat"), "rb").read()
+    return m["k"], recs, want
+
+
+def run(k, recs, batches=1, load=0.5, n_kmers=None):
+    t = kh.KmerHashTable(k, n_kmers if n_kmers is not None else max(len(recs), 1), load)
+    for part in np.array_split(recs, batches):
+        t.insert_all(part)
+    nc, nb = t.assemble()
+    text = t.contigs_text()
+    assert len(text) == nb
+    return t, text, nc
+
+
+def test_device_present():
+    assert kh.device_count() >= 1
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_golden_byte_identical(name):
+    k, recs, want = golden(name)
+    t, got, nc = run(k, recs)
+    assert got == want                          # test_0.dat bytes, start-node order
+    s = t.stats()
+    assert nc == MANIFEST[name]["contigs"] == s["n_contigs"] == s["n_starts"]
+    assert s["n_lookups"] == len(recs) - nc
+    assert s["n_inserted"] == len(recs)
+    assert s["n_dup"] == s["n_missing"] == s["n_full"] == s["n_bad_ext"] == 0
+
+
+@pytest.mark.parametrize("name", ["mixed19", "small51", "k32"])
+@pytest.mark.parametrize("batches", [2, 7])
+def test_multi_batch_insert_keeps_start_order(name, batches):
+    k, recs, want = golden(name)
+    _, got, _ = run(k, recs, batches=batches)
+    assert got == want
+
+
+@pytest.mark.parametrize("load", [0.25, 0.7, 0.95])
+def test_load_factor_does_not_change_output(load):
+    k, recs, want = golden("small51")
+    _, got, _ = run(k, recs, load=load)
+    assert got == want
+
+
+@pytest.mark.parametrize("name", ["mixed19", "small51", "k29", "k30", "k60"])
+def test_find_matches_oracle(name):
+    k, recs, _ = golden(name)
+    t = kh.KmerHashTable(k, len(recs))
+    t.insert_all(recs)
+    P = (k + 3) // 4
+    rng = np.random.default_rng(5)
+    present = recs[rng.choice(len(recs), 500, replace=False)]
+    got, found = t.find(present[:, :P])
+    assert found.all() and np.array_equal(got, present)
+    # absent keys: random k-mers checked against the oracle's stock table
+    ot = ob.Table(k, 2 * len(recs))
+    for r in recs:
+        ot.insert(r)
+    bases = "ACGT"
+    absent = np.stack([kh.pack_kmer(k, "".join(bases[x] for x in rng.integers(0, 4, k)))
+                       for _ in range(300)])
+    got, found = t.find(absent)
+    for i in range(len(absent)):
+        ok, rec = ot.find(absent[i])
+        assert found[i] == ok
+        if ok:
+            assert np.array_equal(got[i], rec)
+    assert np.all(got[~found] == 0)
+
+
+def test_explicit_start_list():
+    # assemble_contigs(hashmap, start_nodes) with a caller-supplied start list (kmer_hash.cpp:38)
+    k, recs, want = golden("mixed19")
+    t = kh.KmerHashTable(k, len(recs))
+    t.insert_all(recs)
+    starts = recs[recs[:, (k + 3) // 4] == ord("F")]
+    t.set_starts(starts[::-1])
+    t.assemble()
+    assert t.contigs_text().splitlines() == want.splitlines()[::-1]
+
+
+def test_empty_table():
+    t = kh.KmerHashTable(19, 0)
+    assert t.assemble() == (0, 0)
+    assert t.contigs_text() == b""
+    t.insert_all(np.zeros((0, 7), np.uint8))
+    assert t.assemble() == (0, 0)
+
+
+def test_clear_and_reuse():
+    k, recs, want = golden("small51")
+    t = kh.KmerHashTable(k, len(recs))
+    for _ in range(3):
+        t.clear()
+        t.insert_all(recs)
+        t.assemble()
+        assert t.contigs_text() == want
+
+
+def test_missing_kmer_raises():
+    k, recs, _ = golden("tiny19")
+    P = (k + 3) // 4
+    interior = np.where((recs[:, P] != ord("F")) & (recs[:, P + 1] != ord("F")))[0][10]
+    t = kh.KmerHashTable(k, len(recs))
+    t.insert_all(np.delete(recs, interior, axis=0))
+    with pytest.raises(kh.KmerHashError) as e:
+        t.assemble()
+    assert e.value.code == _lib.KH_ERR_NOT_FOUND
+
+
+def test_duplicate_insert_is_reported():
+    k, recs, _ = golden("small51")
+    t = kh.KmerHashTable(k, 2 * len(recs))
+    t.insert_all(recs)
+    with pytest.raises(kh.KmerHashError) as e:
+        t.insert_all(recs[:10])
+    assert e.value.code == _lib.KH_ERR_DUPLICATE
+
+
+def test_overfill_is_reported():
+    k, recs, _ = golden("small51")
+    t = kh.KmerHashTable(k, len(recs) - 1)
+    with pytest.raises(kh.KmerHashError) as e:
+        t.insert_all(recs)
+    assert e.value.code == _lib.KH_ERR_FULL
+
+
+def test_bad_extension_is_reported():
+    k, recs, _ = golden("mixed19")
+    recs = recs.copy()
+    recs[3, (k + 3) // 4 + 1] = ord("N")
+    t = kh.KmerHashTable(k, len(recs))
+    with pytest.raises(kh.KmerHashError) as e:
+        t.insert_all(recs)
+    assert e.value.code == _lib.KH_ERR_BAD_BASE
+
+
+@pytest.mark.parametrize("k,n,lmin,lmax,single,seed", [
+    (19, 1_000_000, 200, 1374, 0, 19),        # C2-like length mix, reduced n
+    (51, 1_000_000, 8, 200, 10, 51),          # C3-like length mix, reduced n
+    (31, 300_000, 1, 500, 50, 31),
+    (45, 300_000, 1, 500, 50, 45),
+])
+def test_generated_vs_oracle(k, n, lmin, lmax, single, seed):
+    g = kh.SyntheticKmers(k, n, lmin, lmax, single, seed=seed)
+    recs = g.records()
+    rc, want, nc, nl, _, _ = ob.assemble(k, recs)
+    assert rc == 0
+    _, got, gnc = run(k, recs)
+    assert got == want and gnc == nc
+
+
+def test_c2_full_size_vs_truth():
+    # BASELINE configs[1]: k=19, 10M synthetic k-mers, bit-exact (vs generator ground truth,
+    # which the oracle matches at every smaller size above)
+    g = kh.SyntheticKmers(19, 10_000_000, 200, 1374, 0, seed=19)
+    recs = g.records()
+    t, got, nc = run(19, recs)
+    assert nc == g.num_contigs
+    assert got == g.truth()
+    s = t.stats()
+    assert s["n_lookups"] == 10_000_000 - nc
+
+
+def test_c3_shape_vs_truth_30m():
+    # configs[2] shape (k=51, U[8,200]) at 30M k-mers: byte-identical to the ground truth
+    g = kh.SyntheticKmers(51, 30_000_000, 8, 200, 0, seed=51)
+    recs = g.records()
+    _, got, nc = run(51, recs)
+    assert nc == g.num_contigs
+    assert got == g.truth()

@@ -1,0 +1,71 @@
+"""The oracle (oracle/kmer_oracle.c) pinned against the reference's own codec and I/O.
+
+Golden vectors were produced by oracle/_ref/ref_harness_<K>, compiled from the reference's
+packing.hpp / pkmer_t.hpp / kmer_t.hpp / read_kmers.hpp (tests/golden/make_golden.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KAT = json.load(open(os.path.join(GOLDEN, "kat.json")))
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+
+
+@pytest.mark.parametrize("v", KAT, ids=[f"k{v['k']}-{v['kmer'][:8]}-{v['fb']}" for v in KAT])
+def test_oracle_codec_kat(v):
+    k = v["k"]
+    p = ob.pack(k, v["kmer"])
+    assert p.tobytes().hex() == v["packed"]               # packing.hpp:77-92
+    assert ob.unpack(k, p) == v["kmer"]                   # packing.hpp:94-107
+    assert ob.djb2(k, p) == v["djb2"]                     # pkmer_t.hpp:31-37
+    if v["next"] is not None:                             # kmer_t.hpp:51-53
+        rec = np.concatenate([p, np.frombuffer(v["fb"].encode(), np.uint8)])
+        assert ob.next_kmer(k, rec).tobytes().hex() == v["next"]
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_oracle_assembly_matches_reference_harness(name):
+    m = MANIFEST[name]
+    k = m["k"]
+    text = open(os.path.join(GOLDEN, f"{name}.txt"), "rb").read()
+    want = open(os.path.join(GOLDEN, f"{name}_test_0.dat"), "rb").read()
+    recs = ob.parse_text(k, text)
+    assert recs.shape[0] == m["n"]
+    rc, got, nc, nl, _, _ = ob.assemble(k, recs)
+    assert rc == 0
+    assert got == want                                    # byte-identical test_0.dat
+    assert nc == m["contigs"]
+    assert nl == m["n"] - m["contigs"]                    # every k-mer is in exactly one contig
+
+
+def test_oracle_table_find_absent_and_present():
+    k = 19
+    text = open(os.path.join(GOLDEN, "mixed19.txt"), "rb").read()
+    recs = ob.parse_text(k, text)
+    t = ob.Table(k, 2 * len(recs))
+    for r in recs:
+        assert t.insert(r)
+    for r in recs[::37]:
+        ok, got = t.find(r[:5])
+        assert ok and bytes(got) == bytes(r)
+    ok, _ = t.find(ob.pack(k, "A" * 19))
+    assert not ok or bytes(_)[:5] == bytes(ob.pack(k, "A" * 19))
+
+
+def test_oracle_missing_kmer_is_an_error():
+    k = 19
+    recs = ob.parse_text(k, open(os.path.join(GOLDEN, "tiny19.txt"), "rb").read())
+    # drop one interior k-mer: the walk must fail like kmer_hash.cpp:47-49
+    interior = [i for i, r in enumerate(recs) if r[5] != ord("F") and r[6] != ord("F")][0]
+    rc = ob.assemble(k, np.delete(recs, interior, axis=0))[0]
+    assert rc == -1
+
+
+def test_oracle_empty_input():
+    rc, text, nc, nl, _, _ = ob.assemble(19, np.zeros((0, 7), np.uint8))
+    assert rc == 0 and text == b"" and nc == 0 and nl == 0
