@@ -63,6 +63,15 @@ _SIGS = {
     "kh_contigs_text": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_contigs_text_dev": (ctypes.c_int, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_u64)]),
     "kh_contigs_offsets": (ctypes.c_int, [c_vp, c_vp, c_u64]),
+    "kh_word_count": (ctypes.c_int, [ctypes.c_int]),
+    "kh_collect_starts_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
+    "kh_route_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.c_int, c_vp, c_vp]),
+    "kh_insert_words_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
+    "kh_walk_begin": (ctypes.c_int, [c_vp, c_u64, ctypes.POINTER(c_u64)]),
+    "kh_walk_emit_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp]),
+    "kh_find_ext_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp]),
+    "kh_walk_apply_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
+    "kh_walk_end_dev": (ctypes.c_int, [c_vp]),
     "kh_dev_malloc": (ctypes.c_int, [ctypes.POINTER(c_vp), c_u64, ctypes.c_int]),
     "kh_dev_free": (ctypes.c_int, [c_vp]),
     "kh_memcpy_htod": (ctypes.c_int, [c_vp, c_vp, c_u64]),

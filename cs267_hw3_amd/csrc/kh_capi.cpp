@@ -83,6 +83,10 @@ struct kh_table {
     DevBuf stage;                            // host-API staging of records / keys
     DevBuf stage2, stage3;
     DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text;
+    DevBuf route_hist, route_off, route_scratch;                          // sharded path
+    DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm;   // round walker
+    uint64_t rw_n = 0, rw_total = 0;
+    bool rw_live = false;
     uint64_t starts_cap = 0;                 // start entries the starts buffer holds
     uint64_t chunk_cap = 0;
 
@@ -213,7 +217,9 @@ int kh_destroy(kh_table* t) {
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     DevBuf* bufs[] = {&t->slots, &t->starts, &t->ctr, &t->stats, &t->mask, &t->mask_off,
                       &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
-                      &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text};
+                      &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
+                      &t->route_hist, &t->route_off, &t->route_scratch, &t->rw_hi, &t->rw_lo,
+                      &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm};
     for (auto* b : bufs) b->release();
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1};
     for (auto ev : evs)
@@ -480,4 +486,184 @@ int kh_memcpy_dtoh(void* dst, const void* src, uint64_t bytes) {
     return KH_OK;
 }
 
+// ---- sharded multi-GPU path -------------------------------------------------------------------
+int kh_word_count(int k) { return (k >= 1 && k <= KH_K_MAX) ? kh::make_params(k).W : KH_ERR_ARG; }
+
+namespace {
+int ensure_route(kh_table* t, uint64_t n, int nranks) {
+    const uint64_t m = kh::route_blocks(n) * (uint64_t)nranks + 1;
+    int rc;
+    if ((rc = t->route_hist.ensure(m * 8))) return rc;
+    if ((rc = t->route_off.ensure(m * 8))) return rc;
+    if ((rc = t->route_scratch.ensure((kh::scan_scratch_words(m) + 2) * 8))) return rc;
+    return KH_OK;
+}
+
+kh::RoundWalk round_walk(kh_table* t) {
+    kh::RoundWalk rw;
+    rw.n = t->rw_n;
+    rw.hi = t->rw_hi.as<uint64_t>();
+    rw.lo = t->rw_lo.as<uint64_t>();
+    rw.buf = t->rw_buf.as<uint64_t>();
+    rw.steps = t->rw_steps.as<uint32_t>();
+    rw.chunk = t->rw_chunk.as<uint32_t>();
+    rw.state = t->rw_state.as<uint8_t>();
+    rw.qperm = t->rw_qperm.as<uint32_t>();
+    rw.contig_len = t->contig_len.as<uint32_t>();
+    rw.chunk_data = t->chunk_data.as<uint64_t>();
+    rw.chunk_owner = t->chunk_owner.as<uint32_t>();
+    rw.chunk_seq = t->chunk_seq.as<uint32_t>();
+    rw.chunk_cap = t->chunk_cap;
+    rw.max_steps = t->rw_total;
+    return rw;
+}
+}  // namespace
+
+int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (n == 0) return KH_OK;
+    if (!dev_recs) return fail(KH_ERR_ARG, "null records");
+    if (int rc = set_device(t)) return rc;
+    int rc;
+    const uint64_t nw = (n + 63) / 64;
+    if ((rc = t->mask.ensure(nw * 8))) return rc;
+    if ((rc = t->mask_off.ensure(nw * 8))) return rc;
+    if ((rc = t->scratch.ensure(kh::scan_scratch_words(nw) * 8 + 64))) return rc;
+    uint64_t have = 0;
+    if ((rc = read_ctr(t, kh::CT_N_STARTS, &have))) return rc;
+    if ((rc = ensure_starts(t, have + n))) return rc;
+    KH_HIP(kh::launch_start_mask(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(), t->stream));
+    KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
+                                     t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                     t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(),
+                                     t->stream));
+    t->assembled = false;
+    return KH_OK;
+}
+
+int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* words_out,
+                 void* counts_out) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
+    if (!counts_out || (n && (!dev_recs || !words_out))) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, n, nranks)) return rc;
+    KH_HIP(kh::launch_route(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks,
+                            t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
+                            t->route_scratch.as<uint64_t>(), (uint64_t*)words_out,
+                            (uint64_t*)counts_out, t->stream));
+    return KH_OK;
+}
+
+int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (m == 0) return KH_OK;
+    if (!words) return fail(KH_ERR_ARG, "null words");
+    if (t->n_inserted + m > t->n_kmers)
+        return fail(KH_ERR_FULL, "inserting %llu k-mers into a shard created for %llu (%llu in)",
+                    (unsigned long long)m, (unsigned long long)t->n_kmers,
+                    (unsigned long long)t->n_inserted);
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
+    KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
+                                   t->stats.as<unsigned long long>(), t->stream));
+    KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
+    KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
+    t->ins_timed = true;
+    t->n_inserted += m;
+    t->assembled = false;
+    return KH_OK;
+}
+
+int kh_walk_begin(kh_table* t, uint64_t total_kmers, uint64_t* n_walkers) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (int rc = set_device(t)) return rc;
+    int rc;
+    uint64_t ns = 0;
+    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
+    const uint64_t tot = total_kmers > ns ? total_kmers : ns;
+    const uint64_t chunk_cap = tot / kh::CHUNK_BASES + ns + 64;
+    if ((rc = t->contig_len.ensure((ns + 1) * 4))) return rc;
+    if ((rc = t->contig_off.ensure((ns + 1) * 8))) return rc;
+    if ((rc = t->chunk_data.ensure(chunk_cap * kh::CHUNK_WORDS * 8))) return rc;
+    if ((rc = t->chunk_owner.ensure(chunk_cap * 4))) return rc;
+    if ((rc = t->chunk_seq.ensure(chunk_cap * 4))) return rc;
+    if ((rc = t->text.ensure(tot + ns * ((uint64_t)t->kp.K + 1) + 64))) return rc;
+    if ((rc = t->scratch.ensure(kh::scan_scratch_words(ns) * 8 + 64))) return rc;
+    const uint64_t nn = ns + 1;
+    if ((rc = t->rw_hi.ensure(nn * 8)) || (rc = t->rw_lo.ensure(nn * 8)) || (rc = t->rw_buf.ensure(nn * 8)) ||
+        (rc = t->rw_steps.ensure(nn * 4)) || (rc = t->rw_chunk.ensure(nn * 4)) ||
+        (rc = t->rw_state.ensure(nn)) || (rc = t->rw_qperm.ensure(nn * 4)))
+        return rc;
+    t->chunk_cap = chunk_cap;
+    t->rw_n = ns;
+    t->rw_total = tot;
+    KH_HIP(hipMemsetAsync(t->ctr.as<unsigned long long>() + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));
+    KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
+    KH_HIP(kh::launch_rw_init(t->kp, round_walk(t), t->starts.as<uint64_t>(), t->stream));
+    t->rw_live = true;
+    t->assembled = false;
+    if (n_walkers) *n_walkers = ns;
+    return KH_OK;
+}
+
+int kh_walk_emit_dev(kh_table* t, int nranks, void* keys_out, void* counts_out) {
+    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
+    if (!counts_out || (t->rw_n && !keys_out)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, t->rw_n, nranks)) return rc;
+    KH_HIP(kh::launch_rw_emit(t->kp, round_walk(t), (uint32_t)nranks, t->route_hist.as<uint64_t>(),
+                              t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(),
+                              (uint64_t*)keys_out, (uint64_t*)counts_out,
+                              t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(),
+                              t->stream));
+    return KH_OK;
+}
+
+int kh_find_ext_dev(kh_table* t, const void* keys, uint64_t m, void* ext_out) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (m == 0) return KH_OK;
+    if (!keys || !ext_out) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_find_ext(t->kp, (const uint64_t*)keys, m, view(t), (uint8_t*)ext_out, t->stream));
+    return KH_OK;
+}
+
+int kh_walk_apply_dev(kh_table* t, const void* ext, uint64_t m) {
+    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
+    if (m == 0) return KH_OK;
+    if (!ext) return fail(KH_ERR_ARG, "null replies");
+    if (m > t->rw_n) return fail(KH_ERR_ARG, "%llu replies for %llu walkers", (unsigned long long)m,
+                                 (unsigned long long)t->rw_n);
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_rw_apply(t->kp, round_walk(t), (const uint8_t*)ext, m,
+                               t->stats.as<unsigned long long>(), t->stream));
+    return KH_OK;
+}
+
+int kh_walk_end_dev(kh_table* t) {
+    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
+    if (int rc = set_device(t)) return rc;
+    kh::WalkBuffers wb;
+    wb.starts = t->starts.as<uint64_t>();
+    wb.n_starts = t->rw_n;
+    wb.contig_len = t->contig_len.as<uint32_t>();
+    wb.chunk_data = t->chunk_data.as<uint64_t>();
+    wb.chunk_owner = t->chunk_owner.as<uint32_t>();
+    wb.chunk_seq = t->chunk_seq.as<uint32_t>();
+    wb.chunk_cap = t->chunk_cap;
+    wb.max_steps = t->rw_total;
+    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
+    KH_HIP(kh::launch_materialize(t->kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                  t->text.as<char>(), t->ctr.as<unsigned long long>(), t->stream));
+    KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
+    t->walk_timed = true;
+    t->last_contigs = t->rw_n;
+    t->assembled = true;
+    t->rw_live = false;
+    return KH_OK;
+}
+
 }  // extern "C"
+

@@ -181,15 +181,24 @@ struct kh_gen {
     std::vector<uint32_t> salt;  // re-draw counter per contig (uniqueness)
     Perm perm;
 
-    uint32_t base(uint64_t i, uint64_t j) const {
-        const uint64_t w = splitmix(splitmix(seed ^ 0x6a09e667f3bcc908ull ^ (i * 0x9e3779b97f4a7c15ull)) ^
-                                    ((uint64_t)salt[i] << 40) ^ (j >> 5));
-        return (uint32_t)(w >> (2 * (j & 31))) & 3u;
+    // 32 bases of contig i per 64-bit word: base j = bits 2(j%32).. of word(i, j/32).
+    uint64_t word(uint64_t i, uint64_t b) const {
+        return splitmix(splitmix(seed ^ 0x6a09e667f3bcc908ull ^ (i * 0x9e3779b97f4a7c15ull)) ^
+                        ((uint64_t)salt[i] << 40) ^ b);
     }
+    uint32_t base(uint64_t i, uint64_t j) const { return (uint32_t)(word(i, j >> 5) >> (2 * (j & 31))) & 3u; }
     // k-mer t of contig i as (hi, lo) plus the ext code.
     void kmer(uint64_t i, uint64_t t, kh::Key& k, uint32_t& ext) const {
         unsigned __int128 V = 0;
-        for (int q = 0; q < K; ++q) V = (V << 2) | base(i, t + q);
+        uint64_t wb = ~0ull, w = 0;
+        for (int q = 0; q < K; ++q) {
+            const uint64_t j = t + q;
+            if ((j >> 5) != wb) {
+                wb = j >> 5;
+                w = word(i, wb);
+            }
+            V = (V << 2) | ((w >> (2 * (j & 31))) & 3u);
+        }
         k.lo = (uint64_t)V & kh::LO_MASK;
         k.hi = (uint64_t)(V >> 62);
         const uint32_t bwd = t == 0 ? kh::EXT_F : base(i, t - 1);
@@ -354,7 +363,11 @@ int kh_gen_truth(const kh_gen* g, uint64_t pb, uint64_t pe, char* out, uint64_t 
             const uint64_t i = sel[s].second;
             char* d = out + o[s];
             const uint64_t nb = g->len[i] + (uint64_t)g->K - 1;
-            for (uint64_t j = 0; j < nb; ++j) d[j] = (char)kh::code_char(g->base(i, j));
+            uint64_t w = 0;
+            for (uint64_t j = 0; j < nb; ++j) {
+                if ((j & 31) == 0) w = g->word(i, j >> 5);
+                d[j] = (char)kh::code_char((uint32_t)(w >> (2 * (j & 31))) & 3u);
+            }
             d[nb] = '\n';
         }
     });

@@ -150,6 +150,22 @@ static hipError_t scan_exclusive(F f, uint64_t m, uint64_t* out, uint64_t* scrat
 // can decide; it re-reads word1 with an atomic (coherent across XCD L2s) on its next loop
 // iteration — never spinning inside the branch, so a writer lane in the same wave always
 // completes its store first.
+// Probing reads slots with plain loads and spends an atomic only on a slot that looked EMPTY
+// (a stale EMPTY just makes the CAS fail and return the live word; a live word never changes,
+// so a plain read of one is never wrong). Word1 is published with a write-through (sc1) store.
+template <int W>
+__device__ __forceinline__ void load_slot(const uint64_t* slots, uint64_t s, uint64_t& w0,
+                                          uint64_t& w1) {
+    if (W == 2) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(slots + 2 * s);
+        w0 = v.x;
+        w1 = v.y;
+    } else {
+        w0 = slots[s];
+        w1 = 0;
+    }
+}
+
 template <int W>
 __device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p, uint64_t* slots,
                                            uint64_t cap, unsigned long long* stats) {
@@ -159,27 +175,34 @@ __device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p
     uint64_t s = home_slot(key_hash(k), cap);
     uint64_t probes = 0;
     uint32_t spins = 0;
+    uint64_t c0, c1;
+    load_slot<W>(slots, s, c0, c1);
     while (true) {
-        const unsigned long long old = atomicCAS(&S[W * s], (unsigned long long)EMPTY, w0);
-        if (old == EMPTY) {
-            if (W == 2) atomicExch(&S[2 * s + 1], w1);
-            return;
+        if (c0 == EMPTY) {
+            const unsigned long long old = atomicCAS(&S[W * s], (unsigned long long)EMPTY, w0);
+            if (old == EMPTY) {
+                if (W == 2)
+                    __hip_atomic_store(&S[2 * s + 1], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            c0 = old;
+            c1 = EMPTY;  // unknown: re-read coherently below if needed
         }
-        if ((old >> 6) == (w0 >> 6)) {
+        if ((c0 >> 6) == (w0 >> 6)) {
             if (W == 1) {
                 atomicAdd(&stats[ST_DUP], 1ull);
                 return;
             }
-            const unsigned long long o1 =
-                atomicCAS(&S[2 * s + 1], (unsigned long long)EMPTY, (unsigned long long)EMPTY);
-            if (o1 == EMPTY) {
+            if (c1 == EMPTY)
+                c1 = atomicCAS(&S[2 * s + 1], (unsigned long long)EMPTY, (unsigned long long)EMPTY);
+            if (c1 == EMPTY) {
                 if (++spins > (1u << 26)) {
                     atomicAdd(&stats[ST_SPIN], 1ull);
                     return;
                 }
-                continue;  // word1 not yet published: retry this slot next iteration
+                continue;  // word1 not yet published: re-read it on the next iteration
             }
-            if (o1 == w1) {
+            if (c1 == w1) {
                 atomicAdd(&stats[ST_DUP], 1ull);
                 return;
             }
@@ -189,6 +212,7 @@ __device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p
             return;
         }
         s = (s + 1 == cap) ? 0 : s + 1;
+        load_slot<W>(slots, s, c0, c1);
     }
 }
 
@@ -311,25 +335,22 @@ hipError_t launch_load_starts(const KParams& p, const uint8_t* recs, uint64_t n,
 
 // ---------------------------------------------------------------------------------------------
 // Probe: returns true and the slot's word0 if the key is present. Table is read-only here
-// (written by an earlier kernel), so plain 8/16-byte loads are coherent.
+// (written by an earlier kernel), so plain 8/16-byte loads are coherent. Both words feed the
+// hit test unconditionally so the compiler keeps ONE dwordx4 per probe (a short-circuit on
+// word0 made it split the slot into two dependent dwordx2 round trips).
 template <int W>
 __device__ __forceinline__ bool probe(Key k, const KParams& p, const uint64_t* __restrict__ slots,
                                       uint64_t cap, uint64_t& w0_out) {
     uint64_t s = home_slot(key_hash(k), cap);
     const uint64_t want0 = (W == 1) ? k.lo : k.hi;
     for (uint64_t probes = 0; probes < cap; ++probes) {
-        uint64_t w0, w1 = 0;
-        if (W == 2) {
-            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(slots + 2 * s);
-            w0 = v.x;
-            w1 = v.y;
-        } else {
-            w0 = slots[s];
-        }
-        if (w0 == EMPTY) return false;
-        if ((w0 >> 6) == want0 && (W == 1 || w1 == k.lo)) {
+        uint64_t w0, w1;
+        load_slot<W>(slots, s, w0, w1);
+        const bool empty = w0 == EMPTY;
+        const bool hit = !empty & ((w0 >> 6) == want0) & ((W == 1) | (w1 == k.lo));
+        if (hit | empty) {
             w0_out = w0;
-            return true;
+            return hit;
         }
         s = (s + 1 == cap) ? 0 : s + 1;
     }
@@ -368,102 +389,169 @@ hipError_t launch_find(const KParams& p, const uint8_t* keys, uint64_t n, TableV
 
 // ---------------------------------------------------------------------------------------------
 // Walker (kmer_hash.cpp:41-53). Each lane owns one contig at a time: append the forward base,
-// shift it into the key (next_kmer), probe, repeat until fwd == 'F'. Finished lanes refill from
-// a work queue that the wave pulls WALK_GRAB start k-mers at a time (one atomic per pull instead
-// of one per contig). Appended bases are packed 2 bits each into 256-base chunks allocated on
-// demand; k_write_chunks turns them into characters at the contig's final offset.
+// shift it into the key (next_kmer), probe, repeat until fwd == 'F'.
+//
+// The loop is a per-lane state machine that issues exactly ONE table load per lane per
+// iteration: a lane whose probe hit an occupied foreign slot simply probes the next slot on the
+// next iteration instead of looping inside the wave (which made every lane wait for the longest
+// probe chain in its wave). Finished lanes refill from a work queue the wave pulls WALK_GRAB start
+// k-mers at a time; the batch's start records are preloaded one per lane with a coalesced load
+// and handed out by shuffle, so refilling costs no dependent memory round trip. Appended bases are
+// packed 2 bits each into 256-base chunks; k_write_chunks turns them into characters at the
+// contig's final offset. Contig c owns chunk c outright (its first 256 bases); only longer contigs
+// draw further chunks from a counter, so contig starts never contend on one atomic word (a
+// per-contig atomicAdd on a single counter capped the walk at ~88 allocations/us).
+struct LaneOut {
+    uint32_t* contig_len;
+    uint64_t* chunk_data;
+    uint32_t* chunk_owner;   // only chunks >= n_first are recorded (chunk c < n_first is contig c)
+    uint32_t* chunk_seq;
+    uint64_t chunk_cap;
+    uint64_t n_first;        // = number of contigs
+};
+
+// Append base `b` as base number `steps` of contig c (2 bits, 32 per word, 8 words per chunk).
+__device__ __forceinline__ void append_base(const LaneOut& o, uint64_t c, uint32_t b, uint32_t& steps,
+                                            uint32_t& chunk, uint64_t& buf, unsigned long long* ctr,
+                                            unsigned long long* stats) {
+    if (steps == 0) {
+        chunk = (uint32_t)c;
+    } else if ((steps & (CHUNK_BASES - 1)) == 0) {
+        chunk = (uint32_t)(o.n_first + atomicAdd(&ctr[CT_CHUNK_NEXT], 1ull));
+        if (chunk < o.chunk_cap) {
+            o.chunk_owner[chunk] = (uint32_t)c;
+            o.chunk_seq[chunk] = steps / CHUNK_BASES;
+        } else {
+            atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+        }
+    }
+    buf |= (uint64_t)b << (2 * (steps & 31));
+    if ((steps & 31) == 31) {
+        if (chunk < o.chunk_cap) o.chunk_data[(uint64_t)chunk * CHUNK_WORDS + ((steps >> 5) & 7)] = buf;
+        buf = 0;
+    }
+    ++steps;
+}
+
+__device__ __forceinline__ void finish_contig(const LaneOut& o, uint64_t c, uint32_t steps, uint32_t chunk,
+                                              uint64_t buf) {
+    o.contig_len[c] = steps + 1;
+    if ((steps & 31) && chunk < o.chunk_cap)
+        o.chunk_data[(uint64_t)chunk * CHUNK_WORDS + ((steps >> 5) & 7)] = buf;
+}
+
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __restrict__ slots,
                                                 uint64_t cap, WalkBuffers wb,
                                                 unsigned long long* ctr,
                                                 unsigned long long* stats) {
     const uint32_t lane = lane_id();
-    uint64_t q_next = 0, q_end = 0;  // wave-uniform queue window
-    bool active = false, done = false;
-    uint64_t c = 0;
+    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, wb.n_starts};
+    const uint64_t n = wb.n_starts;
+    // wave-uniform batch window: contigs [bbase, bbase + WALK_GRAB), bused of them handed out
+    uint64_t bbase = 0;
+    uint32_t bused = WALK_GRAB;
+    bool bdry = false;
+    uint64_t bw0 = 0, bw1 = 0;  // this lane's preloaded start record of the batch
+
+    bool active = false, done = false, resolved = false;
+    uint64_t c = 0, s = 0, buf = 0;
     Key k{0, 0};
-    uint32_t fwd = 0;
-    uint32_t steps = 0;  // bases appended so far (= k-mers in contig - 1)
-    uint32_t chunk = 0;
-    uint64_t buf = 0;
+    uint32_t fwd = 0, steps = 0, chunk = 0;
     while (true) {
-        const bool need = !active && !done;
-        const uint64_t m = __ballot(need);
-        if (m) {
-            const uint32_t cnt = (uint32_t)__popcll(m);
-            const uint32_t rank = mbcnt64(m);
-            const uint64_t avail = q_end - q_next;
-            uint64_t nbase = 0;
-            if (cnt > avail) {
-                unsigned long long g = 0;
-                if (lane == 0) g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB);
-                nbase = __shfl(g, 0, 64);
-            }
-            const uint64_t mine = (rank < avail) ? q_next + rank : nbase + (rank - avail);
-            if (cnt > avail) {
-                q_next = nbase + (cnt - avail);
-                q_end = nbase + WALK_GRAB;
-            } else {
-                q_next += cnt;
-            }
-            if (need) {
-                if (mine >= wb.n_starts) {
-                    done = true;
+        // -- refill / finish until no lane finishes (single-k-mer contigs finish at once) ----
+        while (true) {
+            const bool need = !active && !done;
+            const uint64_t m = __ballot(need);
+            if (m) {
+                const uint32_t cnt = (uint32_t)__popcll(m);
+                const uint32_t rank = mbcnt64(m);
+                const uint32_t avail = WALK_GRAB - bused;
+                const uint32_t src_old = min(bused + rank, (uint32_t)WALK_GRAB - 1);
+                const uint64_t o0 = __shfl(bw0, (int)src_old, 64);
+                const uint64_t o1 = __shfl(bw1, (int)src_old, 64);
+                const uint64_t oc = bbase + src_old;
+                uint64_t n0 = 0, n1 = 0, nc = ~0ull;
+                if (cnt > avail) {
+                    if (!bdry) {
+                        unsigned long long g = 0;
+                        if (lane == 0) g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB);
+                        bbase = __shfl(g, 0, 64);
+                        if (bbase >= n) bdry = true;
+                        const uint64_t mi = bbase + lane;
+                        if (mi < n) {
+                            bw0 = wb.starts[mi * W];
+                            bw1 = (W == 2) ? wb.starts[mi * W + 1] : 0;
+                        }
+                        const uint32_t src_new = min(rank - min(rank, avail), (uint32_t)WALK_GRAB - 1);
+                        n0 = __shfl(bw0, (int)src_new, 64);
+                        n1 = __shfl(bw1, (int)src_new, 64);
+                        nc = bbase + src_new;
+                    }
+                    bused = cnt - avail;
                 } else {
-                    c = mine;
-                    const uint64_t w0 = wb.starts[c * W];
-                    const uint64_t w1 = (W == 2) ? wb.starts[c * W + 1] : 0;
-                    k = slot_key(w0, w1, p);
-                    fwd = ext_fwd(slot_ext(w0));
-                    steps = 0;
-                    buf = 0;
-                    active = true;
+                    bused += cnt;
+                }
+                if (need) {
+                    uint64_t cc = ~0ull, x0 = 0, x1 = 0;
+                    if (rank < avail) {
+                        cc = oc;
+                        x0 = o0;
+                        x1 = o1;
+                    } else {
+                        cc = nc;
+                        x0 = n0;
+                        x1 = n1;
+                    }
+                    if (cc < n) {
+                        c = cc;
+                        k = slot_key(x0, x1, p);
+                        fwd = ext_fwd(slot_ext(x0));
+                        steps = 0;
+                        buf = 0;
+                        active = true;
+                        resolved = true;
+                    } else {
+                        done = true;
+                    }
                 }
             }
+            const bool fin = active && resolved && fwd > 3;
+            if (fin) {
+                if (fwd != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+                finish_contig(o, c, steps, chunk, buf);
+                active = false;
+            }
+            if (!__any(fin)) break;
         }
         if (!__any(active)) break;
+        // -- advance: resolved lanes append their forward base and move to the next k-mer --------
+        if (active && resolved) {
+            append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
+            k = key_next(k, fwd, p);
+            s = home_slot(key_hash(k), cap);
+            resolved = false;
+        }
+        // -- one table load per active lane ---------------------------------------------------
         if (active) {
-            bool finish = false;
-            if (fwd == EXT_F) {
-                finish = true;
-            } else if (fwd > 3) {
-                atomicAdd(&stats[ST_BAD_EXT], 1ull);
-                finish = true;
-            } else {
-                if ((steps & (CHUNK_BASES - 1)) == 0) {
-                    chunk = (uint32_t)atomicAdd(&ctr[CT_CHUNK_NEXT], 1ull);
-                    if (chunk < wb.chunk_cap) {
-                        wb.chunk_owner[chunk] = (uint32_t)c;
-                        wb.chunk_seq[chunk] = steps / CHUNK_BASES;
-                    } else {
-                        atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
-                    }
+            uint64_t w0, w1;
+            load_slot<W>(slots, s, w0, w1);
+            const bool empty = w0 == EMPTY;
+            const bool hit = !empty & ((w0 >> 6) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
+            if (hit) {
+                fwd = ext_fwd(slot_ext(w0));
+                resolved = true;
+                if (steps > wb.max_steps) {
+                    atomicAdd(&stats[ST_CYCLE], 1ull);
+                    finish_contig(o, c, steps, chunk, buf);
+                    active = false;
                 }
-                buf |= (uint64_t)fwd << (2 * (steps & 31));
-                if ((steps & 31) == 31) {
-                    if (chunk < wb.chunk_cap)
-                        wb.chunk_data[(uint64_t)chunk * CHUNK_WORDS + ((steps >> 5) & 7)] = buf;
-                    buf = 0;
-                }
-                ++steps;
-                k = key_next(k, fwd, p);
-                uint64_t w0 = 0;
-                if (probe<W>(k, p, slots, cap, w0)) {
-                    fwd = ext_fwd(slot_ext(w0));
-                    if (steps > wb.max_steps) {
-                        atomicAdd(&stats[ST_CYCLE], 1ull);
-                        finish = true;
-                    }
-                } else {
-                    atomicAdd(&stats[ST_MISSING], 1ull);
-                    finish = true;
-                }
-            }
-            if (finish) {
-                wb.contig_len[c] = steps + 1;
-                if ((steps & 31) && chunk < wb.chunk_cap)
-                    wb.chunk_data[(uint64_t)chunk * CHUNK_WORDS + ((steps >> 5) & 7)] = buf;
+            } else if (empty) {
+                atomicAdd(&stats[ST_MISSING], 1ull);
+                finish_contig(o, c, steps, chunk, buf);
                 active = false;
+            } else {
+                s = (s + 1 == cap) ? 0 : s + 1;
             }
         }
     }
@@ -502,18 +590,20 @@ __global__ __launch_bounds__(BLOCK) void k_write_heads(KParams p, const uint64_t
 __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* chunk_data,
                                                         const uint32_t* owner, const uint32_t* seq,
                                                         const unsigned long long* ctr,
-                                                        uint64_t chunk_cap, const uint32_t* len,
+                                                        uint64_t chunk_cap, uint64_t n_first,
+                                                        const uint32_t* len,
                                                         const uint64_t* off, char* out) {
-    // The chunk count is only known on the device (walker allocation head), so the grid is sized
-    // for the capacity and bounded here.
-    const uint64_t nchunks = min((uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
+    // Chunks [0, n_first) are the contigs' own first chunks; the extra-chunk count is only known
+    // on the device (walker allocation head), so the grid is sized for the capacity and bounded
+    // here.
+    const uint64_t nchunks = min(n_first + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
     const uint64_t nwords = nchunks * CHUNK_WORDS;
     for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nwords;
          t += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t ch = t / CHUNK_WORDS;
         const uint32_t w = (uint32_t)(t % CHUNK_WORDS);
-        const uint32_t c = owner[ch];
-        const uint64_t j0 = (uint64_t)seq[ch] * CHUNK_BASES + (uint64_t)w * 32;
+        const uint32_t c = ch < n_first ? (uint32_t)ch : owner[ch];
+        const uint64_t j0 = (ch < n_first ? 0ull : (uint64_t)seq[ch] * CHUNK_BASES) + (uint64_t)w * 32;
         const uint64_t app = (uint64_t)len[c] - 1;
         if (j0 >= app) continue;
         const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
@@ -538,8 +628,315 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
     const unsigned gc =
         (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr,
-                                        wb.chunk_cap, wb.contig_len, offsets, out);
+                                        wb.chunk_cap, nc, wb.contig_len, offsets, out);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Sharded multi-GPU path. The key space is split by owner_of(key_hash); records
+// are routed to their owner once (insert), then contigs are walked in rounds: every home rank
+// emits the next k-mer of each live walker to its owner, owners answer with the ext byte, homes
+// apply the answers. The exchange between emit and apply is the caller's (RCCL all-to-all).
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_start_mask(KParams p, const uint8_t* __restrict__ recs,
+                                                      uint64_t n, uint64_t* start_mask) {
+    const uint64_t nw = (n + 63) >> 6;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < nw * 64;
+         i0 += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t i = i0 + (threadIdx.x & 63);
+        const bool st = i < n && recs[i * (uint64_t)p.R + p.P] == 'F';
+        const uint64_t bal = __ballot(st);
+        if ((threadIdx.x & 63) == 0) start_mask[i0 >> 6] = bal;
+    }
+}
+
+hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, uint64_t* start_mask,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = (unsigned)hmin((n + BLOCK - 1) / BLOCK, 8192);
+    k_start_mask<1><<<grid, BLOCK, 0, s>>>(p, recs, n, start_mask);
+    return hipGetLastError();
+}
+
+// Owner-major view of a [blocks][ranks] histogram for the exclusive scan.
+struct HistF {
+    const uint64_t* hist;
+    uint64_t nb;
+    uint32_t P;
+    __device__ uint64_t operator()(uint64_t i) const { return hist[(i % nb) * P + i / nb]; }
+};
+
+__global__ void k_route_counts(const uint64_t* off, uint64_t nb, uint32_t P,
+                               const unsigned long long* total, uint64_t* counts) {
+    const uint32_t q = threadIdx.x;
+    if (q < P) {
+        const uint64_t a = off[(uint64_t)q * nb];
+        const uint64_t b = (q + 1 < P) ? off[(uint64_t)(q + 1) * nb] : (uint64_t)*total;
+        counts[q] = b - a;
+    }
+    if (q == 0) counts[P] = (uint64_t)*total;
+}
+
+// Generic two-kernel owner grouping. Op must provide:
+//   int owner(uint64_t i)             -> rank in [0,P) or -1 to skip (read-only)
+//   void emit(uint64_t i, int q, uint64_t dst)   (may mutate per-item state; called once)
+template <class Op>
+__global__ __launch_bounds__(BLOCK) void k_group_hist(Op op, uint64_t n, uint32_t P, uint64_t* hist) {
+    __shared__ uint32_t h[MAX_RANKS];
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+    for (uint32_t j = threadIdx.x; j < ROUTE_TILE; j += BLOCK) {
+        const uint64_t i = b0 + j;
+        if (i < n) {
+            const int q = op.owner(i);
+            if (q >= 0) atomicAdd(&h[q], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) hist[(uint64_t)blockIdx.x * P + q] = h[q];
+}
+
+template <class Op>
+__global__ __launch_bounds__(BLOCK) void k_group_scatter(Op op, uint64_t n, uint32_t P,
+                                                         const uint64_t* off, uint64_t nb) {
+    __shared__ uint32_t h[MAX_RANKS];
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+    for (uint32_t j = threadIdx.x; j < ROUTE_TILE; j += BLOCK) {
+        const uint64_t i = b0 + j;
+        int q = -1;
+        if (i < n) q = op.owner(i);
+        uint64_t dst = 0;
+        if (q >= 0) dst = off[(uint64_t)q * nb + blockIdx.x] + atomicAdd(&h[q], 1u);
+        if (i < n) op.emit(i, q, dst);
+    }
+}
+
+template <class Op>
+static hipError_t group_by_owner(Op op, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
+                                 uint64_t* scratch, uint64_t* counts, unsigned long long* total,
+                                 hipStream_t s) {
+    const uint64_t nb = route_blocks(n);
+    if (nb == 0) {
+        hipError_t e = hipMemsetAsync(counts, 0, (P + 1) * 8, s);
+        return e;
+    }
+    k_group_hist<Op><<<(unsigned)nb, BLOCK, 0, s>>>(op, n, P, hist);
+    hipError_t e = scan_exclusive(HistF{hist, nb, P}, nb * P, off, scratch,
+                                  (unsigned long long*)nullptr, total, s);
+    if (e != hipSuccess) return e;
+    k_route_counts<<<1, MAX_RANKS, 0, s>>>(off, nb, P, total, counts);
+    k_group_scatter<Op><<<(unsigned)nb, BLOCK, 0, s>>>(op, n, P, off, nb);
+    return hipGetLastError();
+}
+
+template <int W>
+struct RouteOp {
+    KParams p;
+    const uint8_t* recs;
+    uint32_t P;
+    uint64_t* out;
+    __device__ int owner(uint64_t i) const {
+        const Key k = key_from_packed(recs + i * (uint64_t)p.R, p);
+        return (int)owner_of(key_hash(k), P);
+    }
+    __device__ void emit(uint64_t i, int q, uint64_t dst) const {
+        Key k;
+        uint32_t ext;
+        parse_record(recs + i * (uint64_t)p.R, p, k, ext);
+        out[dst * W] = slot_w0(k, ext, p);
+        if (W == 2) out[dst * W + 1] = k.lo;
+    }
+};
+
+hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
+                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out_words,
+                        uint64_t* counts, hipStream_t s) {
+    // the scan's total goes to counts[nranks] via a device word: reuse the last hist entry slot
+    unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
+    uint64_t* sc = scratch + 1;
+    if (p.W == 1)
+        return group_by_owner(RouteOp<1>{p, recs, nranks, out_words}, n, nranks, hist, off, sc, counts,
+                              total, s);
+    return group_by_owner(RouteOp<2>{p, recs, nranks, out_words}, n, nranks, hist, off, sc, counts,
+                          total, s);
+}
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_insert_words(KParams p, const uint64_t* __restrict__ words,
+                                                        uint64_t m, uint64_t* slots, uint64_t cap,
+                                                        unsigned long long* stats) {
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m;
+         i += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t w0 = words[i * W];
+        const uint64_t w1 = (W == 2) ? words[i * W + 1] : 0;
+        const uint32_t ext = slot_ext(w0);
+        if (ext_bwd(ext) == EXT_BAD || ext_fwd(ext) == EXT_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+        insert_one<W>(slot_key(w0, w1, p), ext, p, slots, cap, stats);
+    }
+}
+
+hipError_t launch_insert_words(const KParams& p, const uint64_t* words, uint64_t m, TableView t,
+                               unsigned long long* stats, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    const unsigned grid = (unsigned)hmin((m + BLOCK - 1) / BLOCK, 256ull * 32);
+    if (p.W == 1)
+        k_insert_words<1><<<grid, BLOCK, 0, s>>>(p, words, m, t.slots, t.cap, stats);
+    else
+        k_insert_words<2><<<grid, BLOCK, 0, s>>>(p, words, m, t.slots, t.cap, stats);
+    return hipGetLastError();
+}
+
+// ---- round walker ---------------------------------------------------------------------------
+static constexpr uint8_t RW_F = 4, RW_BAD = 5, RW_DONE = 6, RW_PENDING = 7;
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_rw_init(KParams p, RoundWalk rw, const uint64_t* starts) {
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < rw.n;
+         i += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t w0 = starts[i * W];
+        const uint64_t w1 = (W == 2) ? starts[i * W + 1] : 0;
+        const Key k = slot_key(w0, w1, p);
+        rw.hi[i] = k.hi;
+        rw.lo[i] = k.lo;
+        rw.buf[i] = 0;
+        rw.steps[i] = 0;
+        rw.chunk[i] = 0;
+        const uint32_t f = ext_fwd(slot_ext(w0));
+        rw.state[i] = (uint8_t)(f > 4 ? RW_BAD : f);
+    }
+}
+
+hipError_t launch_rw_init(const KParams& p, const RoundWalk& rw, const uint64_t* starts, hipStream_t s) {
+    if (rw.n == 0) return hipSuccess;
+    const unsigned grid = (unsigned)hmin((rw.n + BLOCK - 1) / BLOCK, 8192);
+    if (p.W == 1)
+        k_rw_init<1><<<grid, BLOCK, 0, s>>>(p, rw, starts);
+    else
+        k_rw_init<2><<<grid, BLOCK, 0, s>>>(p, rw, starts);
+    return hipGetLastError();
+}
+
+template <int W>
+struct EmitOp {
+    KParams p;
+    RoundWalk rw;
+    uint32_t P;
+    uint64_t* keys;
+    unsigned long long* ctr;
+    unsigned long long* stats;
+    __device__ int owner(uint64_t i) const {
+        const uint8_t st = rw.state[i];
+        if (st > 3) return -1;
+        const Key k = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
+        return (int)owner_of(key_hash(k), P);
+    }
+    __device__ void emit(uint64_t i, int q, uint64_t dst) const {
+        const uint8_t st = rw.state[i];
+        if (st == RW_DONE) return;
+        const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
+        uint32_t steps = rw.steps[i], chunk = rw.chunk[i];
+        uint64_t buf = rw.buf[i];
+        if (st == RW_F || st == RW_BAD) {
+            if (st == RW_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+            finish_contig(o, i, steps, chunk, buf);
+            rw.state[i] = RW_DONE;
+            return;
+        }
+        append_base(o, i, st, steps, chunk, buf, ctr, stats);
+        const Key k = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
+        rw.hi[i] = k.hi;
+        rw.lo[i] = k.lo;
+        rw.steps[i] = steps;
+        rw.chunk[i] = chunk;
+        rw.buf[i] = buf;
+        rw.state[i] = RW_PENDING;
+        if (W == 2) {
+            keys[dst * 2] = k.hi;
+            keys[dst * 2 + 1] = k.lo;
+        } else {
+            keys[dst] = k.lo;
+        }
+        rw.qperm[dst] = (uint32_t)i;
+        (void)q;
+    }
+};
+
+hipError_t launch_rw_emit(const KParams& p, const RoundWalk& rw, uint32_t nranks, uint64_t* hist,
+                          uint64_t* off, uint64_t* scratch, uint64_t* keys, uint64_t* counts,
+                          unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+    unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
+    uint64_t* sc = scratch + 1;
+    if (p.W == 1)
+        return group_by_owner(EmitOp<1>{p, rw, nranks, keys, ctr, stats}, rw.n, nranks, hist, off, sc,
+                              counts, total, s);
+    return group_by_owner(EmitOp<2>{p, rw, nranks, keys, ctr, stats}, rw.n, nranks, hist, off, sc,
+                          counts, total, s);
+}
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_find_ext(KParams p, const uint64_t* __restrict__ keys,
+                                                    uint64_t m, const uint64_t* slots, uint64_t cap,
+                                                    uint8_t* ext) {
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < m;
+         j += (uint64_t)gridDim.x * BLOCK) {
+        Key k;
+        if (W == 2) {
+            k.hi = keys[j * 2];
+            k.lo = keys[j * 2 + 1];
+        } else {
+            k.hi = 0;
+            k.lo = keys[j];
+        }
+        uint64_t w0 = 0;
+        ext[j] = probe<W>(k, p, slots, cap, w0) ? (uint8_t)slot_ext(w0) : (uint8_t)0xFF;
+    }
+}
+
+hipError_t launch_find_ext(const KParams& p, const uint64_t* keys, uint64_t m, TableView t,
+                           uint8_t* ext, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    const unsigned grid = (unsigned)hmin((m + BLOCK - 1) / BLOCK, 8192);
+    if (p.W == 1)
+        k_find_ext<1><<<grid, BLOCK, 0, s>>>(p, keys, m, t.slots, t.cap, ext);
+    else
+        k_find_ext<2><<<grid, BLOCK, 0, s>>>(p, keys, m, t.slots, t.cap, ext);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rw_apply(RoundWalk rw, const uint8_t* ext, uint64_t m,
+                                                    unsigned long long* stats) {
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < m;
+         j += (uint64_t)gridDim.x * BLOCK) {
+        const uint32_t i = rw.qperm[j];
+        const uint8_t r = ext[j];
+        const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
+        if (r == 0xFF) {
+            atomicAdd(&stats[ST_MISSING], 1ull);
+            finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
+            rw.state[i] = RW_DONE;
+        } else if (rw.steps[i] > rw.max_steps) {
+            atomicAdd(&stats[ST_CYCLE], 1ull);
+            finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
+            rw.state[i] = RW_DONE;
+        } else {
+            const uint32_t f = ext_fwd(r);
+            rw.state[i] = (uint8_t)(f > 4 ? RW_BAD : f);
+        }
+    }
+}
+
+hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t* ext, uint64_t m,
+                           unsigned long long* stats, hipStream_t s) {
+    (void)p;
+    if (m == 0) return hipSuccess;
+    const unsigned grid = (unsigned)hmin((m + BLOCK - 1) / BLOCK, 8192);
+    k_rw_apply<<<grid, BLOCK, 0, s>>>(rw, ext, m, stats);
     return hipGetLastError();
 }
 
 }  // namespace kh
+

@@ -81,3 +81,58 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
 uint64_t scan_scratch_words(uint64_t m);
 
 }  // namespace kh
+
+// ---- sharded multi-GPU path (one table per rank; the exchange itself is the caller's) -------
+namespace kh {
+
+// Items per block of the owner-routing kernels (histogram / scatter).
+static constexpr int ROUTE_TILE = 2048;
+static constexpr int MAX_RANKS = 64;
+inline uint64_t route_blocks(uint64_t n) { return (n + ROUTE_TILE - 1) / ROUTE_TILE; }
+
+// Start bits only (no insert): bwd == 'F' per record, wave ballot -> start_mask[i/64].
+hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, uint64_t* start_mask,
+                             hipStream_t s);
+
+// Records -> internal words (W per record) grouped by owner rank (owner_of(key_hash)).
+// hist/off: route_blocks(n) * nranks words each; counts: nranks + 1 words (last = n).
+hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
+                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out_words,
+                        uint64_t* counts, hipStream_t s);
+
+// Insert routed internal words.
+hipError_t launch_insert_words(const KParams& p, const uint64_t* words, uint64_t m, TableView t,
+                               unsigned long long* stats, hipStream_t s);
+
+// Round-based walker state (structure of arrays, one entry per local start k-mer).
+struct RoundWalk {
+    uint64_t n;          // walkers = local start k-mers
+    uint64_t* hi;        // current key
+    uint64_t* lo;
+    uint64_t* buf;       // partial word of appended bases
+    uint32_t* steps;     // bases appended
+    uint32_t* chunk;     // current chunk
+    uint8_t* state;      // 0..3 fwd base, 4 'F', 5 bad, 6 done, 7 query in flight
+    uint32_t* qperm;     // query slot -> walker
+    uint32_t* contig_len;
+    uint64_t* chunk_data;
+    uint32_t* chunk_owner;
+    uint32_t* chunk_seq;
+    uint64_t chunk_cap;
+    uint64_t max_steps;
+};
+
+hipError_t launch_rw_init(const KParams& p, const RoundWalk& rw, const uint64_t* starts, hipStream_t s);
+// Emit one query per walker that has a next k-mer, grouped by owner rank; finish walkers at 'F'.
+// keys: W words per query; counts: nranks + 1 words (last = total queries).
+hipError_t launch_rw_emit(const KParams& p, const RoundWalk& rw, uint32_t nranks, uint64_t* hist,
+                          uint64_t* off, uint64_t* scratch, uint64_t* keys, uint64_t* counts,
+                          unsigned long long* ctr, unsigned long long* stats, hipStream_t s);
+// Owner side: ext byte of each queried key (0xFF = absent).
+hipError_t launch_find_ext(const KParams& p, const uint64_t* keys, uint64_t m, TableView t,
+                           uint8_t* ext, hipStream_t s);
+// Home side: apply the replies of the m queries emitted last round.
+hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t* ext, uint64_t m,
+                           unsigned long long* stats, hipStream_t s);
+
+}  // namespace kh

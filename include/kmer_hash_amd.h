@@ -105,6 +105,26 @@ int kh_contigs_text(kh_table* t, char* host_out, uint64_t cap);          /* D2H 
 int kh_contigs_text_dev(kh_table* t, const char** dev_text, uint64_t* bytes);
 int kh_contigs_offsets(kh_table* t, uint64_t* host_offsets, uint64_t n); /* line starts */
 
+/* ---- sharded multi-GPU path --------------------------------------------------------------------
+ * One table per rank (GPU). The key space is split by an owner hash; the caller moves the buffers
+ * between ranks (RCCL all-to-all over xGMI; cs267_hw3_amd/dist.py). Replaces the per-owner batched
+ * insert RPCs (hash_map.hpp:38-46,64-77) and the per-step remote find RPCs (hash_map.hpp:94-100).
+ * Routed records and query keys are kh_word_count(k) 64-bit words each. counts_out receives
+ * nranks + 1 uint64 on the device: per-destination counts, then their total. All async. */
+int kh_word_count(int k);
+int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n); /* local start k-mers */
+int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
+                 void* dev_counts_out);
+int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);
+/* Round walk: begin (sync; sizes buffers; total_kmers = k-mers over all ranks, bounds contig
+ * length), then per round emit -> exchange keys -> find_ext (owner) -> exchange replies -> apply,
+ * until no rank emits; end materialises this rank's contig text (kh_contigs_text*). */
+int kh_walk_begin(kh_table* t, uint64_t total_kmers, uint64_t* n_walkers);
+int kh_walk_emit_dev(kh_table* t, int nranks, void* dev_keys_out, void* dev_counts_out);
+int kh_find_ext_dev(kh_table* t, const void* dev_keys, uint64_t m, void* dev_ext_out);
+int kh_walk_apply_dev(kh_table* t, const void* dev_ext, uint64_t m);
+int kh_walk_end_dev(kh_table* t);
+
 /* ---- device memory helpers (for hosts without an allocator of their own) --------------------*/
 int kh_dev_malloc(void** p, uint64_t bytes, int device);
 int kh_dev_free(void* p);

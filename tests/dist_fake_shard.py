@@ -1,0 +1,115 @@
+"""CPU test double of cs267_hw3_amd.dist.GpuShard — TEST INFRASTRUCTURE ONLY.
+
+Implements the per-rank local operations with Python dicts and the oracle's codec (string-round-trip
+next_kmer, djb2 owner), so the SPMD driver's routing, count exchange, round structure and
+termination are exercised over a real torch.distributed gloo group with no GPU.
+"""
+import numpy as np
+import torch
+
+import oracle_bind as ob
+
+
+class FakeShard:
+    W = 2  # 16 bytes per routed record / query key
+
+    def __init__(self, k):
+        self.k = k
+        self.P = (k + 3) // 4
+        self.R = self.P + 2
+        assert self.R <= 16
+        self.clear()
+
+    # -- helpers ------------------------------------------------------------------------------
+    def _enc(self, rows):
+        """list of <=16-byte strings -> int64 tensor [len * 2]."""
+        buf = np.zeros((max(len(rows), 1), 16), np.uint8)
+        for i, r in enumerate(rows):
+            buf[i, :len(r)] = np.frombuffer(r, np.uint8)
+        return torch.from_numpy(buf.view(np.int64).reshape(-1).copy())
+
+    def _dec(self, t, m, width):
+        a = t[:m * 2].numpy().view(np.uint8).reshape(m, 16)
+        return [bytes(a[i, :width]) for i in range(m)]
+
+    def _owner(self, key, nranks):
+        return ob.djb2(self.k, np.frombuffer(key, np.uint8)) % nranks
+
+    def _group(self, items, nranks):
+        """items: list of (owner, payload) -> (payloads in owner order, counts tensor [P+1])."""
+        order = sorted(range(len(items)), key=lambda i: items[i][0])
+        counts = np.zeros(nranks + 1, np.int64)
+        for q, _ in items:
+            counts[q] += 1
+        counts[nranks] = len(items)
+        return [items[i][1] for i in order], order, torch.from_numpy(counts)
+
+    # -- shard interface --------------------------------------------------------------------------
+    def clear(self):
+        self.table = {}
+        self.starts = []
+
+    def collect_starts(self, recs):
+        for r in recs.numpy():
+            if r[self.P] == ord("F"):
+                self.starts.append(bytes(r))
+
+    def route(self, recs, nranks):
+        rows = [bytes(r) for r in recs.numpy()]
+        payloads, _, counts = self._group([(self._owner(r[:self.P], nranks), r) for r in rows], nranks)
+        return self._enc(payloads), counts
+
+    def insert_words(self, words, m):
+        for rec in self._dec(words, m, self.R):
+            assert rec[:self.P] not in self.table, "duplicate k-mer"
+            self.table[rec[:self.P]] = rec
+
+    def walk_begin(self, total_kmers):
+        # walker = [key bytes, fwd char, contig string, done]
+        self.walkers = []
+        for s in self.starts:
+            self.walkers.append([s[:self.P], chr(s[self.P + 1]),
+                                 ob.unpack(self.k, np.frombuffer(s[:self.P], np.uint8)), False])
+        self.nw = len(self.walkers)
+        return self.nw
+
+    def walk_emit(self, nranks):
+        items = []
+        for i, w in enumerate(self.walkers):
+            if w[3]:
+                continue
+            if w[1] == "F":
+                w[3] = True
+                continue
+            w[2] += w[1]                                   # extract_contig appends fwd ext
+            rec = np.frombuffer(w[0] + b"X" + w[1].encode(), np.uint8)
+            w[0] = bytes(ob.next_kmer(self.k, rec))        # kmer_t.hpp:51-53
+            items.append((self._owner(w[0], nranks), (i, w[0])))
+        payloads, _, counts = self._group(items, nranks)
+        self.qperm = [p[0] for p in payloads]
+        return self._enc([p[1] for p in payloads]), counts
+
+    def find_ext(self, keys, m):
+        out = np.full(max(m, 1), 0xFF, np.uint8)
+        for j, key in enumerate(self._dec(keys, m, self.P)):
+            rec = self.table.get(key)
+            if rec is not None:
+                out[j] = rec[self.P + 1]                   # forward extension char
+        return torch.from_numpy(out)
+
+    def walk_apply(self, ext, m):
+        e = ext[:m].numpy()
+        for j in range(m):
+            w = self.walkers[self.qperm[j]]
+            if e[j] == 0xFF:
+                raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
+            w[1] = chr(e[j])
+
+    def walk_end(self):
+        self.text = "".join(w[2] + "\n" for w in self.walkers).encode()
+
+    def sync(self):
+        pass
+
+    def contigs_text(self):
+        return self.text
