@@ -1,0 +1,557 @@
+// kh_build.hip — atomic-free bulk build of the open-addressing k-mer table (gfx950).
+//
+// Replaces one-CAS-per-key global inserts (bound at ~20 G random CAS/s on MI355X, measured by
+// tools/membench) with streaming passes:
+//   pass 1   group the batch by the top 9 bits of key_hash         512 bins
+//   pass 2   then by the next 8 bits, within each pass-1 bucket     256 bins
+//            (per-block LDS histograms + one exclusive scan per pass; each 4096-item tile is
+//             counting-sorted by bin in LDS first so waves write contiguous runs)
+//   build    one workgroup per region (top 17 hash bits) builds its slot range (~cap/2^17 slots,
+//            ~49 KB at 200M k-mers) in LDS with LDS CAS linear probing, then writes the slice
+//            out with coalesced 16-B stores
+//   overflow keys whose probe run leaves their slice take the global CAS path afterwards, so
+//            every key satisfies the linear-probing invariant "all slots from home to position
+//            are occupied"
+// Placement differs from the CAS path; find()/the walk depend only on the invariant, so outputs
+// are identical (tests run both paths).
+#include <hip/hip_runtime.h>
+
+#include "kh_device.hpp"
+
+namespace kh {
+
+static constexpr int PB = 256;                    // threads per radix block
+static constexpr int PITEMS = PART_TILE / PB;     // inputs per thread per tile (16)
+static constexpr int B1 = 9, B2 = 8;              // radix bits per pass
+static constexpr int NB1 = 1 << B1, NB2 = 1 << B2;
+static constexpr int RBITS = B1 + B2;             // region = top 17 hash bits
+static constexpr uint32_t NREG = 1u << RBITS;
+static constexpr int BUILD_THREADS = 512;
+static constexpr int T1 = 2;                      // consecutive tiles per pass-1 block
+static constexpr uint64_t LDS_BYTES = 160 * 1024;
+// radix-pass LDS: sorted items (2 words) + bin ids + hist/start (u32) + per-bin bases (u64) = 80 KiB
+static constexpr size_t SORT_LDS = (size_t)PART_TILE * 16 + PART_TILE * 2 + 2 * NB1 * 4 + NB1 * 8;
+
+PartPlan part_plan(uint64_t n) {
+    PartPlan pl;
+    pl.n = n;
+    pl.nb1 = (n + (uint64_t)T1 * PART_TILE - 1) / ((uint64_t)T1 * PART_TILE);
+    const uint64_t tiles_per_bucket = (n / NB1 + PART_TILE - 1) / PART_TILE + 1;
+    pl.G = (tiles_per_bucket + 1) / 2;
+    if (pl.G < 1) pl.G = 1;
+    return pl;
+}
+
+uint64_t part_hist_words(const PartPlan& pl) {
+    const uint64_t a = pl.nb1 * NB1, b = (uint64_t)NB1 * NB2 * pl.G;
+    return (a > b ? a : b) + 1;
+}
+
+uint64_t part_scratch_words(const PartPlan& pl) { return scan_scratch_words(part_hist_words(pl)) + 2; }
+
+uint64_t part_overflow_cap(uint64_t n) { return n / 4 + 65536; }
+
+static uint64_t region_max_slots(uint64_t cap) { return cap / NREG + 1; }
+
+bool region_slots_fit(const KParams& p, uint64_t cap) {
+    return region_max_slots(cap) <= LDS_BYTES / (8ull * p.W);
+}
+
+bool part_usable(const KParams& p, uint64_t cap, uint64_t n) {
+    return n >= (1ull << 20) && region_slots_fit(p, cap) && cap >= (uint64_t)NREG * 8;
+}
+
+template <int W>
+__device__ __forceinline__ uint64_t words_hash(uint64_t w0, uint64_t w1, const KParams& p) {
+    return key_hash(slot_key(w0, w1, p));
+}
+
+// ---- tile loading -------------------------------------------------------------------------------
+// Loads up to PART_TILE inputs starting at `base` into registers (item j of thread t is input
+// base + j*PB + t). Records are staged through LDS CH at a time (`stage` >= CH*R bytes): every
+// thread issues its 16-B loads for the whole chunk at once, so a chunk costs one memory latency;
+// start bits are ballot-written to start_mask when given.
+template <int W, bool REC, int CH>
+__device__ __forceinline__ void load_tile(const KParams& p, const uint8_t* recs, const uint64_t* words,
+                                          uint64_t base, uint64_t end, uint64_t* start_mask,
+                                          uint8_t* stage, uint64_t (&a)[PITEMS], uint64_t (&b)[PITEMS]) {
+    if (REC) {
+        constexpr int JPC = CH / PB;  // items per thread per chunk
+#pragma unroll
+        for (int c = 0; c < PITEMS / JPC; ++c) {
+            const uint64_t cb = base + (uint64_t)c * CH;
+            const uint32_t cnt = cb < end ? (uint32_t)min((uint64_t)CH, end - cb) : 0u;
+            if (cnt) {  // uniform
+                // all of this thread's 16-B loads in flight at once, then the LDS stores (a
+                // load->store loop with a runtime trip count serialised one round trip per vector)
+                constexpr int MAXV = (CH * 17 / 16 + PB - 1) / PB;
+                const uint8_t* src = recs + cb * p.R;
+                const uint32_t bytes = cnt * p.R, nvec = bytes >> 4;
+                uint4 r[MAXV];
+#pragma unroll
+                for (int q = 0; q < MAXV; ++q) {
+                    const uint32_t v = threadIdx.x + (uint32_t)q * PB;
+                    if (v < nvec) r[q] = reinterpret_cast<const uint4*>(src)[v];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < MAXV; ++q) {
+                    const uint32_t v = threadIdx.x + (uint32_t)q * PB;
+                    if (v < nvec) reinterpret_cast<uint4*>(stage)[v] = r[q];
+                }
+                for (uint32_t x = (nvec << 4) + threadIdx.x; x < bytes; x += PB) stage[x] = src[x];
+                __syncthreads();
+            }
+#pragma unroll
+            for (int jj = 0; jj < JPC; ++jj) {
+                const int j = c * JPC + jj;
+                const uint32_t li = (uint32_t)jj * PB + threadIdx.x;  // index inside the chunk
+                const bool valid = li < cnt;
+                Key k{0, 0};
+                uint32_t ext = 0;
+                if (valid) parse_record(stage + li * p.R, p, k, ext);
+                if (start_mask && cnt) {
+                    const uint64_t bal = __ballot(valid && ext_bwd(ext) == EXT_F);
+                    const uint64_t wb = cb + (uint64_t)jj * PB + (threadIdx.x & ~63u);
+                    if ((threadIdx.x & 63) == 0 && wb < end) start_mask[wb >> 6] = bal;
+                }
+                a[j] = valid ? slot_w0(k, ext, p) : EMPTY;
+                b[j] = (valid && W == 2) ? k.lo : 0;
+            }
+        }
+        __syncthreads();
+    } else {
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j) {
+            const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
+            a[j] = EMPTY;
+            b[j] = 0;
+            if (i < end) {
+                a[j] = words[i * W];
+                b[j] = (W == 2) ? words[i * W + 1] : 0;
+            }
+        }
+    }
+}
+
+// Block-wide exclusive scan of NB (<= 512) LDS counters into start[]; returns the total.
+template <int NB>
+__device__ __forceinline__ uint32_t scan_bins(const uint32_t* hist, uint32_t* start) {
+    constexpr int PER = (NB + PB - 1) / PB;
+    uint32_t v[PER];
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = threadIdx.x * PER + q;
+        v[q] = i < NB ? hist[i] : 0;
+        s += v[q];
+    }
+    uint64_t tot;
+    uint64_t pre = block_excl_scan(s, tot);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = threadIdx.x * PER + q;
+        if (i < NB) start[i] = (uint32_t)pre;
+        pre += v[q];
+    }
+    __syncthreads();
+    return (uint32_t)tot;
+}
+
+// Counting-sort the tile's items by bin in LDS, then write them to out at gbase[bin] + rank
+// (gbase in LDS), so consecutive lanes store consecutive addresses of one bin.
+template <int W, int NB>
+__device__ __forceinline__ void sorted_write(const uint64_t (&a)[PITEMS], const uint64_t (&b)[PITEMS],
+                                             const uint32_t (&bin)[PITEMS], uint64_t* items,
+                                             uint16_t* sbin, uint32_t* hist, uint32_t* start,
+                                             const uint64_t* gbase, uint64_t* out) {
+    for (int i = threadIdx.x; i < NB; i += PB) hist[i] = 0;
+    __syncthreads();
+    uint32_t rank[PITEMS];
+#pragma unroll
+    for (int j = 0; j < PITEMS; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
+    __syncthreads();
+    const uint32_t total = scan_bins<NB>(hist, start);
+#pragma unroll
+    for (int j = 0; j < PITEMS; ++j) {
+        if (a[j] != EMPTY) {
+            const uint32_t pos = start[bin[j]] + rank[j];
+            items[pos * W] = a[j];
+            if (W == 2) items[pos * W + 1] = b[j];
+            sbin[pos] = (uint16_t)bin[j];
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < total; t += PB) {
+        const uint32_t q = sbin[t];
+        const uint64_t g = gbase[q] + (t - start[q]);
+        if (W == 2) {
+            *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(items[2 * t], items[2 * t + 1]);
+        } else {
+            out[g] = items[t];
+        }
+    }
+    __syncthreads();
+}
+
+// ---- pass 1: bin = top 9 hash bits --------------------------------------------------------------
+// Record input: parse the reference records once, one per thread per 256-record sub-tile (the next
+// sub-tile's 16-B loads are in flight while this one is parsed), emit internal words in input
+// order, count bins, and write the start bits. The pass-1 scatter then reads words only.
+template <int W>
+__global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* __restrict__ recs,
+                                                      uint64_t n, uint64_t* words_out, uint64_t* hist1,
+                                                      uint64_t* start_mask) {
+    __shared__ uint32_t h[NB1];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[2][PB * 17];
+    for (int i = threadIdx.x; i < NB1; i += PB) h[i] = 0;
+    const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
+    const uint64_t b1 = min(b0 + (uint64_t)T1 * PART_TILE, n);
+    const uint32_t R = (uint32_t)p.R;
+    const uint32_t nsub = (uint32_t)((b1 - b0 + PB - 1) / PB);
+    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+    auto fetch = [&](uint32_t j) {
+        const uint64_t sub = b0 + (uint64_t)j * PB;
+        const uint32_t nvec = (uint32_t)(min((uint64_t)PB, b1 - sub) * R) >> 4;
+        const uint4* src = reinterpret_cast<const uint4*>(recs + sub * R);
+        if (threadIdx.x < nvec) r0 = src[threadIdx.x];
+        if (threadIdx.x + PB < nvec) r1 = src[threadIdx.x + PB];
+    };
+    if (nsub) fetch(0);
+    for (uint32_t j = 0; j < nsub; ++j) {
+        const uint64_t sub = b0 + (uint64_t)j * PB;
+        const uint32_t cnt = (uint32_t)min((uint64_t)PB, b1 - sub);
+        const uint32_t bytes = cnt * R, nvec = bytes >> 4;
+        uint8_t* st = stage[j & 1];
+        if (threadIdx.x < nvec) reinterpret_cast<uint4*>(st)[threadIdx.x] = r0;
+        if (threadIdx.x + PB < nvec) reinterpret_cast<uint4*>(st)[threadIdx.x + PB] = r1;
+        for (uint32_t x = (nvec << 4) + threadIdx.x; x < bytes; x += PB) st[x] = recs[sub * R + x];
+        if (j + 1 < nsub) fetch(j + 1);
+        __syncthreads();
+        const bool valid = threadIdx.x < cnt;
+        Key k{0, 0};
+        uint32_t ext = 0;
+        if (valid) parse_record(st + threadIdx.x * R, p, k, ext);
+        const uint64_t bal = __ballot(valid && ext_bwd(ext) == EXT_F);
+        const uint64_t wb = sub + (threadIdx.x & ~63u);
+        if ((threadIdx.x & 63) == 0 && wb < b1 && start_mask) start_mask[wb >> 6] = bal;
+        if (valid) {
+            const uint64_t w0 = slot_w0(k, ext, p), i = sub + threadIdx.x;
+            if (W == 2) {
+                *reinterpret_cast<ulonglong2*>(words_out + i * 2) = make_ulonglong2(w0, k.lo);
+            } else {
+                words_out[i] = w0;
+            }
+            atomicAdd(&h[key_hash(k) >> (64 - B1)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NB1; i += PB) hist1[(uint64_t)blockIdx.x * NB1 + i] = h[i];
+}
+
+template <int W, bool REC>
+__global__ __launch_bounds__(PB) void k_part1_hist(KParams p, const uint8_t* recs, const uint64_t* words,
+                                                   uint64_t n, uint64_t* hist1, uint64_t* start_mask) {
+    __shared__ uint32_t h[NB1];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[REC ? 1024 * 17 : 16];
+    for (int i = threadIdx.x; i < NB1; i += PB) h[i] = 0;
+    __syncthreads();
+    for (int tt = 0; tt < T1; ++tt) {
+        const uint64_t base = ((uint64_t)blockIdx.x * T1 + tt) * PART_TILE;
+        if (base >= n) break;  // uniform
+        uint64_t a[PITEMS], b[PITEMS];
+        load_tile<W, REC, 1024>(p, recs, words, base, min(base + PART_TILE, n), start_mask, stage, a, b);
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j)
+            if (a[j] != EMPTY) atomicAdd(&h[words_hash<W>(a[j], b[j], p) >> (64 - B1)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NB1; i += PB) hist1[(uint64_t)blockIdx.x * NB1 + i] = h[i];
+}
+
+template <int W, bool REC>
+__global__ __launch_bounds__(PB) void k_part1_scatter(KParams p, const uint8_t* recs,
+                                                      const uint64_t* words, uint64_t n,
+                                                      const uint64_t* off1, uint64_t nb1,
+                                                      uint64_t* buf1) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* items = smem;                                              // PART_TILE * 2 words
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + PART_TILE * 2);  // PART_TILE
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);      // NB1
+    uint32_t* start = hist + NB1;                                        // NB1
+    uint64_t* gbase = reinterpret_cast<uint64_t*>(start + NB1);          // NB1 (8-B aligned)
+    for (int i = threadIdx.x; i < NB1; i += PB) gbase[i] = off1[(uint64_t)blockIdx.x * NB1 + i];
+    __syncthreads();
+    for (int tt = 0; tt < T1; ++tt) {
+        const uint64_t base = ((uint64_t)blockIdx.x * T1 + tt) * PART_TILE;
+        if (base >= n) break;  // uniform
+        uint64_t a[PITEMS], b[PITEMS];
+        load_tile<W, REC, PART_TILE>(p, recs, words, base, min(base + PART_TILE, n), nullptr,
+                                     reinterpret_cast<uint8_t*>(items), a, b);
+        uint32_t bin[PITEMS];
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j) bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - B1));
+        sorted_write<W, NB1>(a, b, bin, items, sbin, hist, start, gbase, buf1);
+        for (int i = threadIdx.x; i < NB1; i += PB) gbase[i] += hist[i];
+        __syncthreads();
+    }
+}
+
+// pass-1 offsets stored block-major: [block][bin]
+struct Off1Idx {
+    uint64_t nb;
+    __device__ uint64_t operator()(uint64_t i) const { return (i % nb) * NB1 + i / nb; }
+};
+
+struct Hist1F {
+    const uint64_t* hist;
+    uint64_t nb;
+    __device__ uint64_t operator()(uint64_t i) const { return hist[(i % nb) * NB1 + i / nb]; }
+};
+
+// ---- pass 2: bin = next 8 hash bits, within each pass-1 bucket ----------------------------------
+// bucket b starts at the offset of (block 0, bin b) = off1[b] in the block-major layout
+__device__ __forceinline__ void bucket_range(const uint64_t* off1, uint64_t nb1, uint64_t n, uint32_t b,
+                                             uint64_t& s, uint64_t& e) {
+    (void)nb1;
+    s = off1[b];
+    e = (b + 1 < (uint32_t)NB1) ? off1[b + 1] : n;
+}
+
+template <int W>
+__global__ __launch_bounds__(PB) void k_part2_hist(KParams p, const uint64_t* buf1, uint64_t n,
+                                                   const uint64_t* off1, uint64_t nb1, uint64_t G,
+                                                   uint64_t* hist2) {
+    __shared__ uint32_t h[NB2];
+    for (int i = threadIdx.x; i < NB2; i += PB) h[i] = 0;
+    __syncthreads();
+    const uint32_t bk = blockIdx.x / (uint32_t)G, g = blockIdx.x % (uint32_t)G;
+    uint64_t s, e;
+    bucket_range(off1, nb1, n, bk, s, e);
+    for (uint64_t t = s + (uint64_t)g * PART_TILE; t < e; t += G * PART_TILE) {
+        uint64_t a[PITEMS], b[PITEMS];
+        load_tile<W, false, PART_TILE>(p, nullptr, buf1, t, min(t + PART_TILE, e), nullptr, nullptr, a, b);
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j)
+            if (a[j] != EMPTY)
+                atomicAdd(&h[(words_hash<W>(a[j], b[j], p) >> (64 - RBITS)) & (NB2 - 1)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NB2; i += PB) hist2[(uint64_t)blockIdx.x * NB2 + i] = h[i];
+}
+
+template <int W>
+__global__ __launch_bounds__(PB) void k_part2_scatter(KParams p, const uint64_t* buf1, uint64_t n,
+                                                      const uint64_t* off1, uint64_t nb1, uint64_t G,
+                                                      const uint64_t* off2, uint64_t* buf2) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* items = smem;
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + PART_TILE * 2);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);
+    uint32_t* start = hist + NB1;
+    uint64_t* gbase = reinterpret_cast<uint64_t*>(start + NB1);
+    const uint32_t bk = blockIdx.x / (uint32_t)G, g = blockIdx.x % (uint32_t)G;
+    uint64_t s, e;
+    bucket_range(off1, nb1, n, bk, s, e);
+    for (int i = threadIdx.x; i < NB2; i += PB) gbase[i] = off2[((uint64_t)bk * G + g) * NB2 + i];
+    __syncthreads();
+    for (uint64_t t = s + (uint64_t)g * PART_TILE; t < e; t += G * PART_TILE) {
+        uint64_t a[PITEMS], b[PITEMS];
+        load_tile<W, false, PART_TILE>(p, nullptr, buf1, t, min(t + PART_TILE, e), nullptr, nullptr, a, b);
+        uint32_t bin[PITEMS];
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j)
+            bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - RBITS)) & (NB2 - 1);
+        sorted_write<W, NB2>(a, b, bin, items, sbin, hist, start, gbase, buf2);
+        // advance the running per-bin bases by this tile's counts (hist still holds them)
+        for (int i = threadIdx.x; i < NB2; i += PB) gbase[i] += hist[i];
+        __syncthreads();
+    }
+}
+
+// pass-2 offsets stored [bucket][block-in-bucket][bin]
+struct Off2Idx {
+    uint32_t G;
+    __device__ uint64_t operator()(uint64_t i) const {
+        const uint32_t x = (uint32_t)i, per = (uint32_t)NB2 * G;
+        const uint32_t bk = x / per, rem = x % per, f = rem / G, g = rem % G;
+        return ((uint64_t)bk * G + g) * NB2 + f;
+    }
+};
+
+// order (pass-1 bucket, pass-2 bin, block-in-bucket)
+struct Hist2F {
+    const uint64_t* hist;
+    uint32_t G;
+    __device__ uint64_t operator()(uint64_t i) const {
+        const uint32_t x = (uint32_t)i, per = (uint32_t)NB2 * G;
+        const uint32_t bk = x / per, rem = x % per, f = rem / G, g = rem % G;
+        return hist[((uint64_t)bk * G + g) * NB2 + f];
+    }
+};
+
+// ---- build ------------------------------------------------------------------------------------
+// LDS insert with linear probing inside the slice; false = the run left the slice.
+template <int W>
+__device__ __forceinline__ bool lds_insert(unsigned long long* lt, uint32_t S, uint64_t loc, uint64_t w0,
+                                           uint64_t w1, unsigned long long* stats) {
+    uint32_t spins = 0;
+    while (loc < S) {
+        const unsigned long long old = atomicCAS(&lt[W * loc], (unsigned long long)EMPTY, w0);
+        if (old == EMPTY) {
+            if (W == 2)
+                __hip_atomic_store(&lt[2 * loc + 1], (unsigned long long)w1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            return true;
+        }
+        if ((old >> 6) == (w0 >> 6)) {
+            if (W == 1) {
+                atomicAdd(&stats[ST_DUP], 1ull);
+                return true;
+            }
+            const unsigned long long o1 =
+                __hip_atomic_load(&lt[2 * loc + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (o1 == EMPTY) {  // the claiming lane has not stored word1 yet: retry this slot
+                if (++spins > (1u << 24)) {
+                    atomicAdd(&stats[ST_SPIN], 1ull);
+                    return true;
+                }
+                continue;
+            }
+            if (o1 == w1) {
+                atomicAdd(&stats[ST_DUP], 1ull);
+                return true;
+            }
+        }
+        ++loc;
+    }
+    return false;
+}
+
+template <int W>
+__global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const uint64_t* buf2, uint64_t n,
+                                                              const uint64_t* off2, uint64_t G,
+                                                              uint64_t* slots, uint64_t cap, int table_empty,
+                                                              uint64_t* ovf, uint64_t ovf_cap,
+                                                              unsigned long long* ctr,
+                                                              unsigned long long* stats) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
+    for (uint32_t r = blockIdx.x; r < NREG; r += gridDim.x) {
+        const uint64_t lo = mulhi64((uint64_t)r << (64 - RBITS), cap);
+        const uint64_t hi = (r + 1 < NREG) ? mulhi64((uint64_t)(r + 1) << (64 - RBITS), cap) : cap;
+        const uint32_t S = (uint32_t)(hi - lo);
+        if (W == 2) {
+            ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
+            const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
+                l2[i] = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
+                lt[i] = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
+        }
+        __syncthreads();
+        const uint64_t b = off2[(uint64_t)(r >> B2) * G * NB2 + (r & (NB2 - 1))];
+        const uint64_t e = (r + 1 < NREG) ? off2[(uint64_t)((r + 1) >> B2) * G * NB2 + ((r + 1) & (NB2 - 1))] : n;
+        for (uint64_t j = b + threadIdx.x; j < e; j += BUILD_THREADS) {
+            uint64_t w0, w1 = 0;
+            if (W == 2) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(buf2 + j * 2);
+                w0 = v.x;
+                w1 = v.y;
+            } else {
+                w0 = buf2[j];
+            }
+            const uint64_t home = home_slot(words_hash<W>(w0, w1, p), cap);
+            if (!lds_insert<W>(lt, S, home - lo, w0, w1, stats)) {
+                const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
+                if (idx < ovf_cap) {
+                    ovf[idx * W] = w0;
+                    if (W == 2) ovf[idx * W + 1] = w1;
+                } else {
+                    atomicAdd(&stats[ST_FULL], 1ull);
+                }
+            }
+        }
+        __syncthreads();
+        if (W == 2) {
+            ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
+            const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) dst[i] = l2[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) slots[lo + i] = lt[i];
+        }
+        __syncthreads();
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(PB) void k_insert_overflow(KParams p, const uint64_t* ovf, uint64_t ovf_cap,
+                                                        const unsigned long long* ctr, uint64_t* slots,
+                                                        uint64_t cap, unsigned long long* stats) {
+    const uint64_t m = min((uint64_t)ctr[CT_OVF], ovf_cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * PB + threadIdx.x; i < m; i += (uint64_t)gridDim.x * PB) {
+        const uint64_t w0 = ovf[i * W], w1 = (W == 2) ? ovf[i * W + 1] : 0;
+        insert_one<W>(slot_key(w0, w1, p), slot_ext(w0), p, slots, cap, stats);
+    }
+}
+
+template <class K>
+static hipError_t allow_lds(K kernel, size_t bytes) {
+    return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <int W, bool REC>
+static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
+                              TableView t, bool table_empty, const PartBuffers& B, uint64_t* start_mask,
+                              unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+    static bool attrs = false;  // per template instance
+    hipError_t e;
+    if (!attrs) {
+        if ((e = allow_lds(k_part1_scatter<W, false>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_part2_scatter<W>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_part_build<W>, LDS_BYTES)) != hipSuccess) return e;
+        attrs = true;
+    }
+    const PartPlan pl = part_plan(n);
+    const unsigned nb1 = (unsigned)pl.nb1;
+    if (REC) {
+        // records -> words (input order) in buf2, which pass 2 only writes after pass 1 is done
+        k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, B.hist1, start_mask);
+        words = B.buf2;
+    } else {
+        k_part1_hist<W, false><<<nb1, PB, 0, s>>>(p, nullptr, words, n, B.hist1, nullptr);
+    }
+    e = scan_exclusive(Hist1F{B.hist1, pl.nb1}, pl.nb1 * NB1, B.off1, B.scratch,
+                       (unsigned long long*)nullptr, (unsigned long long*)nullptr, s, Off1Idx{pl.nb1});
+    if (e != hipSuccess) return e;
+    k_part1_scatter<W, false><<<nb1, PB, SORT_LDS, s>>>(p, nullptr, words, n, B.off1, pl.nb1, B.buf1);
+    const unsigned nb2 = (unsigned)(NB1 * pl.G);
+    k_part2_hist<W><<<nb2, PB, 0, s>>>(p, B.buf1, n, B.off1, pl.nb1, pl.G, B.hist2);
+    e = scan_exclusive(Hist2F{B.hist2, (uint32_t)pl.G}, (uint64_t)NB1 * NB2 * pl.G, B.off2, B.scratch,
+                       (unsigned long long*)nullptr, (unsigned long long*)nullptr, s, Off2Idx{(uint32_t)pl.G});
+    if (e != hipSuccess) return e;
+    k_part2_scatter<W><<<nb2, PB, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.nb1, pl.G, B.off2, B.buf2);
+    if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
+    const size_t lds = (size_t)region_max_slots(t.cap) * W * 8;
+    k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, n, B.off2, pl.G, t.slots, t.cap,
+                                                     table_empty ? 1 : 0, B.overflow,
+                                                     part_overflow_cap(n), ctr, stats);
+    k_insert_overflow<W><<<1024, PB, 0, s>>>(p, B.overflow, part_overflow_cap(n), ctr, t.slots, t.cap,
+                                             stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
+                              TableView t, bool table_empty, const PartBuffers& b,
+                              uint64_t* start_mask, unsigned long long* ctr,
+                              unsigned long long* stats, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (recs) {
+        return p.W == 1 ? part_insert<1, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, ctr, stats, s)
+                        : part_insert<2, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, ctr, stats, s);
+    }
+    return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, ctr, stats, s)
+                    : part_insert<2, false>(p, nullptr, words, n, t, table_empty, b, nullptr, ctr, stats, s);
+}
+
+}  // namespace kh

@@ -4,6 +4,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -84,6 +85,9 @@ struct kh_table {
     DevBuf stage2, stage3;
     DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text;
     DevBuf route_hist, route_off, route_scratch;                          // sharded path
+    DevBuf pb_buf1, pb_buf2, pb_hist1, pb_off1, pb_hist2, pb_off2, pb_scratch, pb_ovf;  // part build
+    bool last_insert_part = false;
+    bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
     DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm;   // round walker
     uint64_t rw_n = 0, rw_total = 0;
     bool rw_live = false;
@@ -154,6 +158,46 @@ int check_stats(kh_table* t) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// Empty the slot array (all-ones) unless that already happened since the last clear.
+int clean_slots(kh_table* t) {
+    if (!t->slots_stale) return KH_OK;
+    KH_HIP(hipMemsetAsync(t->slots.p, 0xff, t->cap * (uint64_t)t->kp.W * 8, t->stream));
+    t->slots_stale = false;
+    return KH_OK;
+}
+
+// Insert strategy: KH_INSERT=cas (global CAS per key), part (partitioned LDS build), auto
+// (default: partitioned when the batch is large and the region slices fit LDS).
+bool use_part_build(const kh_table* t, uint64_t n) {
+    const char* m = getenv("KH_INSERT");
+    const bool usable = kh::part_usable(t->kp, t->cap, n);
+    if (m && !strcmp(m, "cas")) return false;
+    if (m && !strcmp(m, "part"))
+        return kh::region_slots_fit(t->kp, t->cap) && n > 0;
+    return usable;
+}
+
+int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
+    const kh::PartPlan pl = kh::part_plan(n);
+    const uint64_t W = (uint64_t)t->kp.W, hw = kh::part_hist_words(pl);
+    int rc;
+    if ((rc = t->pb_buf1.ensure(n * W * 8)) || (rc = t->pb_buf2.ensure(n * W * 8)) ||
+        (rc = t->pb_hist1.ensure(hw * 8)) || (rc = t->pb_off1.ensure(hw * 8)) ||
+        (rc = t->pb_hist2.ensure(hw * 8)) || (rc = t->pb_off2.ensure(hw * 8)) ||
+        (rc = t->pb_scratch.ensure(kh::part_scratch_words(pl) * 8)) ||
+        (rc = t->pb_ovf.ensure(kh::part_overflow_cap(n) * W * 8)))
+        return rc;
+    b.buf1 = t->pb_buf1.as<uint64_t>();
+    b.buf2 = t->pb_buf2.as<uint64_t>();
+    b.hist1 = t->pb_hist1.as<uint64_t>();
+    b.off1 = t->pb_off1.as<uint64_t>();
+    b.hist2 = t->pb_hist2.as<uint64_t>();
+    b.off2 = t->pb_off2.as<uint64_t>();
+    b.scratch = t->pb_scratch.as<uint64_t>();
+    b.overflow = t->pb_ovf.as<uint64_t>();
+    return KH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -219,7 +263,9 @@ int kh_destroy(kh_table* t) {
                       &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
                       &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->rw_hi, &t->rw_lo,
-                      &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm};
+                      &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm,
+                      &t->pb_buf1, &t->pb_buf2, &t->pb_hist1, &t->pb_off1, &t->pb_hist2,
+                      &t->pb_off2, &t->pb_scratch, &t->pb_ovf};
     for (auto* b : bufs) b->release();
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1};
     for (auto ev : evs)
@@ -232,7 +278,7 @@ int kh_destroy(kh_table* t) {
 int kh_clear(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (int rc = set_device(t)) return rc;
-    KH_HIP(hipMemsetAsync(t->slots.p, 0xff, t->cap * (uint64_t)t->kp.W * 8, t->stream));
+    t->slots_stale = true;
     KH_HIP(hipMemsetAsync(t->ctr.p, 0, kh::CT_NUM * 8, t->stream));
     KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
     t->n_inserted = 0;
@@ -271,9 +317,23 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     if ((rc = t->mask_off.ensure(nw * 8))) return rc;
     if ((rc = t->scratch.ensure(kh::scan_scratch_words(nw > n ? nw : n) * 8 + 64))) return rc;
     if ((rc = ensure_starts(t, t->n_inserted + n))) return rc;
+    const bool part = use_part_build(t, n);
+    kh::PartBuffers pb{};
+    if (part && (rc = ensure_part(t, n, pb))) return rc;
+    // a partitioned build into a fresh table rewrites every slot: no clear needed
+    const bool fresh = part && t->n_inserted == 0 && t->slots_stale;
+    if (!fresh && (rc = clean_slots(t))) return rc;
+    t->slots_stale = false;
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
-    KH_HIP(kh::launch_insert(t->kp, (const uint8_t*)dev_recs, n, view(t), t->mask.as<uint64_t>(),
-                             t->stats.as<unsigned long long>(), t->stream));
+    if (part)
+        KH_HIP(kh::launch_part_insert(t->kp, (const uint8_t*)dev_recs, nullptr, n, view(t),
+                                      fresh, pb, t->mask.as<uint64_t>(),
+                                      t->ctr.as<unsigned long long>(),
+                                      t->stats.as<unsigned long long>(), t->stream));
+    else
+        KH_HIP(kh::launch_insert(t->kp, (const uint8_t*)dev_recs, n, view(t), t->mask.as<uint64_t>(),
+                                 t->stats.as<unsigned long long>(), t->stream));
+    t->last_insert_part = part;
     KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
     KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
                                      t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
@@ -304,6 +364,7 @@ int kh_find_dev(kh_table* t, const void* dev_keys, uint64_t n, void* dev_out, vo
     if (n == 0) return KH_OK;
     if (!dev_keys || !dev_out || !dev_found) return fail(KH_ERR_ARG, "null buffer");
     if (int rc = set_device(t)) return rc;
+    if (int rc = clean_slots(t)) return rc;
     KH_HIP(kh::launch_find(t->kp, (const uint8_t*)dev_keys, n, view(t), (uint8_t*)dev_out,
                            (uint8_t*)dev_found, t->stream));
     return KH_OK;
@@ -346,6 +407,7 @@ int kh_set_starts(kh_table* t, const uint8_t* recs, uint64_t n) {
 int kh_assemble_dev(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (int rc = set_device(t)) return rc;
+    if (int rc = clean_slots(t)) return rc;
     int rc;
     uint64_t ns = 0;
     // The start count decides buffer sizes and the grid (the reference also knows
@@ -443,7 +505,8 @@ int kh_get_stats(kh_table* t, kh_stats* s) {
         s->out_bytes = ct[kh::CT_OUT_BYTES];
         // bytes = sum(K + len) -> lookups = sum(len - 1) = bytes - contigs * (K + 1)
         s->n_lookups = s->out_bytes - s->n_contigs * ((uint64_t)t->kp.K + 1);
-        s->n_chunks = ct[kh::CT_CHUNK_NEXT] < t->chunk_cap ? ct[kh::CT_CHUNK_NEXT] : t->chunk_cap;
+        const uint64_t nch = t->last_contigs + ct[kh::CT_CHUNK_NEXT];
+        s->n_chunks = nch < t->chunk_cap ? nch : t->chunk_cap;
     }
     s->n_dup = st[kh::ST_DUP];
     s->n_full = st[kh::ST_FULL];
@@ -564,9 +627,23 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
                     (unsigned long long)m, (unsigned long long)t->n_kmers,
                     (unsigned long long)t->n_inserted);
     if (int rc = set_device(t)) return rc;
+    const bool part = use_part_build(t, m);
+    kh::PartBuffers pb{};
+    if (part)
+        if (int rc = ensure_part(t, m, pb)) return rc;
+    const bool fresh = part && t->n_inserted == 0 && t->slots_stale;
+    if (!fresh)
+        if (int rc = clean_slots(t)) return rc;
+    t->slots_stale = false;
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
-    KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
-                                   t->stats.as<unsigned long long>(), t->stream));
+    if (part)
+        KH_HIP(kh::launch_part_insert(t->kp, nullptr, (const uint64_t*)words, m, view(t),
+                                      fresh, pb, nullptr, t->ctr.as<unsigned long long>(),
+                                      t->stats.as<unsigned long long>(), t->stream));
+    else
+        KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
+                                       t->stats.as<unsigned long long>(), t->stream));
+    t->last_insert_part = part;
     KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
     KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
     t->ins_timed = true;
@@ -578,6 +655,7 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
 int kh_walk_begin(kh_table* t, uint64_t total_kmers, uint64_t* n_walkers) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (int rc = set_device(t)) return rc;
+    if (int rc = clean_slots(t)) return rc;
     int rc;
     uint64_t ns = 0;
     if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
@@ -626,6 +704,7 @@ int kh_find_ext_dev(kh_table* t, const void* keys, uint64_t m, void* ext_out) {
     if (m == 0) return KH_OK;
     if (!keys || !ext_out) return fail(KH_ERR_ARG, "null buffer");
     if (int rc = set_device(t)) return rc;
+    if (int rc = clean_slots(t)) return rc;
     KH_HIP(kh::launch_find_ext(t->kp, (const uint64_t*)keys, m, view(t), (uint8_t*)ext_out, t->stream));
     return KH_OK;
 }

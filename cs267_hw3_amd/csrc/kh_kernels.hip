@@ -12,209 +12,12 @@
 // Everything is integer work bound by HBM random access; there is no MFMA on this path.
 #include <hip/hip_runtime.h>
 
+#include "kh_device.hpp"
 #include "kh_kernels.hpp"
 
 namespace kh {
 
-static constexpr int BLOCK = 256;
-static constexpr int SCAN_ITEMS = 8;
-static constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;  // 2048 elements per block
-static constexpr int WALK_GRAB = 64;                   // start k-mers per work-queue pull
-static constexpr int MAX_R = 17;                       // K <= 60 -> PACKED <= 15 -> R <= 17
-
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
-
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// ---------------------------------------------------------------------------------------------
-// Block-wide exclusive scan of one uint64 per thread (256 threads = 4 waves of 64).
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total) {
-    __shared__ uint64_t wsum[BLOCK / 64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint64_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    uint64_t pre = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < BLOCK / 64; ++i) {
-        if (i < w) pre += wsum[i];
-        tot += wsum[i];
-    }
-    __syncthreads();
-    total = tot;
-    return pre + x - v;
-}
-
-struct PopcF {
-    const uint64_t* mask;
-    __device__ uint64_t operator()(uint64_t i) const { return (uint64_t)__popcll(mask[i]); }
-};
-
-struct ContigBytesF {
-    const uint32_t* len;
-    uint64_t K;
-    __device__ uint64_t operator()(uint64_t i) const { return K + (uint64_t)len[i]; }
-};
-
-template <class F>
-__global__ __launch_bounds__(BLOCK) void k_scan_reduce(F f, uint64_t m, uint64_t* bsum) {
-    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
-    uint64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_ITEMS; ++j)
-        if (b0 + j < m) s += f(b0 + j);
-    uint64_t tot;
-    block_excl_scan(s, tot);
-    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
-}
-
-// One block: exclusive scan of the nb block sums in place, starting at *base (if given);
-// *base (if given) and *total_out (if given) receive base + sum.
-__global__ __launch_bounds__(BLOCK) void k_scan_top(uint64_t* bsum, uint64_t nb,
-                                                    unsigned long long* base,
-                                                    unsigned long long* total_out) {
-    uint64_t carry = base ? (uint64_t)*base : 0ull;
-    for (uint64_t c0 = 0; c0 < nb; c0 += SCAN_TILE) {
-        const uint64_t i0 = c0 + (uint64_t)threadIdx.x * SCAN_ITEMS;
-        uint64_t v[SCAN_ITEMS];
-        uint64_t s = 0;
-#pragma unroll
-        for (int j = 0; j < SCAN_ITEMS; ++j) {
-            v[j] = (i0 + j < nb) ? bsum[i0 + j] : 0ull;
-            s += v[j];
-        }
-        uint64_t tot;
-        uint64_t pre = block_excl_scan(s, tot) + carry;
-#pragma unroll
-        for (int j = 0; j < SCAN_ITEMS; ++j) {
-            if (i0 + j < nb) bsum[i0 + j] = pre;
-            pre += v[j];
-        }
-        carry += tot;
-    }
-    if (threadIdx.x == 0) {
-        if (base) *base = carry;
-        if (total_out) *total_out = carry;
-    }
-}
-
-template <class F>
-__global__ __launch_bounds__(BLOCK) void k_scan_apply(F f, uint64_t m, const uint64_t* bsum,
-                                                      uint64_t* out) {
-    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
-    uint64_t v[SCAN_ITEMS];
-    uint64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_ITEMS; ++j) {
-        v[j] = (b0 + j < m) ? f(b0 + j) : 0ull;
-        s += v[j];
-    }
-    uint64_t tot;
-    uint64_t pre = block_excl_scan(s, tot) + bsum[blockIdx.x];
-#pragma unroll
-    for (int j = 0; j < SCAN_ITEMS; ++j) {
-        if (b0 + j < m) out[b0 + j] = pre;
-        pre += v[j];
-    }
-}
-
 uint64_t scan_scratch_words(uint64_t m) { return (m + SCAN_TILE - 1) / SCAN_TILE + 1; }
-
-template <class F>
-static hipError_t scan_exclusive(F f, uint64_t m, uint64_t* out, uint64_t* scratch,
-                                 unsigned long long* base, unsigned long long* total,
-                                 hipStream_t s) {
-    if (m == 0) return hipSuccess;
-    const uint64_t nb = (m + SCAN_TILE - 1) / SCAN_TILE;
-    k_scan_reduce<F><<<dim3((unsigned)nb), dim3(BLOCK), 0, s>>>(f, m, scratch);
-    k_scan_top<<<1, BLOCK, 0, s>>>(scratch, nb, base, total);
-    k_scan_apply<F><<<dim3((unsigned)nb), dim3(BLOCK), 0, s>>>(f, m, scratch, out);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// Insert. One record per lane; a block stages 256 records (256*R contiguous bytes, 16-B aligned)
-// through LDS with dwordx4 loads so the 15-byte (k=51) / 7-byte (k=19) records are read fully
-// coalesced, then parses them from LDS.
-//
-// W=2 publish protocol (no 128-bit CAS on gfx950): CAS word0 (hi bits + ext) from EMPTY, then
-// atomically store word1 (lo bits). A prober whose word0 matches ours must see word1 before it
-// can decide; it re-reads word1 with an atomic (coherent across XCD L2s) on its next loop
-// iteration — never spinning inside the branch, so a writer lane in the same wave always
-// completes its store first.
-// Probing reads slots with plain loads and spends an atomic only on a slot that looked EMPTY
-// (a stale EMPTY just makes the CAS fail and return the live word; a live word never changes,
-// so a plain read of one is never wrong). Word1 is published with a write-through (sc1) store.
-template <int W>
-__device__ __forceinline__ void load_slot(const uint64_t* slots, uint64_t s, uint64_t& w0,
-                                          uint64_t& w1) {
-    if (W == 2) {
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(slots + 2 * s);
-        w0 = v.x;
-        w1 = v.y;
-    } else {
-        w0 = slots[s];
-        w1 = 0;
-    }
-}
-
-template <int W>
-__device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p, uint64_t* slots,
-                                           uint64_t cap, unsigned long long* stats) {
-    unsigned long long* S = reinterpret_cast<unsigned long long*>(slots);
-    const unsigned long long w0 = slot_w0(k, ext, p);
-    const unsigned long long w1 = k.lo;
-    uint64_t s = home_slot(key_hash(k), cap);
-    uint64_t probes = 0;
-    uint32_t spins = 0;
-    uint64_t c0, c1;
-    load_slot<W>(slots, s, c0, c1);
-    while (true) {
-        if (c0 == EMPTY) {
-            const unsigned long long old = atomicCAS(&S[W * s], (unsigned long long)EMPTY, w0);
-            if (old == EMPTY) {
-                if (W == 2)
-                    __hip_atomic_store(&S[2 * s + 1], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return;
-            }
-            c0 = old;
-            c1 = EMPTY;  // unknown: re-read coherently below if needed
-        }
-        if ((c0 >> 6) == (w0 >> 6)) {
-            if (W == 1) {
-                atomicAdd(&stats[ST_DUP], 1ull);
-                return;
-            }
-            if (c1 == EMPTY)
-                c1 = atomicCAS(&S[2 * s + 1], (unsigned long long)EMPTY, (unsigned long long)EMPTY);
-            if (c1 == EMPTY) {
-                if (++spins > (1u << 26)) {
-                    atomicAdd(&stats[ST_SPIN], 1ull);
-                    return;
-                }
-                continue;  // word1 not yet published: re-read it on the next iteration
-            }
-            if (c1 == w1) {
-                atomicAdd(&stats[ST_DUP], 1ull);
-                return;
-            }
-        }
-        if (++probes >= cap) {
-            atomicAdd(&stats[ST_FULL], 1ull);
-            return;
-        }
-        s = (s + 1 == cap) ? 0 : s + 1;
-        load_slot<W>(slots, s, c0, c1);
-    }
-}
 
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_insert(KParams p, const uint8_t* __restrict__ recs,
@@ -334,29 +137,6 @@ hipError_t launch_load_starts(const KParams& p, const uint8_t* recs, uint64_t n,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Probe: returns true and the slot's word0 if the key is present. Table is read-only here
-// (written by an earlier kernel), so plain 8/16-byte loads are coherent. Both words feed the
-// hit test unconditionally so the compiler keeps ONE dwordx4 per probe (a short-circuit on
-// word0 made it split the slot into two dependent dwordx2 round trips).
-template <int W>
-__device__ __forceinline__ bool probe(Key k, const KParams& p, const uint64_t* __restrict__ slots,
-                                      uint64_t cap, uint64_t& w0_out) {
-    uint64_t s = home_slot(key_hash(k), cap);
-    const uint64_t want0 = (W == 1) ? k.lo : k.hi;
-    for (uint64_t probes = 0; probes < cap; ++probes) {
-        uint64_t w0, w1;
-        load_slot<W>(slots, s, w0, w1);
-        const bool empty = w0 == EMPTY;
-        const bool hit = !empty & ((w0 >> 6) == want0) & ((W == 1) | (w1 == k.lo));
-        if (hit | empty) {
-            w0_out = w0;
-            return hit;
-        }
-        s = (s + 1 == cap) ? 0 : s + 1;
-    }
-    return false;
-}
-
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_find(KParams p, const uint8_t* keys, uint64_t n,
                                                 const uint64_t* slots, uint64_t cap, uint8_t* out,

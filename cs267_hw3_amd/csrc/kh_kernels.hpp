@@ -25,6 +25,7 @@ enum CtrIdx : int {
     CT_WALK_NEXT = 1,  // walker work-queue head
     CT_CHUNK_NEXT = 2, // chunk allocator head
     CT_OUT_BYTES = 3,  // total contig bytes (incl. '\n')
+    CT_OVF = 4,        // partitioned build: keys whose probe run left their region
     CT_NUM = 8
 };
 
@@ -134,5 +135,48 @@ hipError_t launch_find_ext(const KParams& p, const uint64_t* keys, uint64_t m, T
 // Home side: apply the replies of the m queries emitted last round.
 hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t* ext, uint64_t m,
                            unsigned long long* stats, hipStream_t s);
+
+}  // namespace kh
+
+// ---- partitioned (atomic-free) bulk build ------------------------------------------------------
+namespace kh {
+
+// The key space is cut into 2^17 hash ranges (top 17 bits of key_hash); because the home slot
+// mulhi(h, cap) is monotonic in h, region r owns the slot range
+// [floor(r*cap/2^17), floor((r+1)*cap/2^17)). Two radix passes (512 x 256 bins) group the batch by
+// region, then one workgroup per region builds its slot range in LDS (kh_build.hip).
+static constexpr int PART_TILE = 4096;  // inputs per block-tile of the radix passes
+
+struct PartPlan {
+    uint64_t n;       // inputs
+    uint64_t nb1;     // pass-1 blocks
+    uint64_t G;       // pass-2 blocks per bucket
+};
+PartPlan part_plan(uint64_t n);
+uint64_t part_hist_words(const PartPlan& pl);     // words of each hist / offset buffer
+uint64_t part_scratch_words(const PartPlan& pl);  // words of scan scratch (+ one total word)
+uint64_t part_overflow_cap(uint64_t n);           // overflow entries
+// True when the region slices fit LDS and the batch is large enough to be worth it.
+bool part_usable(const KParams& p, uint64_t cap, uint64_t n);
+// True when every region slice fits LDS (forced partitioned mode for tests of small batches).
+bool region_slots_fit(const KParams& p, uint64_t cap);
+
+struct PartBuffers {
+    uint64_t* buf1;      // n * W words
+    uint64_t* buf2;      // n * W words
+    uint64_t* hist1;
+    uint64_t* off1;
+    uint64_t* hist2;
+    uint64_t* off2;
+    uint64_t* scratch;
+    uint64_t* overflow;  // part_overflow_cap(n) * W words
+};
+
+// Build: input is either reference records (recs, R bytes each; start bits -> start_mask) or
+// internal words (words, W each). table_empty: skip loading the current region contents.
+hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words,
+                              uint64_t n, TableView t, bool table_empty, const PartBuffers& b,
+                              uint64_t* start_mask, unsigned long long* ctr,
+                              unsigned long long* stats, hipStream_t s);
 
 }  // namespace kh

@@ -191,3 +191,40 @@ def test_c3_shape_vs_truth_30m():
     _, got, nc = run(51, recs)
     assert nc == g.num_contigs
     assert got == g.truth()
+
+
+# ---- both insert strategies (KH_INSERT=cas: global CAS per key; part: partitioned LDS build) ----
+@pytest.fixture(params=["cas", "part"])
+def insert_mode(request, monkeypatch):
+    monkeypatch.setenv("KH_INSERT", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("name", ["mixed19", "small51", "k29", "k30", "k60", "singles51"])
+@pytest.mark.parametrize("batches", [1, 3])
+def test_golden_both_insert_paths(insert_mode, name, batches):
+    k, recs, want = golden(name)
+    t, got, _ = run(k, recs, batches=batches)
+    assert got == want
+    assert t.stats()["n_dup"] == 0
+
+
+@pytest.mark.parametrize("k,n,batches", [(51, 3_000_000, 1), (51, 3_000_000, 2), (19, 2_000_000, 1),
+                                         (31, 2_000_000, 3)])
+def test_generated_both_insert_paths(insert_mode, k, n, batches):
+    g = kh.SyntheticKmers(k, n, 8, 300, 10, seed=k * 7 + batches)
+    t, got, nc = run(k, g.records(), batches=batches)
+    assert got == g.truth() and nc == g.num_contigs
+    assert t.stats()["n_dup"] == 0
+
+
+def test_part_build_detects_duplicates(monkeypatch):
+    monkeypatch.setenv("KH_INSERT", "part")
+    g = kh.SyntheticKmers(51, 2_000_000, 8, 200, 0, seed=3)
+    recs = g.records()
+    dup = np.concatenate([recs, recs[:1000]])
+    t = kh.KmerHashTable(51, len(dup))
+    with pytest.raises(kh.KmerHashError) as e:
+        t.insert_all(dup)
+    assert e.value.code == _lib.KH_ERR_DUPLICATE
+    assert t.stats()["n_dup"] == 1000
