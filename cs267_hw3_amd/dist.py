@@ -195,28 +195,66 @@ class DistributedKmerHashMap:
     def _int64(self, like, n):
         return torch.empty(max(int(n), 1), dtype=torch.int64, device=like.device)
 
-    def _exchange_counts(self, counts):
-        """counts: [P+1] int64 (per-destination, total) -> (send_splits, recv_splits, totals)."""
+    # RCCL as shipped with this torch build corrupts all_to_all_single messages of >= 2 GiB per
+    # peer (tools/dbg_a2a.py: half the elements wrong at 2.0 and 3.2 GiB, exact at 1 GiB), so no
+    # single call moves more than A2A_CHUNK_BYTES per peer.
+    A2A_CHUNK_BYTES = 512 << 20
+
+    def _exchange_counts(self, counts, elems_per_item=1):
+        """counts: [P+1] int64 (per-destination, total) -> (send_splits, recv_splits, totals,
+        global max per-peer split). One small all-to-all; each rank also learns every rank's
+        total (global termination) and largest split (chunk count), no extra all-reduce."""
         P = self.P
-        send = torch.stack([counts[:P], counts[P:P + 1].expand(P)], 1).contiguous().view(-1)
+        mx = counts[:P].max().reshape(1)
+        send = torch.stack([counts[:P], counts[P:P + 1].expand(P), mx.expand(P)], 1)
+        send = send.contiguous().view(-1)
         recv = torch.empty_like(send)
-        self.comm.all_to_all(recv, send, [2] * P, [2] * P)
-        host = torch.cat([send, recv]).cpu().view(2, P, 2)
+        self.comm.all_to_all(recv, send, [3] * P, [3] * P)
+        host = torch.cat([send, recv]).cpu().view(2, P, 3)
         send_splits = host[0, :, 0].tolist()
         recv_splits = host[1, :, 0].tolist()
         totals = host[1, :, 1].tolist()
-        return send_splits, recv_splits, totals
+        gmax = int(host[1, :, 2].max())
+        return send_splits, recv_splits, totals, gmax
+
+    def _all_to_all(self, out, inp, out_splits, in_splits, gmax_elems):
+        """all_to_all_single in chunks of at most A2A_CHUNK_BYTES per peer. gmax_elems is the
+        largest per-peer split over ALL ranks, so every rank runs the same number of calls."""
+        limit = max(1, self.A2A_CHUNK_BYTES // inp.element_size())
+        rounds = (gmax_elems + limit - 1) // limit
+        if rounds <= 1:
+            self.comm.all_to_all(out, inp, out_splits, in_splits)
+            return
+        P = self.P
+        in_off = [0] * P
+        out_off = [0] * P
+        for q in range(1, P):
+            in_off[q] = in_off[q - 1] + in_splits[q - 1]
+            out_off[q] = out_off[q - 1] + out_splits[q - 1]
+        for r in range(rounds):
+            lo = r * limit
+            sc = [max(0, min(limit, in_splits[q] - lo)) for q in range(P)]
+            rc = [max(0, min(limit, out_splits[q] - lo)) for q in range(P)]
+            parts = [inp[in_off[q] + lo:in_off[q] + lo + sc[q]] for q in range(P) if sc[q]]
+            send = torch.cat(parts) if parts else inp[:0]
+            recv = torch.empty(sum(rc), dtype=out.dtype, device=out.device)
+            self.comm.all_to_all(recv, send, rc, sc)
+            pos = 0
+            for q in range(P):
+                if rc[q]:
+                    out[out_off[q] + lo:out_off[q] + lo + rc[q]].copy_(recv[pos:pos + rc[q]])
+                    pos += rc[q]
 
     def insert_all(self, recs):
         sh, P = self.shard, self.P
         sh.collect_starts(recs)
         words, counts = sh.route(recs, P)
-        send_splits, recv_splits, _ = self._exchange_counts(counts)
+        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
         W = sh.W
         m = sum(recv_splits)
         recv = self._int64(words, m * W)
-        self.comm.all_to_all(recv[:m * W] if m else recv[:0], words[:sum(send_splits) * W],
-                             [c * W for c in recv_splits], [c * W for c in send_splits])
+        self._all_to_all(recv[:m * W], words[:sum(send_splits) * W],
+                         [c * W for c in recv_splits], [c * W for c in send_splits], gmax * W)
         sh.insert_words(recv, m)
         return m
 
@@ -226,17 +264,17 @@ class DistributedKmerHashMap:
         self.rounds = 0
         while True:
             keys, counts = sh.walk_emit(P)
-            send_splits, recv_splits, totals = self._exchange_counts(counts)
+            send_splits, recv_splits, totals, gmax = self._exchange_counts(counts)
             if sum(totals) == 0:
                 break
             self.rounds += 1
             ms, mr = sum(send_splits), sum(recv_splits)
             qin = self._int64(keys, mr * W)
-            self.comm.all_to_all(qin[:mr * W], keys[:ms * W], [c * W for c in recv_splits],
-                                 [c * W for c in send_splits])
+            self._all_to_all(qin[:mr * W], keys[:ms * W], [c * W for c in recv_splits],
+                             [c * W for c in send_splits], gmax * W)
             ext = sh.find_ext(qin, mr)
             rep = torch.empty(max(ms, 1), dtype=torch.uint8, device=ext.device)
-            self.comm.all_to_all(rep[:ms], ext[:mr], send_splits, recv_splits)
+            self._all_to_all(rep[:ms], ext[:mr], send_splits, recv_splits, gmax)
             sh.walk_apply(rep, ms)
         sh.walk_end()
         sh.sync()

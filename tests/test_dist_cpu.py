@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, name, outdir):
+def _rank_main(rank, world, port, name, outdir, chunk_bytes=None):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -35,6 +35,8 @@ def _rank_main(rank, world, port, name, outdir):
     k = MANIFEST[name]["k"]
     recs = kh.read_kmers(os.path.join(GOLDEN, f"{name}.txt"), k, world, rank)
     dm = DistributedKmerHashMap(TorchComm(), FakeShard(k))
+    if chunk_bytes:
+        dm.A2A_CHUNK_BYTES = chunk_bytes   # force the chunked all-to-all path
     dm.insert_all(torch.from_numpy(recs))
     rounds = dm.assemble(MANIFEST[name]["n"])
     with open(os.path.join(outdir, f"test_{rank}.dat"), "wb") as f:
@@ -45,11 +47,12 @@ def _rank_main(rank, world, port, name, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world", [("mixed19", 2), ("small51", 2), ("singles51", 2),
-                                        ("small51", 3)])
-def test_sharded_driver_gloo(tmp_path, name, world):
-    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+@pytest.mark.parametrize("name,world,chunk", [("mixed19", 2, None), ("small51", 2, None),
+                                              ("singles51", 2, None), ("small51", 3, None),
+                                              ("small51", 3, 64), ("mixed19", 2, 1000)])
+def test_sharded_driver_gloo(tmp_path, name, world, chunk):
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), chunk),
+                       nprocs=world, join=True, start_method="spawn")
     import cs267_hw3_amd as kh
     m = MANIFEST[name]
     g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"],

@@ -40,3 +40,18 @@ def test_driver_rejects_wrong_k(tmp_path):
     r = subprocess.run([exe, os.path.join(GOLDEN, "tiny19.txt")], cwd=tmp_path,
                        capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "19-mers" in r.stderr
+
+
+@pytest.mark.gpu
+def test_dist_launcher_one_rank(tmp_path):
+    """cs267_hw3_amd.kmer_hash_dist under torchrun (1 rank, RCCL): same test_0.dat."""
+    import sys
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+                        "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port",
+                        "29533", "-m", "cs267_hw3_amd.kmer_hash_dist",
+                        os.path.join(GOLDEN, "small51.txt"), "test", "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = open(tmp_path / "out_0.dat", "rb").read()
+    assert got == open(os.path.join(GOLDEN, "small51_test_0.dat"), "rb").read()

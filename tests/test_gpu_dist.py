@@ -51,3 +51,30 @@ def test_sharded_missing_kmer_raises():
     interior = np.where((recs[:, P] != ord("F")) & (recs[:, P + 1] != ord("F")))[0][5]
     with pytest.raises(kh.KmerHashError):
         run_threaded(19, np.delete(recs, interior, axis=0), 2)
+
+
+@pytest.mark.parametrize("mode", ["cas", "part"])
+@pytest.mark.parametrize("P", [1, 2])
+def test_sharded_large_both_insert_paths(monkeypatch, mode, P):
+    """>= 1M routed words per rank: the partitioned build consumes words, not records."""
+    from cs267_hw3_amd.dist import run_threaded
+    monkeypatch.setenv("KH_INSERT", mode)
+    g = kh.SyntheticKmers(51, 2_500_000 * P, 8, 200, 0, seed=77 + P)
+    texts = run_threaded(51, g.records(), P)
+    check_ranks(g, texts, P)
+
+
+@pytest.mark.parametrize("mode", ["cas", "part"])
+def test_insert_words_direct(monkeypatch, mode):
+    import torch
+    from cs267_hw3_amd.dist import GpuShard
+    monkeypatch.setenv("KH_INSERT", mode)
+    g = kh.SyntheticKmers(51, 3_000_000, 8, 200, 0, seed=5)
+    sh = GpuShard(51, 3_000_000)
+    with torch.cuda.stream(sh.stream):
+        recs = torch.from_numpy(g.records()).cuda()
+        words, counts = sh.route(recs, 1)
+        sh.insert_words(words, recs.shape[0])
+        sh.sync()
+    s = sh.stats()
+    assert s["n_dup"] == 0 and s["n_inserted"] == 3_000_000

@@ -15,7 +15,12 @@ import json
 import os
 import sys
 
-KERNELS = {"k_insert": "k_insert<", "k_walk": "k_walk<"}
+KERNELS = {"k_insert": "k_insert<", "k_walk": "k_walk<", "k_part1_convert": "k_part1_convert<",
+           "k_part1_scatter": "k_part1_scatter<", "k_part2_hist": "k_part2_hist<",
+           "k_part2_scatter": "k_part2_scatter<", "k_part_build": "k_part_build<",
+           "k_insert_overflow": "k_insert_overflow<"}
+PIPELINE = ["k_part1_convert", "k_part1_scatter", "k_part2_hist", "k_part2_scatter", "k_part_build",
+            "k_insert_overflow"]
 
 
 def per_kernel(counter, prefix):
@@ -47,6 +52,8 @@ def main():
     for k in KERNELS:
         if k in fetch and k in write:
             e[k] = 2 * fetch[k] * 1024 + write[k] * 1024
+    if all(k in e for k in PIPELINE):
+        e["insert_pipeline"] = sum(e[k] for k in PIPELINE)
     doc[workload] = e
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
