@@ -671,7 +671,7 @@ int kh_walk_begin(kh_table* t, uint64_t total_kmers, uint64_t* n_walkers) {
     const uint64_t nn = ns + 1;
     if ((rc = t->rw_hi.ensure(nn * 8)) || (rc = t->rw_lo.ensure(nn * 8)) || (rc = t->rw_buf.ensure(nn * 8)) ||
         (rc = t->rw_steps.ensure(nn * 4)) || (rc = t->rw_chunk.ensure(nn * 4)) ||
-        (rc = t->rw_state.ensure(nn)) || (rc = t->rw_qperm.ensure(nn * 4)))
+        (rc = t->rw_state.ensure((nn + 7) & ~7ull)) || (rc = t->rw_qperm.ensure(nn * 4)))
         return rc;
     t->chunk_cap = chunk_cap;
     t->rw_n = ns;
@@ -741,6 +741,50 @@ int kh_walk_end_dev(kh_table* t) {
     t->last_contigs = t->rw_n;
     t->assembled = true;
     t->rw_live = false;
+    return KH_OK;
+}
+
+int kh_walk_emit_fixed_dev(kh_table* t, int nranks, uint64_t cap, void* send, void* qperm) {
+    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
+    if (!send || !qperm || cap == 0) return fail(KH_ERR_ARG, "null buffer / zero capacity");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = t->route_scratch.ensure((kh::MAX_RANKS + 2) * 8)) return rc;
+    KH_HIP(kh::launch_rw_emit_fixed(t->kp, round_walk(t), (uint32_t)nranks, cap, (uint64_t*)send,
+                                    (uint32_t*)qperm, t->route_scratch.as<unsigned long long>(),
+                                    t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(),
+                                    t->stream));
+    return KH_OK;
+}
+
+int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* recv, void* reply) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
+    if (!recv || !reply) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = clean_slots(t)) return rc;
+    KH_HIP(kh::launch_find_ext_fixed(t->kp, (const uint64_t*)recv, (uint32_t)nranks, cap, view(t),
+                                     (uint8_t*)reply, t->stream));
+    return KH_OK;
+}
+
+int kh_walk_apply_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* send, const void* qperm,
+                            const void* reply) {
+    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
+    if (!send || !qperm || !reply) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_rw_apply_fixed(t->kp, round_walk(t), (uint32_t)nranks, cap, (const uint64_t*)send,
+                                     (const uint32_t*)qperm, (const uint8_t*)reply,
+                                     t->stats.as<unsigned long long>(), t->stream));
+    return KH_OK;
+}
+
+int kh_walk_active_dev(kh_table* t, void* out) {
+    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
+    if (!out) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_count_active(round_walk(t), (unsigned long long*)out, t->stream));
     return KH_OK;
 }
 

@@ -718,5 +718,202 @@ hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t*
     return hipGetLastError();
 }
 
+// ---- fixed-capacity rounds ------------------------------------------------------------------
+// Every round exchanges fixed-size per-peer segments, so the host never waits for counts:
+//   send/recv: P segments of L = 1 + C*W words: [count, key_0 .. key_{C-1}]
+//   replies:   P segments of C bytes (ext byte, 0xFF = absent)
+// A walker whose query does not fit its owner's segment this round keeps its state and
+// simply emits again next round.
+__device__ __forceinline__ void apply_reply(const RoundWalk& rw, uint32_t i, uint8_t r,
+                                            unsigned long long* stats) {
+    const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
+    if (r == 0xFF) {
+        atomicAdd(&stats[ST_MISSING], 1ull);
+        finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
+        rw.state[i] = RW_DONE;
+    } else if (rw.steps[i] > rw.max_steps) {
+        atomicAdd(&stats[ST_CYCLE], 1ull);
+        finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
+        rw.state[i] = RW_DONE;
+    } else {
+        const uint32_t f = ext_fwd(r);
+        rw.state[i] = (uint8_t)(f > 4 ? RW_BAD : f);
+    }
+}
+
+// One tile = EMIT_IPT walkers per thread: per-owner counts are aggregated in LDS over the whole
+// tile so a round makes one cursor atomicAdd per (tile, owner). Same-address device-scope
+// atomics serialise at the memory side across the 8 XCDs (~12 ns each, measured: one atomic per
+// 256-walker block cost ~100 us/round at 1.9M walkers).
+static constexpr int EMIT_IPT = 16;
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_rw_emit_fixed(KParams p, RoundWalk rw, uint32_t P, uint64_t C,
+                                                         uint64_t* send, uint32_t* qperm,
+                                                         unsigned long long* cursors,
+                                                         unsigned long long* ctr,
+                                                         unsigned long long* stats) {
+    __shared__ uint32_t lc[MAX_RANKS];
+    __shared__ uint64_t base[MAX_RANKS];
+    const uint64_t L = 1 + C * W;
+    const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
+    constexpr uint64_t TILE = (uint64_t)BLOCK * EMIT_IPT;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < rw.n; t0 += (uint64_t)gridDim.x * TILE) {
+        for (uint32_t q = threadIdx.x; q < P; q += BLOCK) lc[q] = 0;
+        __syncthreads();
+        Key nk[EMIT_IPT];
+        int8_t qo[EMIT_IPT];
+        uint32_t lr[EMIT_IPT];
+#pragma unroll
+        for (int j = 0; j < EMIT_IPT; ++j) {
+            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+            uint8_t st = i < rw.n ? rw.state[i] : RW_DONE;
+            qo[j] = -1;
+            lr[j] = 0;
+            nk[j] = Key{0, 0};
+            if (st == RW_F || st == RW_BAD) {
+                if (st == RW_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+                finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
+                rw.state[i] = RW_DONE;
+            } else if (st <= 3) {
+                nk[j] = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
+                const uint32_t q = owner_of(key_hash(nk[j]), P);
+                qo[j] = (int8_t)q;
+                lr[j] = atomicAdd(&lc[q], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t r = threadIdx.x; r < P; r += BLOCK)
+            base[r] = lc[r] ? atomicAdd(&cursors[r], (unsigned long long)lc[r]) : 0ull;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < EMIT_IPT; ++j) {
+            if (qo[j] < 0) continue;
+            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+            const uint32_t q = (uint32_t)qo[j];
+            const uint64_t slot = base[q] + lr[j];
+            if (slot >= C) continue;  // owner's segment full: retry next round
+            uint32_t steps = rw.steps[i], chunk = rw.chunk[i];
+            uint64_t buf = rw.buf[i];
+            append_base(o, i, rw.state[i], steps, chunk, buf, ctr, stats);
+            rw.steps[i] = steps;
+            rw.chunk[i] = chunk;
+            rw.buf[i] = buf;
+            rw.hi[i] = nk[j].hi;
+            rw.lo[i] = nk[j].lo;
+            rw.state[i] = RW_PENDING;
+            uint64_t* seg = send + (uint64_t)q * L + 1 + slot * W;
+            if (W == 2) {
+                seg[0] = nk[j].hi;
+                seg[1] = nk[j].lo;
+            } else {
+                seg[0] = nk[j].lo;
+            }
+            qperm[(uint64_t)q * C + slot] = (uint32_t)i;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_fixed_headers(uint64_t* send, uint32_t P, uint64_t L, uint64_t C,
+                                const unsigned long long* cursors) {
+    for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) {
+        const uint64_t c = cursors[q];
+        send[(uint64_t)q * L] = c < C ? c : C;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_find_ext_fixed(KParams p, const uint64_t* __restrict__ recv,
+                                                          uint32_t P, uint64_t C, const uint64_t* slots,
+                                                          uint64_t cap, uint8_t* reply) {
+    const uint64_t L = 1 + C * W;
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < (uint64_t)P * C;
+         j += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t q = j / C, slot = j % C;
+        const uint64_t* seg = recv + q * L;
+        if (slot >= seg[0]) continue;
+        Key k;
+        if (W == 2) {
+            k.hi = seg[1 + slot * 2];
+            k.lo = seg[2 + slot * 2];
+        } else {
+            k.hi = 0;
+            k.lo = seg[1 + slot];
+        }
+        uint64_t w0 = 0;
+        reply[j] = probe<W>(k, p, slots, cap, w0) ? (uint8_t)slot_ext(w0) : (uint8_t)0xFF;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rw_apply_fixed(RoundWalk rw, uint32_t P, uint64_t C, uint64_t L,
+                                                          const uint64_t* send, const uint32_t* qperm,
+                                                          const uint8_t* reply, unsigned long long* stats) {
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < (uint64_t)P * C;
+         j += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t q = j / C, slot = j % C;
+        if (slot >= send[q * L]) continue;
+        apply_reply(rw, qperm[j], reply[j], stats);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_count_active(RoundWalk rw, unsigned long long* out) {
+    uint64_t c = 0;
+    const uint64_t nw = (rw.n + 7) / 8;  // state bytes, 8 per load (buffer padded to 8)
+    const uint64_t* st8 = reinterpret_cast<const uint64_t*>(rw.state);
+    for (uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t v = st8[w];
+        const uint64_t rem = rw.n - w * 8;
+        const uint32_t lim = rem < 8 ? (uint32_t)rem : 8u;
+        for (uint32_t b = 0; b < lim; ++b) c += ((v >> (8 * b)) & 0xFF) != RW_DONE;
+    }
+    uint64_t tot;
+    block_excl_scan(c, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(out, (unsigned long long)tot);
+}
+
+static unsigned fixed_grid(uint64_t m) { return (unsigned)hmin((m + BLOCK - 1) / BLOCK, 4096); }
+
+hipError_t launch_rw_emit_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
+                                uint64_t* send, uint32_t* qperm, unsigned long long* cursors,
+                                unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(cursors, 0, P * 8, s);
+    if (e != hipSuccess) return e;
+    if (rw.n) {
+        const unsigned g = (unsigned)hmin((rw.n + BLOCK * EMIT_IPT - 1) / (BLOCK * EMIT_IPT), 1024);
+        if (p.W == 1)
+            k_rw_emit_fixed<1><<<g, BLOCK, 0, s>>>(p, rw, P, C, send, qperm, cursors, ctr, stats);
+        else
+            k_rw_emit_fixed<2><<<g, BLOCK, 0, s>>>(p, rw, P, C, send, qperm, cursors, ctr, stats);
+    }
+    k_fixed_headers<<<1, 64, 0, s>>>(send, P, 1 + C * p.W, C, cursors);
+    return hipGetLastError();
+}
+
+hipError_t launch_find_ext_fixed(const KParams& p, const uint64_t* recv, uint32_t P, uint64_t C, TableView t,
+                                 uint8_t* reply, hipStream_t s) {
+    if (P * C == 0) return hipSuccess;
+    if (p.W == 1)
+        k_find_ext_fixed<1><<<fixed_grid(P * C), BLOCK, 0, s>>>(p, recv, P, C, t.slots, t.cap, reply);
+    else
+        k_find_ext_fixed<2><<<fixed_grid(P * C), BLOCK, 0, s>>>(p, recv, P, C, t.slots, t.cap, reply);
+    return hipGetLastError();
+}
+
+hipError_t launch_rw_apply_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
+                                 const uint64_t* send, const uint32_t* qperm, const uint8_t* reply,
+                                 unsigned long long* stats, hipStream_t s) {
+    if (P * C == 0) return hipSuccess;
+    k_rw_apply_fixed<<<fixed_grid(P * C), BLOCK, 0, s>>>(rw, P, C, 1 + C * p.W, send, qperm, reply, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_active(const RoundWalk& rw, unsigned long long* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, 8, s);
+    if (e != hipSuccess) return e;
+    if (rw.n) k_count_active<<<(unsigned)hmin((rw.n + 8 * BLOCK - 1) / (8 * BLOCK), 128), BLOCK, 0, s>>>(rw, out);
+    return hipGetLastError();
+}
+
 }  // namespace kh
 

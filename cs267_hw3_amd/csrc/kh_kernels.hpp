@@ -136,6 +136,19 @@ hipError_t launch_find_ext(const KParams& p, const uint64_t* keys, uint64_t m, T
 hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t* ext, uint64_t m,
                            unsigned long long* stats, hipStream_t s);
 
+// Fixed-capacity rounds (no count exchange, no host sync per round): per-peer segments of
+// L = 1 + C*W words [count, keys...] and C reply bytes; cursors = P device words (scratch).
+hipError_t launch_rw_emit_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
+                                uint64_t* send, uint32_t* qperm, unsigned long long* cursors,
+                                unsigned long long* ctr, unsigned long long* stats, hipStream_t s);
+hipError_t launch_find_ext_fixed(const KParams& p, const uint64_t* recv, uint32_t P, uint64_t C, TableView t,
+                                 uint8_t* reply, hipStream_t s);
+hipError_t launch_rw_apply_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
+                                 const uint64_t* send, const uint32_t* qperm, const uint8_t* reply,
+                                 unsigned long long* stats, hipStream_t s);
+// Number of walkers not yet finished -> *out (device word).
+hipError_t launch_count_active(const RoundWalk& rw, unsigned long long* out, hipStream_t s);
+
 }  // namespace kh
 
 // ---- partitioned (atomic-free) bulk build ------------------------------------------------------

@@ -166,6 +166,22 @@ class GpuShard:
     def walk_end(self):
         check(self.L.kh_walk_end_dev(self.h))
 
+    # fixed-capacity rounds
+    def emit_fixed(self, nranks, cap, send, qperm):
+        check(self.L.kh_walk_emit_fixed_dev(self.h, nranks, cap, self._p(send), self._p(qperm)))
+
+    def find_ext_fixed(self, nranks, cap, recv, reply):
+        check(self.L.kh_find_ext_fixed_dev(self.h, nranks, cap, self._p(recv), self._p(reply)))
+
+    def apply_fixed(self, nranks, cap, send, qperm, reply):
+        check(self.L.kh_walk_apply_fixed_dev(self.h, nranks, cap, self._p(send), self._p(qperm),
+                                             self._p(reply)))
+
+    def active(self):
+        out = self.zeros(1, torch.int64)
+        check(self.L.kh_walk_active_dev(self.h, self._p(out)))
+        return out
+
     def sync(self):
         self.table.sync()
 
@@ -186,10 +202,14 @@ class DistributedKmerHashMap:
                       (= test_<rank>.dat bytes); collective.
     """
 
-    def __init__(self, comm, shard):
+    CHECK_EVERY = 8  # rounds between host-side termination checks (fixed protocol)
+
+    def __init__(self, comm, shard, protocol="fixed"):
+        assert protocol in ("fixed", "variable")
         self.comm = comm
         self.shard = shard
         self.P = comm.world
+        self.protocol = protocol
         self.rounds = 0
 
     def _int64(self, like, n):
@@ -258,7 +278,62 @@ class DistributedKmerHashMap:
         sh.insert_words(recv, m)
         return m
 
+    def _active_stats(self, local):
+        """(sum, max) over ranks of the walkers not yet finished (one all-to-all + host sync)."""
+        P = self.P
+        send = local.reshape(1).expand(P).contiguous()
+        recv = torch.empty_like(send)
+        self.comm.all_to_all(recv, send, [1] * P, [1] * P)
+        v = recv.cpu().tolist()
+        return sum(v), max(v)
+
+    CAP_LIMIT = None  # tests: cap the per-peer segment to force overflow/retry rounds
+
+    def _capacity(self, gmax):
+        """Per-peer segment capacity for the next rounds (identical on every rank: a function
+        of the global max of live walkers). A rank's live walkers spread ~evenly over the P
+        owners; the 25% + 64 headroom makes overflow (retry next round) rare."""
+        P = self.P
+        c = gmax if P == 1 else min(gmax, (gmax * 5 + 4 * P - 1) // (4 * P) + 64)
+        if self.CAP_LIMIT:
+            c = min(c, self.CAP_LIMIT)
+        return max(1, c)
+
     def assemble(self, total_kmers):
+        """Walk this rank's start k-mers (collective); returns the number of rounds."""
+        if self.protocol == "variable":
+            return self._assemble_variable(total_kmers)
+        sh, P, W = self.shard, self.P, self.shard.W
+        sh.walk_begin(total_kmers)
+        gsum, gmax = self._active_stats(sh.active())
+        C = self._capacity(gmax)
+        cap0 = C
+        L0 = 1 + cap0 * W
+        dev = sh.active().device
+        send = torch.empty(P * L0, dtype=torch.int64, device=dev)
+        recv = torch.empty_like(send)
+        qperm = torch.empty(P * cap0, dtype=torch.int32, device=dev)
+        reply = torch.empty(P * cap0, dtype=torch.uint8, device=dev)
+        rrecv = torch.empty_like(reply)
+        self.rounds = 0
+        while gsum > 0:
+            L = 1 + C * W
+            for _ in range(self.CHECK_EVERY):
+                sh.emit_fixed(P, C, send, qperm)
+                self._all_to_all(recv[:P * L], send[:P * L], [L] * P, [L] * P, L)
+                sh.find_ext_fixed(P, C, recv, reply)
+                self._all_to_all(rrecv[:P * C], reply[:P * C], [C] * P, [C] * P, C)
+                sh.apply_fixed(P, C, send, qperm, rrecv)
+                self.rounds += 1
+            gsum, gmax = self._active_stats(sh.active())
+            C = min(C, self._capacity(gmax))
+        sh.walk_end()
+        sh.sync()
+        return self.rounds
+
+    def _assemble_variable(self, total_kmers):
+        """Variable-size rounds: exact per-peer counts exchanged (and read on the host) every
+        round before the keys move."""
         sh, P, W = self.shard, self.P, self.shard.W
         sh.walk_begin(total_kmers)
         self.rounds = 0
@@ -286,7 +361,7 @@ class DistributedKmerHashMap:
 
 
 # --------------------------------------------------------------------------------------------
-def run_threaded(k, recs_np, nranks, device=0):
+def run_threaded(k, recs_np, nranks, device=0, protocol="fixed", cap_limit=None):
     """P logical ranks on one GPU (threads): returns the per-rank contig texts."""
     import numpy as np
     comms = ThreadComm.group(nranks)
@@ -303,7 +378,8 @@ def run_threaded(k, recs_np, nranks, device=0):
             shard = GpuShard(k, max(n, 1), device=device)
             with torch.cuda.stream(shard.stream):
                 recs = torch.from_numpy(np.ascontiguousarray(recs_np[b:e])).to(shard.dev)
-                dm = DistributedKmerHashMap(comms[r], shard)
+                dm = DistributedKmerHashMap(comms[r], shard, protocol=protocol)
+                dm.CAP_LIMIT = cap_limit
                 dm.insert_all(recs)
                 shard.sync()
                 comms[r].barrier()
@@ -351,7 +427,8 @@ def bench_main(args, w, world, rank):
           flush=True)
     # each shard holds ~n_total/world keys; hash imbalance is tiny at this size, give 2% slack
     shard = GpuShard(k, int(n_per * 1.02) + 4096, device=local)
-    dm = DistributedKmerHashMap(comm, shard)
+    protocol = os.environ.get("KH_DIST_PROTOCOL", "fixed")
+    dm = DistributedKmerHashMap(comm, shard, protocol=protocol)
     R = record_size(k)
 
     def step():
@@ -400,7 +477,7 @@ def bench_main(args, w, world, rank):
             "config": {"workload": w["desc"], "k": k, "n_kmers_total": n_total,
                        "n_kmers_per_gpu": n_per, "contigs": nc, "lookups": nl,
                        "parallelism": f"{world} GPUs, key space sharded by owner hash, "
-                                      f"RCCL all-to-all per walk round",
+                                      f"RCCL all-to-all per walk round ({protocol} segments)",
                        "walk_rounds": dm.rounds},
             "inserts_per_s": n_total / tmax, "lookups_per_s": nl / tmax,
             "contigs_per_s": nc / tmax, "verified_vs_truth": ok,

@@ -124,6 +124,16 @@ int kh_walk_emit_dev(kh_table* t, int nranks, void* dev_keys_out, void* dev_coun
 int kh_find_ext_dev(kh_table* t, const void* dev_keys, uint64_t m, void* dev_ext_out);
 int kh_walk_apply_dev(kh_table* t, const void* dev_ext, uint64_t m);
 int kh_walk_end_dev(kh_table* t);
+/* Fixed-capacity rounds (what cs267_hw3_amd/dist.py runs): every round exchanges P segments of
+ * L = 1 + cap*W words ([count, keys...]) and P segments of cap reply bytes, so no rank waits on
+ * the host for counts; a walker that does not fit a segment retries next round.
+ * qperm: P*cap uint32 scratch owned by the caller (kept between emit and apply). */
+int kh_walk_emit_fixed_dev(kh_table* t, int nranks, uint64_t cap, void* dev_send, void* dev_qperm);
+int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* dev_recv,
+                          void* dev_reply);
+int kh_walk_apply_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* dev_send,
+                            const void* dev_qperm, const void* dev_reply_recv);
+int kh_walk_active_dev(kh_table* t, void* dev_u64_out);   /* walkers not finished -> device word */
 
 /* ---- device memory helpers (for hosts without an allocator of their own) --------------------*/
 int kh_dev_malloc(void** p, uint64_t bytes, int device);

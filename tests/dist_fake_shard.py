@@ -105,6 +105,56 @@ class FakeShard:
                 raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
             w[1] = chr(e[j])
 
+    # -- fixed-capacity rounds (same contract as kh_walk_emit_fixed_dev & co.) ------------------
+    def emit_fixed(self, nranks, cap, send, qperm):
+        L = 1 + cap * self.W
+        cursors = [0] * nranks
+        sv = send.numpy()
+        qp = qperm.numpy()
+        for i, w in enumerate(self.walkers):
+            if w[3]:
+                continue
+            if w[1] == "F":
+                w[3] = True
+                continue
+            rec = np.frombuffer(w[0] + b"X" + w[1].encode(), np.uint8)
+            nk = bytes(ob.next_kmer(self.k, rec))          # kmer_t.hpp:51-53
+            q = self._owner(nk, nranks)
+            if cursors[q] >= cap:
+                continue                                   # segment full: retry next round
+            slot = cursors[q]
+            cursors[q] += 1
+            w[2] += w[1]                                   # extract_contig appends fwd ext
+            w[0] = nk
+            w[1] = None                                    # pending
+            sv[q * L + 1 + slot * 2:q * L + 3 + slot * 2] = self._enc([nk]).numpy()[:2]
+            qp[q * cap + slot] = i
+        for q in range(nranks):
+            sv[q * L] = cursors[q]
+
+    def find_ext_fixed(self, nranks, cap, recv, reply):
+        L = 1 + cap * self.W
+        rv = recv.numpy()
+        out = reply.numpy()
+        for q in range(nranks):
+            m = int(rv[q * L])
+            keys = self._dec(torch.from_numpy(rv[q * L + 1:q * L + 1 + m * 2].copy()), m, self.P)
+            for j, key in enumerate(keys):
+                rec = self.table.get(key)
+                out[q * cap + j] = rec[self.P + 1] if rec is not None else 0xFF
+
+    def apply_fixed(self, nranks, cap, send, qperm, reply):
+        L = 1 + cap * self.W
+        sv, qp, rp = send.numpy(), qperm.numpy(), reply.numpy()
+        for q in range(nranks):
+            for j in range(int(sv[q * L])):
+                if rp[q * cap + j] == 0xFF:
+                    raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
+                self.walkers[qp[q * cap + j]][1] = chr(rp[q * cap + j])
+
+    def active(self):
+        return torch.tensor([sum(not w[3] for w in self.walkers)], dtype=torch.int64)
+
     def walk_end(self):
         self.text = "".join(w[2] + "\n" for w in self.walkers).encode()
 

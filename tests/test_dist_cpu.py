@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, name, outdir, chunk_bytes=None):
+def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="fixed", cap=None):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -34,7 +34,10 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None):
                             world_size=world)
     k = MANIFEST[name]["k"]
     recs = kh.read_kmers(os.path.join(GOLDEN, f"{name}.txt"), k, world, rank)
-    dm = DistributedKmerHashMap(TorchComm(), FakeShard(k))
+    dm = DistributedKmerHashMap(TorchComm(), FakeShard(k), protocol=protocol)
+    if cap:
+        dm.CAP_LIMIT = cap                 # force segment overflow -> retry rounds
+        dm.CHECK_EVERY = 3
     if chunk_bytes:
         dm.A2A_CHUNK_BYTES = chunk_bytes   # force the chunked all-to-all path
     dm.insert_all(torch.from_numpy(recs))
@@ -47,11 +50,14 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world,chunk", [("mixed19", 2, None), ("small51", 2, None),
-                                              ("singles51", 2, None), ("small51", 3, None),
-                                              ("small51", 3, 64), ("mixed19", 2, 1000)])
-def test_sharded_driver_gloo(tmp_path, name, world, chunk):
-    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), chunk),
+@pytest.mark.parametrize("name,world,chunk,protocol,cap", [
+    ("mixed19", 2, None, "fixed", None), ("small51", 2, None, "fixed", None),
+    ("singles51", 2, None, "fixed", None), ("small51", 3, None, "fixed", None),
+    ("small51", 3, 64, "fixed", None), ("small51", 3, None, "fixed", 2),
+    ("mixed19", 2, None, "fixed", 5), ("mixed19", 2, 1000, "variable", None),
+    ("small51", 3, 64, "variable", None), ("singles51", 2, None, "variable", None)])
+def test_sharded_driver_gloo(tmp_path, name, world, chunk, protocol, cap):
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), chunk, protocol, cap),
                        nprocs=world, join=True, start_method="spawn")
     import cs267_hw3_amd as kh
     m = MANIFEST[name]

@@ -21,13 +21,15 @@ def check_ranks(g, texts, P):
         assert got == g.truth(b, e), f"rank {r}"
 
 
+@pytest.mark.parametrize("protocol,cap", [("fixed", None), ("fixed", 3), ("variable", None)])
 @pytest.mark.parametrize("name", ["mixed19", "small51", "singles51", "k30", "k60", "tiny19"])
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
-def test_sharded_golden(name, P):
+def test_sharded_golden(name, P, protocol, cap):
+    """cap=3 forces per-peer segment overflow: walkers that do not fit retry next round."""
     from cs267_hw3_amd.dist import run_threaded
     m = MANIFEST[name]
     recs = kh.pack_text(m["k"], open(os.path.join(GOLDEN, f"{name}.txt"), "rb").read())
-    texts = run_threaded(m["k"], recs, P)
+    texts = run_threaded(m["k"], recs, P, protocol=protocol, cap_limit=cap)
     g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"],
                           seed=m["seed"])
     check_ranks(g, texts, P)
@@ -35,22 +37,24 @@ def test_sharded_golden(name, P):
     assert sorted(b"".join(texts).splitlines()) == sorted(want.splitlines())
 
 
+@pytest.mark.parametrize("protocol", ["fixed", "variable"])
 @pytest.mark.parametrize("k,n,P", [(51, 2_000_000, 8), (19, 1_000_000, 4)])
-def test_sharded_generated(k, n, P):
+def test_sharded_generated(k, n, P, protocol):
     from cs267_hw3_amd.dist import run_threaded
     g = kh.SyntheticKmers(k, n, 8, 400, 10, seed=k + P)
-    texts = run_threaded(k, g.records(), P)
+    texts = run_threaded(k, g.records(), P, protocol=protocol)
     check_ranks(g, texts, P)
 
 
-def test_sharded_missing_kmer_raises():
+@pytest.mark.parametrize("protocol", ["fixed", "variable"])
+def test_sharded_missing_kmer_raises(protocol):
     from cs267_hw3_amd.dist import run_threaded
     m = MANIFEST["tiny19"]
     recs = kh.pack_text(19, open(os.path.join(GOLDEN, "tiny19.txt"), "rb").read())
     P = (19 + 3) // 4
     interior = np.where((recs[:, P] != ord("F")) & (recs[:, P + 1] != ord("F")))[0][5]
     with pytest.raises(kh.KmerHashError):
-        run_threaded(19, np.delete(recs, interior, axis=0), 2)
+        run_threaded(19, np.delete(recs, interior, axis=0), 2, protocol=protocol)
 
 
 @pytest.mark.parametrize("mode", ["cas", "part"])
