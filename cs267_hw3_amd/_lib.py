@@ -39,6 +39,8 @@ class KhStats(ctypes.Structure):
 
 
 # name -> (restype, argtypes)
+SEG_SUBS = 8  # KH_SEG_SUBS: sub-segments per peer segment of the fixed walk rounds
+
 _SIGS = {
     "kh_abi_version": (ctypes.c_int, []),
     "kh_packed_size": (ctypes.c_int, [ctypes.c_int]),
@@ -72,10 +74,10 @@ _SIGS = {
     "kh_find_ext_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp]),
     "kh_walk_apply_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_walk_end_dev": (ctypes.c_int, [c_vp]),
-    "kh_walk_emit_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp]),
+    "kh_walk_step_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp]),
     "kh_find_ext_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp]),
-    "kh_walk_apply_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp, c_vp]),
     "kh_walk_active_dev": (ctypes.c_int, [c_vp, c_vp]),
+    "kh_walk_signature": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "kh_dev_malloc": (ctypes.c_int, [ctypes.POINTER(c_vp), c_u64, ctypes.c_int]),
     "kh_dev_free": (ctypes.c_int, [c_vp]),
     "kh_memcpy_htod": (ctypes.c_int, [c_vp, c_vp, c_u64]),

@@ -88,9 +88,10 @@ struct kh_table {
     DevBuf pb_buf1, pb_buf2, pb_hist1, pb_off1, pb_hist2, pb_off2, pb_scratch, pb_ovf;  // part build
     bool last_insert_part = false;
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
-    DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm;   // round walker
+    DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm, rw_pos, rw_ctl;  // round walker
     uint64_t rw_n = 0, rw_total = 0;
     bool rw_live = false;
+    bool rw_stepped = false;   // a fixed-round step has run since kh_walk_begin
     uint64_t starts_cap = 0;                 // start entries the starts buffer holds
     uint64_t chunk_cap = 0;
 
@@ -200,6 +201,8 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
 
 }  // namespace
 
+static_assert(KH_SEG_SUBS == kh::SEG_SUBS, "segment layout");
+
 extern "C" {
 
 int kh_abi_version(void) { return KH_ABI_VERSION; }
@@ -263,7 +266,7 @@ int kh_destroy(kh_table* t) {
                       &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
                       &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->rw_hi, &t->rw_lo,
-                      &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm,
+                      &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm, &t->rw_pos, &t->rw_ctl,
                       &t->pb_buf1, &t->pb_buf2, &t->pb_hist1, &t->pb_off1, &t->pb_hist2,
                       &t->pb_off2, &t->pb_scratch, &t->pb_ovf};
     for (auto* b : bufs) b->release();
@@ -572,6 +575,7 @@ kh::RoundWalk round_walk(kh_table* t) {
     rw.chunk = t->rw_chunk.as<uint32_t>();
     rw.state = t->rw_state.as<uint8_t>();
     rw.qperm = t->rw_qperm.as<uint32_t>();
+    rw.pos = t->rw_pos.as<uint32_t>();
     rw.contig_len = t->contig_len.as<uint32_t>();
     rw.chunk_data = t->chunk_data.as<uint64_t>();
     rw.chunk_owner = t->chunk_owner.as<uint32_t>();
@@ -671,15 +675,18 @@ int kh_walk_begin(kh_table* t, uint64_t total_kmers, uint64_t* n_walkers) {
     const uint64_t nn = ns + 1;
     if ((rc = t->rw_hi.ensure(nn * 8)) || (rc = t->rw_lo.ensure(nn * 8)) || (rc = t->rw_buf.ensure(nn * 8)) ||
         (rc = t->rw_steps.ensure(nn * 4)) || (rc = t->rw_chunk.ensure(nn * 4)) ||
-        (rc = t->rw_state.ensure((nn + 7) & ~7ull)) || (rc = t->rw_qperm.ensure(nn * 4)))
+        (rc = t->rw_state.ensure((nn + 7) & ~7ull)) || (rc = t->rw_qperm.ensure(nn * 4)) ||
+        (rc = t->rw_pos.ensure(nn * 4)) || (rc = t->rw_ctl.ensure(kh::CTL_WORDS * 8)))
         return rc;
     t->chunk_cap = chunk_cap;
     t->rw_n = ns;
     t->rw_total = tot;
     KH_HIP(hipMemsetAsync(t->ctr.as<unsigned long long>() + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
+    KH_HIP(hipMemsetAsync(t->rw_ctl.p, 0, kh::CTL_WORDS * 8, t->stream));
     KH_HIP(kh::launch_rw_init(t->kp, round_walk(t), t->starts.as<uint64_t>(), t->stream));
     t->rw_live = true;
+    t->rw_stepped = false;
     t->assembled = false;
     if (n_walkers) *n_walkers = ns;
     return KH_OK;
@@ -744,16 +751,20 @@ int kh_walk_end_dev(kh_table* t) {
     return KH_OK;
 }
 
-int kh_walk_emit_fixed_dev(kh_table* t, int nranks, uint64_t cap, void* send, void* qperm) {
+int kh_walk_step_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* reply_prev, void* send) {
     if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
     if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
-    if (!send || !qperm || cap == 0) return fail(KH_ERR_ARG, "null buffer / zero capacity");
+    if (!send) return fail(KH_ERR_ARG, "null buffer");
+    if (cap == 0 || cap % KH_SEG_SUBS) return fail(KH_ERR_ARG, "cap must be a positive multiple of %d", KH_SEG_SUBS);
+    if (cap * (uint64_t)nranks > 0xFFFFFFFFull) return fail(KH_ERR_ARG, "nranks * cap exceeds 2^32");
+    if (t->rw_stepped && !reply_prev)
+        return fail(KH_ERR_STATE, "queries in flight: pass the previous round's replies");
     if (int rc = set_device(t)) return rc;
-    if (int rc = t->route_scratch.ensure((kh::MAX_RANKS + 2) * 8)) return rc;
-    KH_HIP(kh::launch_rw_emit_fixed(t->kp, round_walk(t), (uint32_t)nranks, cap, (uint64_t*)send,
-                                    (uint32_t*)qperm, t->route_scratch.as<unsigned long long>(),
-                                    t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(),
-                                    t->stream));
+    KH_HIP(kh::launch_rw_step_fixed(t->kp, round_walk(t), (uint32_t)nranks, cap,
+                                    t->rw_stepped ? (const uint8_t*)reply_prev : nullptr, (uint64_t*)send,
+                                    t->rw_ctl.as<unsigned long long>(), t->ctr.as<unsigned long long>(),
+                                    t->stats.as<unsigned long long>(), t->stream));
+    t->rw_stepped = true;
     return KH_OK;
 }
 
@@ -761,6 +772,7 @@ int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* rec
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
     if (!recv || !reply) return fail(KH_ERR_ARG, "null buffer");
+    if (cap == 0 || cap % KH_SEG_SUBS) return fail(KH_ERR_ARG, "cap must be a positive multiple of %d", KH_SEG_SUBS);
     if (int rc = set_device(t)) return rc;
     if (int rc = clean_slots(t)) return rc;
     KH_HIP(kh::launch_find_ext_fixed(t->kp, (const uint64_t*)recv, (uint32_t)nranks, cap, view(t),
@@ -768,15 +780,22 @@ int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* rec
     return KH_OK;
 }
 
-int kh_walk_apply_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* send, const void* qperm,
-                            const void* reply) {
+int kh_walk_signature(kh_table* t, uint64_t* sig) {
     if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
-    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
-    if (!send || !qperm || !reply) return fail(KH_ERR_ARG, "null buffer");
-    if (int rc = set_device(t)) return rc;
-    KH_HIP(kh::launch_rw_apply_fixed(t->kp, round_walk(t), (uint32_t)nranks, cap, (const uint64_t*)send,
-                                     (const uint32_t*)qperm, (const uint8_t*)reply,
-                                     t->stats.as<unsigned long long>(), t->stream));
+    if (!sig) return fail(KH_ERR_ARG, "null output");
+    // everything the fixed-round launches take as kernel arguments (besides the caller's buffers)
+    const kh::RoundWalk rw = round_walk(t);
+    const uint64_t v[] = {(uint64_t)(uintptr_t)rw.hi, (uint64_t)(uintptr_t)rw.lo, (uint64_t)(uintptr_t)rw.buf,
+                          (uint64_t)(uintptr_t)rw.steps, (uint64_t)(uintptr_t)rw.chunk,
+                          (uint64_t)(uintptr_t)rw.state, (uint64_t)(uintptr_t)rw.pos,
+                          (uint64_t)(uintptr_t)rw.contig_len, (uint64_t)(uintptr_t)rw.chunk_data,
+                          (uint64_t)(uintptr_t)rw.chunk_owner, (uint64_t)(uintptr_t)rw.chunk_seq, rw.chunk_cap,
+                          rw.n, rw.max_steps, (uint64_t)(uintptr_t)t->slots.p, t->cap, (uint64_t)t->kp.K,
+                          (uint64_t)(uintptr_t)t->ctr.p, (uint64_t)(uintptr_t)t->stats.p,
+                          (uint64_t)(uintptr_t)t->rw_ctl.p, (uint64_t)(uintptr_t)t->stream};
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (uint64_t x : v) h = (h ^ x) * 0x100000001B3ull + (h >> 29);
+    *sig = h;
     return KH_OK;
 }
 
@@ -784,7 +803,10 @@ int kh_walk_active_dev(kh_table* t, void* out) {
     if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
     if (!out) return fail(KH_ERR_ARG, "null buffer");
     if (int rc = set_device(t)) return rc;
-    KH_HIP(kh::launch_count_active(round_walk(t), (unsigned long long*)out, t->stream));
+    const void* src = t->rw_stepped ? (const void*)(t->rw_ctl.as<unsigned long long>() + kh::CTL_LIVE)
+                                    : (const void*)&t->rw_n;
+    KH_HIP(hipMemcpyAsync(out, src, 8, t->rw_stepped ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                          t->stream));
     return KH_OK;
 }
 

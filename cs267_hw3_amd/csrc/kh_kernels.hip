@@ -719,199 +719,216 @@ hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t*
 }
 
 // ---- fixed-capacity rounds ------------------------------------------------------------------
-// Every round exchanges fixed-size per-peer segments, so the host never waits for counts:
-//   send/recv: P segments of L = 1 + C*W words: [count, key_0 .. key_{C-1}]
-//   replies:   P segments of C bytes (ext byte, 0xFF = absent)
-// A walker whose query does not fit its owner's segment this round keeps its state and
-// simply emits again next round.
-__device__ __forceinline__ void apply_reply(const RoundWalk& rw, uint32_t i, uint8_t r,
-                                            unsigned long long* stats) {
-    const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
-    if (r == 0xFF) {
-        atomicAdd(&stats[ST_MISSING], 1ull);
-        finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
-        rw.state[i] = RW_DONE;
-    } else if (rw.steps[i] > rw.max_steps) {
-        atomicAdd(&stats[ST_CYCLE], 1ull);
-        finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
-        rw.state[i] = RW_DONE;
-    } else {
-        const uint32_t f = ext_fwd(r);
-        rw.state[i] = (uint8_t)(f > 4 ? RW_BAD : f);
-    }
+// Every round exchanges fixed-size per-peer segments (layout in kh_kernels.hpp), so the host never
+// waits for counts. One kernel per round applies the previous round's replies and emits the next
+// queries; a walker whose query does not fit its sub-segment keeps its state and emits again next
+// round.
+// Same-address device-scope atomics serialise at the memory side (~12 ns each on MI355X,
+// measured: one atomic per 256-walker block on one counter cost ~100 us/round at 1.9M walkers).
+// So: one tile = EMIT_IPT walkers per thread with per-owner counts aggregated in LDS (one
+// reservation per (tile, owner)), reservations spread over SEG_SUBS cursors per owner on separate
+// lines, and the end-of-round bookkeeping (block done / live count) likewise per sub-group.
+static constexpr int EMIT_IPT = 8;
+
+__device__ __forceinline__ uint64_t ld_agent(const unsigned long long* a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long* a, unsigned long long v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One tile = EMIT_IPT walkers per thread: per-owner counts are aggregated in LDS over the whole
-// tile so a round makes one cursor atomicAdd per (tile, owner). Same-address device-scope
-// atomics serialise at the memory side across the 8 XCDs (~12 ns each, measured: one atomic per
-// 256-walker block cost ~100 us/round at 1.9M walkers).
-static constexpr int EMIT_IPT = 16;
-
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_rw_emit_fixed(KParams p, RoundWalk rw, uint32_t P, uint64_t C,
-                                                         uint64_t* send, uint32_t* qperm,
-                                                         unsigned long long* cursors,
+__global__ __launch_bounds__(BLOCK) void k_rw_step_fixed(KParams p, RoundWalk rw, uint32_t P, uint64_t C,
+                                                         const uint8_t* __restrict__ reply_prev,
+                                                         uint64_t* send, unsigned long long* ctl,
                                                          unsigned long long* ctr,
                                                          unsigned long long* stats) {
     __shared__ uint32_t lc[MAX_RANKS];
     __shared__ uint64_t base[MAX_RANKS];
-    const uint64_t L = 1 + C * W;
+    __shared__ int last;
+    const uint64_t L = SEG_SUBS + C * W;
+    const uint64_t C8 = C / SEG_SUBS;
+    const uint32_t x = blockIdx.x % SEG_SUBS;
     const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
     constexpr uint64_t TILE = (uint64_t)BLOCK * EMIT_IPT;
+    uint64_t live = 0;  // walkers of this thread still unfinished after this round
     for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < rw.n; t0 += (uint64_t)gridDim.x * TILE) {
         for (uint32_t q = threadIdx.x; q < P; q += BLOCK) lc[q] = 0;
         __syncthreads();
+        // phases over the whole tile (loads of one phase are independent, so each thread keeps
+        // EMIT_IPT of them in flight): state -> reply index -> reply byte -> key
+        uint8_t sts[EMIT_IPT];
+        uint32_t ps[EMIT_IPT];
+#pragma unroll
+        for (int j = 0; j < EMIT_IPT; ++j) {
+            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+            sts[j] = i < rw.n ? rw.state[i] : RW_DONE;
+        }
+#pragma unroll
+        for (int j = 0; j < EMIT_IPT; ++j) {
+            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+            ps[j] = sts[j] == RW_PENDING ? rw.pos[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < EMIT_IPT; ++j) {
+            if (sts[j] == RW_PENDING) ps[j] = reply_prev[ps[j]];  // ps now holds the reply byte
+        }
         Key nk[EMIT_IPT];
         int8_t qo[EMIT_IPT];
         uint32_t lr[EMIT_IPT];
 #pragma unroll
         for (int j = 0; j < EMIT_IPT; ++j) {
             const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
-            uint8_t st = i < rw.n ? rw.state[i] : RW_DONE;
+            uint8_t st = sts[j];
             qo[j] = -1;
             lr[j] = 0;
             nk[j] = Key{0, 0};
+            if (st == RW_PENDING) {  // apply last round's reply
+                const uint8_t r = (uint8_t)ps[j];
+                if (r == 0xFF || rw.steps[i] > rw.max_steps) {
+                    atomicAdd(&stats[r == 0xFF ? ST_MISSING : ST_CYCLE], 1ull);
+                    finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
+                    st = RW_DONE;
+                } else {
+                    const uint32_t f = ext_fwd(r);
+                    st = (uint8_t)(f > 4 ? RW_BAD : f);
+                }
+            }
             if (st == RW_F || st == RW_BAD) {
                 if (st == RW_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
                 finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
-                rw.state[i] = RW_DONE;
+                st = RW_DONE;
             } else if (st <= 3) {
                 nk[j] = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
                 const uint32_t q = owner_of(key_hash(nk[j]), P);
                 qo[j] = (int8_t)q;
                 lr[j] = atomicAdd(&lc[q], 1u);
             }
+            sts[j] = st;
         }
         __syncthreads();
         for (uint32_t r = threadIdx.x; r < P; r += BLOCK)
-            base[r] = lc[r] ? atomicAdd(&cursors[r], (unsigned long long)lc[r]) : 0ull;
+            base[r] = lc[r] ? atomicAdd(&ctl[(x * MAX_RANKS + r) * CTL_LINE], (unsigned long long)lc[r]) : 0ull;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < EMIT_IPT; ++j) {
-            if (qo[j] < 0) continue;
             const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
-            const uint32_t q = (uint32_t)qo[j];
-            const uint64_t slot = base[q] + lr[j];
-            if (slot >= C) continue;  // owner's segment full: retry next round
-            uint32_t steps = rw.steps[i], chunk = rw.chunk[i];
-            uint64_t buf = rw.buf[i];
-            append_base(o, i, rw.state[i], steps, chunk, buf, ctr, stats);
-            rw.steps[i] = steps;
-            rw.chunk[i] = chunk;
-            rw.buf[i] = buf;
-            rw.hi[i] = nk[j].hi;
-            rw.lo[i] = nk[j].lo;
-            rw.state[i] = RW_PENDING;
-            uint64_t* seg = send + (uint64_t)q * L + 1 + slot * W;
-            if (W == 2) {
-                seg[0] = nk[j].hi;
-                seg[1] = nk[j].lo;
-            } else {
-                seg[0] = nk[j].lo;
+            if (i >= rw.n) continue;
+            uint8_t st = sts[j];
+            if (qo[j] >= 0) {
+                const uint32_t q = (uint32_t)qo[j];
+                const uint64_t slot = base[q] + lr[j];
+                if (slot < C8) {
+                    uint32_t steps = rw.steps[i], chunk = rw.chunk[i];
+                    uint64_t buf = rw.buf[i];
+                    append_base(o, i, st, steps, chunk, buf, ctr, stats);
+                    rw.steps[i] = steps;
+                    rw.chunk[i] = chunk;
+                    rw.buf[i] = buf;
+                    rw.hi[i] = nk[j].hi;
+                    rw.lo[i] = nk[j].lo;
+                    uint64_t* seg = send + (uint64_t)q * L + SEG_SUBS + (x * C8 + slot) * W;
+                    if (W == 2) {
+                        seg[0] = nk[j].hi;
+                        seg[1] = nk[j].lo;
+                    } else {
+                        seg[0] = nk[j].lo;
+                    }
+                    rw.pos[i] = (uint32_t)(q * C + x * C8 + slot);
+                    st = RW_PENDING;
+                }  // else: owner's segment full, retry next round with the same state
             }
-            qperm[(uint64_t)q * C + slot] = (uint32_t)i;
+            live += st != RW_DONE;
+            rw.state[i] = st;
         }
         __syncthreads();
     }
-}
-
-__global__ void k_fixed_headers(uint64_t* send, uint32_t P, uint64_t L, uint64_t C,
-                                const unsigned long long* cursors) {
-    for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) {
-        const uint64_t c = cursors[q];
-        send[(uint64_t)q * L] = c < C ? c : C;
+    // round epilogue: the last block of each sub-group reports to the global counter; the last of
+    // those writes the segment headers and the live count, then re-arms ctl for the next round
+    uint64_t tot;
+    block_excl_scan(live, tot);
+    if (threadIdx.x == 0) {
+        const uint32_t groups = gridDim.x < SEG_SUBS ? gridDim.x : SEG_SUBS;
+        const uint32_t gsize = (gridDim.x - x + SEG_SUBS - 1) / SEG_SUBS;
+        // No __threadfence here: on gfx950 an agent-scope fence writes back the XCD's L2 (~25 us
+        // per round at 1k blocks, measured). Ordering comes from the atomics themselves: they
+        // execute at the memory side and each returning atomic is complete before the next one
+        // issues (the cursor reservations returned before the __syncthreads above). The keys
+        // written to `send` are read by the next kernel, after the kernel boundary.
+        uint64_t chain = tot ? atomicAdd(&ctl[CTL_ACC0 + x * CTL_LINE], (unsigned long long)tot) : 0;
+        asm volatile("" ::"v"(chain));  // wait for the live-count atomic before signalling done
+        int l = 0;
+        if (atomicAdd(&ctl[CTL_DONE0 + x * CTL_LINE], 1ull) == gsize - 1)
+            l = atomicAdd(&ctl[CTL_GDONE], 1ull) == groups - 1;
+        last = l;
+    }
+    __syncthreads();
+    if (last) {
+        for (uint32_t e = threadIdx.x; e < P * SEG_SUBS; e += BLOCK) {
+            const uint32_t q = e / SEG_SUBS, xs = e % SEG_SUBS;
+            unsigned long long* cur = &ctl[(xs * MAX_RANKS + q) * CTL_LINE];
+            const uint64_t c = ld_agent(cur);
+            send[(uint64_t)q * L + xs] = c < C8 ? c : C8;
+            st_agent(cur, 0ull);
+        }
+        if (threadIdx.x == 0) {
+            uint64_t lv = 0;
+            for (int xs = 0; xs < SEG_SUBS; ++xs) {
+                lv += ld_agent(&ctl[CTL_ACC0 + xs * CTL_LINE]);
+                st_agent(&ctl[CTL_ACC0 + xs * CTL_LINE], 0ull);
+                st_agent(&ctl[CTL_DONE0 + xs * CTL_LINE], 0ull);
+            }
+            st_agent(&ctl[CTL_LIVE], lv);
+            st_agent(&ctl[CTL_GDONE], 0ull);
+        }
     }
 }
 
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_find_ext_fixed(KParams p, const uint64_t* __restrict__ recv,
-                                                          uint32_t P, uint64_t C, const uint64_t* slots,
+                                                          uint64_t C, const uint64_t* slots,
                                                           uint64_t cap, uint8_t* reply) {
-    const uint64_t L = 1 + C * W;
-    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < (uint64_t)P * C;
-         j += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t q = j / C, slot = j % C;
-        const uint64_t* seg = recv + q * L;
-        if (slot >= seg[0]) continue;
+    const uint64_t L = SEG_SUBS + C * W, C8 = C / SEG_SUBS;
+    const uint64_t q = blockIdx.y / SEG_SUBS, xs = blockIdx.y % SEG_SUBS;
+    const uint64_t* seg = recv + q * L;
+    const uint64_t m = seg[xs];
+    const uint64_t* keys = seg + SEG_SUBS + xs * C8 * W;
+    uint8_t* out = reply + q * C + xs * C8;
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < m; j += (uint64_t)gridDim.x * BLOCK) {
         Key k;
         if (W == 2) {
-            k.hi = seg[1 + slot * 2];
-            k.lo = seg[2 + slot * 2];
+            k.hi = keys[j * 2];
+            k.lo = keys[j * 2 + 1];
         } else {
             k.hi = 0;
-            k.lo = seg[1 + slot];
+            k.lo = keys[j];
         }
         uint64_t w0 = 0;
-        reply[j] = probe<W>(k, p, slots, cap, w0) ? (uint8_t)slot_ext(w0) : (uint8_t)0xFF;
+        out[j] = probe<W>(k, p, slots, cap, w0) ? (uint8_t)slot_ext(w0) : (uint8_t)0xFF;
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_rw_apply_fixed(RoundWalk rw, uint32_t P, uint64_t C, uint64_t L,
-                                                          const uint64_t* send, const uint32_t* qperm,
-                                                          const uint8_t* reply, unsigned long long* stats) {
-    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < (uint64_t)P * C;
-         j += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t q = j / C, slot = j % C;
-        if (slot >= send[q * L]) continue;
-        apply_reply(rw, qperm[j], reply[j], stats);
-    }
-}
-
-__global__ __launch_bounds__(BLOCK) void k_count_active(RoundWalk rw, unsigned long long* out) {
-    uint64_t c = 0;
-    const uint64_t nw = (rw.n + 7) / 8;  // state bytes, 8 per load (buffer padded to 8)
-    const uint64_t* st8 = reinterpret_cast<const uint64_t*>(rw.state);
-    for (uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t v = st8[w];
-        const uint64_t rem = rw.n - w * 8;
-        const uint32_t lim = rem < 8 ? (uint32_t)rem : 8u;
-        for (uint32_t b = 0; b < lim; ++b) c += ((v >> (8 * b)) & 0xFF) != RW_DONE;
-    }
-    uint64_t tot;
-    block_excl_scan(c, tot);
-    if (threadIdx.x == 0 && tot) atomicAdd(out, (unsigned long long)tot);
-}
-
-static unsigned fixed_grid(uint64_t m) { return (unsigned)hmin((m + BLOCK - 1) / BLOCK, 4096); }
-
-hipError_t launch_rw_emit_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
-                                uint64_t* send, uint32_t* qperm, unsigned long long* cursors,
+hipError_t launch_rw_step_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
+                                const uint8_t* reply_prev, uint64_t* send, unsigned long long* ctl,
                                 unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(cursors, 0, P * 8, s);
-    if (e != hipSuccess) return e;
-    if (rw.n) {
-        const unsigned g = (unsigned)hmin((rw.n + BLOCK * EMIT_IPT - 1) / (BLOCK * EMIT_IPT), 1024);
-        if (p.W == 1)
-            k_rw_emit_fixed<1><<<g, BLOCK, 0, s>>>(p, rw, P, C, send, qperm, cursors, ctr, stats);
-        else
-            k_rw_emit_fixed<2><<<g, BLOCK, 0, s>>>(p, rw, P, C, send, qperm, cursors, ctr, stats);
-    }
-    k_fixed_headers<<<1, 64, 0, s>>>(send, P, 1 + C * p.W, C, cursors);
+    const unsigned g = (unsigned)hmin((rw.n + BLOCK * EMIT_IPT - 1) / (BLOCK * EMIT_IPT), 2048);
+    // rw.n == 0 still runs one block: it writes the (zero) headers
+    if (p.W == 1)
+        k_rw_step_fixed<1><<<g ? g : 1, BLOCK, 0, s>>>(p, rw, P, C, reply_prev, send, ctl, ctr, stats);
+    else
+        k_rw_step_fixed<2><<<g ? g : 1, BLOCK, 0, s>>>(p, rw, P, C, reply_prev, send, ctl, ctr, stats);
     return hipGetLastError();
 }
 
 hipError_t launch_find_ext_fixed(const KParams& p, const uint64_t* recv, uint32_t P, uint64_t C, TableView t,
                                  uint8_t* reply, hipStream_t s) {
     if (P * C == 0) return hipSuccess;
+    const uint64_t C8 = C / SEG_SUBS;
+    const dim3 grid((unsigned)hmin((C8 + BLOCK - 1) / BLOCK, 512), P * SEG_SUBS);
     if (p.W == 1)
-        k_find_ext_fixed<1><<<fixed_grid(P * C), BLOCK, 0, s>>>(p, recv, P, C, t.slots, t.cap, reply);
+        k_find_ext_fixed<1><<<grid, BLOCK, 0, s>>>(p, recv, C, t.slots, t.cap, reply);
     else
-        k_find_ext_fixed<2><<<fixed_grid(P * C), BLOCK, 0, s>>>(p, recv, P, C, t.slots, t.cap, reply);
-    return hipGetLastError();
-}
-
-hipError_t launch_rw_apply_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
-                                 const uint64_t* send, const uint32_t* qperm, const uint8_t* reply,
-                                 unsigned long long* stats, hipStream_t s) {
-    if (P * C == 0) return hipSuccess;
-    k_rw_apply_fixed<<<fixed_grid(P * C), BLOCK, 0, s>>>(rw, P, C, 1 + C * p.W, send, qperm, reply, stats);
-    return hipGetLastError();
-}
-
-hipError_t launch_count_active(const RoundWalk& rw, unsigned long long* out, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(out, 0, 8, s);
-    if (e != hipSuccess) return e;
-    if (rw.n) k_count_active<<<(unsigned)hmin((rw.n + 8 * BLOCK - 1) / (8 * BLOCK), 128), BLOCK, 0, s>>>(rw, out);
+        k_find_ext_fixed<2><<<grid, BLOCK, 0, s>>>(p, recv, C, t.slots, t.cap, reply);
     return hipGetLastError();
 }
 

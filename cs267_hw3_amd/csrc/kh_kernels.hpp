@@ -114,7 +114,8 @@ struct RoundWalk {
     uint32_t* steps;     // bases appended
     uint32_t* chunk;     // current chunk
     uint8_t* state;      // 0..3 fwd base, 4 'F', 5 bad, 6 done, 7 query in flight
-    uint32_t* qperm;     // query slot -> walker
+    uint32_t* qperm;     // query slot -> walker (variable-size rounds)
+    uint32_t* pos;       // walker -> reply index of its query in flight (fixed rounds)
     uint32_t* contig_len;
     uint64_t* chunk_data;
     uint32_t* chunk_owner;
@@ -136,18 +137,25 @@ hipError_t launch_find_ext(const KParams& p, const uint64_t* keys, uint64_t m, T
 hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t* ext, uint64_t m,
                            unsigned long long* stats, hipStream_t s);
 
-// Fixed-capacity rounds (no count exchange, no host sync per round): per-peer segments of
-// L = 1 + C*W words [count, keys...] and C reply bytes; cursors = P device words (scratch).
-hipError_t launch_rw_emit_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
-                                uint64_t* send, uint32_t* qperm, unsigned long long* cursors,
+// Fixed-capacity rounds (no count exchange, no host sync per round). Per-peer segment of
+// L = SEG_SUBS + C*W words: [count of sub 0..SEG_SUBS-1, keys of sub 0 (C/SEG_SUBS slots), keys
+// of sub 1, ...]; replies: C bytes per peer in the same slot order. Sub-segment x is filled by
+// the blocks with blockIdx % SEG_SUBS == x, so the slot-reservation atomics of a round spread
+// over SEG_SUBS * P cursors on separate cache lines instead of serialising on one address.
+// One step = apply the previous round's replies (reply_prev, indexed by rw.pos) + emit the next
+// queries; ctl = CTL_WORDS device words (zeroed once; every round's last block re-arms them).
+static constexpr int SEG_SUBS = 8;
+static constexpr int CTL_LINE = 16;  // words per 128-B line
+static constexpr int CTL_DONE0 = SEG_SUBS * MAX_RANKS * CTL_LINE;
+static constexpr int CTL_ACC0 = CTL_DONE0 + SEG_SUBS * CTL_LINE;
+static constexpr int CTL_GDONE = CTL_ACC0 + SEG_SUBS * CTL_LINE;
+static constexpr int CTL_LIVE = CTL_GDONE + CTL_LINE;
+static constexpr int CTL_WORDS = CTL_LIVE + CTL_LINE;
+hipError_t launch_rw_step_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
+                                const uint8_t* reply_prev, uint64_t* send, unsigned long long* ctl,
                                 unsigned long long* ctr, unsigned long long* stats, hipStream_t s);
 hipError_t launch_find_ext_fixed(const KParams& p, const uint64_t* recv, uint32_t P, uint64_t C, TableView t,
                                  uint8_t* reply, hipStream_t s);
-hipError_t launch_rw_apply_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
-                                 const uint64_t* send, const uint32_t* qperm, const uint8_t* reply,
-                                 unsigned long long* stats, hipStream_t s);
-// Number of walkers not yet finished -> *out (device word).
-hipError_t launch_count_active(const RoundWalk& rw, unsigned long long* out, hipStream_t s);
 
 }  // namespace kh
 

@@ -37,6 +37,7 @@ class TorchComm:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
 
     def all_to_all(self, out, inp, out_splits, in_splits):
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
@@ -167,15 +168,17 @@ class GpuShard:
         check(self.L.kh_walk_end_dev(self.h))
 
     # fixed-capacity rounds
-    def emit_fixed(self, nranks, cap, send, qperm):
-        check(self.L.kh_walk_emit_fixed_dev(self.h, nranks, cap, self._p(send), self._p(qperm)))
+    def step_fixed(self, nranks, cap, reply_prev, send):
+        rp = self._p(reply_prev) if reply_prev is not None else None
+        check(self.L.kh_walk_step_fixed_dev(self.h, nranks, cap, rp, self._p(send)))
 
     def find_ext_fixed(self, nranks, cap, recv, reply):
         check(self.L.kh_find_ext_fixed_dev(self.h, nranks, cap, self._p(recv), self._p(reply)))
 
-    def apply_fixed(self, nranks, cap, send, qperm, reply):
-        check(self.L.kh_walk_apply_fixed_dev(self.h, nranks, cap, self._p(send), self._p(qperm),
-                                             self._p(reply)))
+    def signature(self):
+        v = ctypes.c_uint64()
+        check(self.L.kh_walk_signature(self.h, ctypes.byref(v)))
+        return v.value
 
     def active(self):
         out = self.zeros(1, torch.int64)
@@ -203,6 +206,9 @@ class DistributedKmerHashMap:
     """
 
     CHECK_EVERY = 8  # rounds between host-side termination checks (fixed protocol)
+    # Capture CHECK_EVERY rounds (kernels + RCCL all-to-alls) into one hipGraph per segment
+    # capacity and replay it; None = on for a TorchComm over nccl (RCCL) unless KH_DIST_GRAPH=0.
+    GRAPH = None
 
     def __init__(self, comm, shard, protocol="fixed"):
         assert protocol in ("fixed", "variable")
@@ -211,6 +217,36 @@ class DistributedKmerHashMap:
         self.P = comm.world
         self.protocol = protocol
         self.rounds = 0
+        self._bufs = None
+        self._graphs = {}
+        self.graph_captures = 0
+
+    def close(self):
+        """Release captured round graphs (before the process group is destroyed)."""
+        if self._graphs:
+            torch.cuda.synchronize()
+            self._graphs.clear()
+            self._bufs = None
+
+    def _use_graph(self):
+        if self.GRAPH is not None:
+            return self.GRAPH
+        import os
+        return (isinstance(self.comm, TorchComm) and self.comm.backend == "nccl"
+                and os.environ.get("KH_DIST_GRAPH", "1") != "0")
+
+    def _round_buffers(self, C, dev):
+        """send/recv (P segments of SEG_SUBS + C*W words) and reply/reply_recv (P*C bytes),
+        kept across calls so captured graphs stay valid; grown when C exceeds them."""
+        P, W, S = self.P, self.shard.W, _lib.SEG_SUBS
+        if self._bufs is None or self._bufs[0] < C:
+            L = S + C * W
+            self._bufs = (C, torch.empty(P * L, dtype=torch.int64, device=dev),
+                          torch.empty(P * L, dtype=torch.int64, device=dev),
+                          torch.empty(P * C, dtype=torch.uint8, device=dev),
+                          torch.empty(P * C, dtype=torch.uint8, device=dev))
+            self._graphs.clear()
+        return self._bufs[1:]
 
     def _int64(self, like, n):
         return torch.empty(max(int(n), 1), dtype=torch.int64, device=like.device)
@@ -291,13 +327,17 @@ class DistributedKmerHashMap:
 
     def _capacity(self, gmax):
         """Per-peer segment capacity for the next rounds (identical on every rank: a function
-        of the global max of live walkers). A rank's live walkers spread ~evenly over the P
-        owners; the 25% + 64 headroom makes overflow (retry next round) rare."""
-        P = self.P
-        c = gmax if P == 1 else min(gmax, (gmax * 5 + 4 * P - 1) // (4 * P) + 64)
+        of the global max of live walkers; a multiple of SEG_SUBS). A rank's live walkers
+        spread ~evenly over the P owners and the SEG_SUBS sub-segments; 25% + 8 slots of
+        headroom per sub-segment make overflow (retry next round) rare."""
+        S = _lib.SEG_SUBS
+        per_sub = -(-gmax * 5 // (4 * self.P * S)) + 8
+        # quantised to {2^e, 1.5 * 2^e}: few distinct capacities -> few captured graphs
+        q = 1 << max(0, per_sub.bit_length() - 1)
+        per_sub = q if per_sub <= q else (q * 3 // 2 if per_sub <= q * 3 // 2 else 2 * q)
         if self.CAP_LIMIT:
-            c = min(c, self.CAP_LIMIT)
-        return max(1, c)
+            per_sub = min(per_sub, -(-self.CAP_LIMIT // S))
+        return S * max(1, per_sub)
 
     def assemble(self, total_kmers):
         """Walk this rank's start k-mers (collective); returns the number of rounds."""
@@ -307,26 +347,40 @@ class DistributedKmerHashMap:
         sh.walk_begin(total_kmers)
         gsum, gmax = self._active_stats(sh.active())
         C = self._capacity(gmax)
-        cap0 = C
-        L0 = 1 + cap0 * W
-        dev = sh.active().device
-        send = torch.empty(P * L0, dtype=torch.int64, device=dev)
-        recv = torch.empty_like(send)
-        qperm = torch.empty(P * cap0, dtype=torch.int32, device=dev)
-        reply = torch.empty(P * cap0, dtype=torch.uint8, device=dev)
-        rrecv = torch.empty_like(reply)
+        S = _lib.SEG_SUBS
+        send, recv, reply, rrecv = self._round_buffers(C, sh.active().device)
+        graph = self._use_graph()
+
+        def one_round(prev, C):
+            L = S + C * W
+            sh.step_fixed(P, C, prev, send)            # apply last replies, emit next queries
+            self._all_to_all(recv[:P * L], send[:P * L], [L] * P, [L] * P, L)
+            sh.find_ext_fixed(P, C, recv, reply)       # owner side
+            self._all_to_all(rrecv[:P * C], reply[:P * C], [C] * P, [C] * P, C)
+
         self.rounds = 0
-        while gsum > 0:
-            L = 1 + C * W
-            for _ in range(self.CHECK_EVERY):
-                sh.emit_fixed(P, C, send, qperm)
-                self._all_to_all(recv[:P * L], send[:P * L], [L] * P, [L] * P, L)
-                sh.find_ext_fixed(P, C, recv, reply)
-                self._all_to_all(rrecv[:P * C], reply[:P * C], [C] * P, [C] * P, C)
-                sh.apply_fixed(P, C, send, qperm, rrecv)
-                self.rounds += 1
+        if gsum > 0:
+            one_round(None, C)                          # first step: no replies to apply yet
+            self.rounds = 1
             gsum, gmax = self._active_stats(sh.active())
+        while gsum > 0:
             C = min(C, self._capacity(gmax))
+            if graph:
+                key = (sh.signature(), C, send.data_ptr(), rrecv.data_ptr())
+                g = self._graphs.get(key)
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=sh.stream):
+                        for _ in range(self.CHECK_EVERY):
+                            one_round(rrecv, C)
+                    self._graphs[key] = g
+                    self.graph_captures += 1
+                g.replay()
+            else:
+                for _ in range(self.CHECK_EVERY):
+                    one_round(rrecv, C)
+            self.rounds += self.CHECK_EVERY
+            gsum, gmax = self._active_stats(sh.active())
         sh.walk_end()
         sh.sync()
         return self.rounds
@@ -478,7 +532,7 @@ def bench_main(args, w, world, rank):
                        "n_kmers_per_gpu": n_per, "contigs": nc, "lookups": nl,
                        "parallelism": f"{world} GPUs, key space sharded by owner hash, "
                                       f"RCCL all-to-all per walk round ({protocol} segments)",
-                       "walk_rounds": dm.rounds},
+                       "walk_rounds": dm.rounds, "round_graphs": dm.graph_captures},
             "inserts_per_s": n_total / tmax, "lookups_per_s": nl / tmax,
             "contigs_per_s": nc / tmax, "verified_vs_truth": ok,
             "roofline": {"bound": "hbm", "kernel": "k_insert_words (rank 0)", "achieved": achieved,
@@ -487,6 +541,8 @@ def bench_main(args, w, world, rank):
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)
+    dm.close()
     shard.table.close()
+    dist.barrier()
     dist.destroy_process_group()
     return 0

@@ -59,6 +59,7 @@ def main(argv):
         ncontigs = text.count(b"\n")
         print(f"Rank {rank} reconstructed {ncontigs} contigs with {recs.shape[0]} nodes. "
               f"({t1 - t0:f} insert, {t2 - t1:f} assemble, {t2 - t0:f} total)")
+    dm.close()
     shard.table.close()
     dist.destroy_process_group()
     return 0

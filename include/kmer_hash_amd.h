@@ -124,16 +124,27 @@ int kh_walk_emit_dev(kh_table* t, int nranks, void* dev_keys_out, void* dev_coun
 int kh_find_ext_dev(kh_table* t, const void* dev_keys, uint64_t m, void* dev_ext_out);
 int kh_walk_apply_dev(kh_table* t, const void* dev_ext, uint64_t m);
 int kh_walk_end_dev(kh_table* t);
-/* Fixed-capacity rounds (what cs267_hw3_amd/dist.py runs): every round exchanges P segments of
- * L = 1 + cap*W words ([count, keys...]) and P segments of cap reply bytes, so no rank waits on
- * the host for counts; a walker that does not fit a segment retries next round.
- * qperm: P*cap uint32 scratch owned by the caller (kept between emit and apply). */
-int kh_walk_emit_fixed_dev(kh_table* t, int nranks, uint64_t cap, void* dev_send, void* dev_qperm);
+/* Fixed-capacity rounds (what cs267_hw3_amd/dist.py runs): every round exchanges one segment
+ * per peer of L = KH_SEG_SUBS + cap*W int64 words and one of cap reply bytes, so no rank waits on
+ * the host for counts. Segment = [count of sub-segment 0..KH_SEG_SUBS-1, then the keys of each
+ * sub-segment, cap/KH_SEG_SUBS slots each]; replies use the same slot order (0xFF = absent). A
+ * walker that does not fit its sub-segment retries next round. One step applies the replies of
+ * the previous round (NULL before the first step) and emits the next queries:
+ *   step(reply_prev, send) -> all-to-all(send -> recv, L words per peer)
+ *   -> find_ext_fixed(recv -> reply) (owner) -> all-to-all(reply -> reply_prev, cap bytes per peer)
+ * Stop when the global sum of kh_walk_active_dev is 0. cap: a multiple of KH_SEG_SUBS, the same
+ * on every rank within a round (it may shrink between rounds); nranks * cap < 2^32. */
+#define KH_SEG_SUBS 8
+int kh_walk_step_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* dev_reply_prev,
+                           void* dev_send);
 int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* dev_recv,
                           void* dev_reply);
-int kh_walk_apply_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* dev_send,
-                            const void* dev_qperm, const void* dev_reply_recv);
-int kh_walk_active_dev(kh_table* t, void* dev_u64_out);   /* walkers not finished -> device word */
+/* walkers unfinished after the last step (all walkers before the first) -> device word */
+int kh_walk_active_dev(kh_table* t, void* dev_u64_out);
+/* Hash of every device pointer / size the fixed-round launches bake in (for hosts that capture
+ * rounds into a hipGraph after the first step: a graph is reusable while the signature, the
+ * caller's buffers and cap are unchanged). */
+int kh_walk_signature(kh_table* t, uint64_t* sig);
 
 /* ---- device memory helpers (for hosts without an allocator of their own) --------------------*/
 int kh_dev_malloc(void** p, uint64_t bytes, int device);

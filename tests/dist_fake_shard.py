@@ -65,11 +65,11 @@ class FakeShard:
             self.table[rec[:self.P]] = rec
 
     def walk_begin(self, total_kmers):
-        # walker = [key bytes, fwd char, contig string, done]
+        # walker = [key bytes, fwd char (None = query in flight), contig string, done, reply pos]
         self.walkers = []
         for s in self.starts:
             self.walkers.append([s[:self.P], chr(s[self.P + 1]),
-                                 ob.unpack(self.k, np.frombuffer(s[:self.P], np.uint8)), False])
+                                 ob.unpack(self.k, np.frombuffer(s[:self.P], np.uint8)), False, -1])
         self.nw = len(self.walkers)
         return self.nw
 
@@ -106,51 +106,55 @@ class FakeShard:
             w[1] = chr(e[j])
 
     # -- fixed-capacity rounds (same contract as kh_walk_emit_fixed_dev & co.) ------------------
-    def emit_fixed(self, nranks, cap, send, qperm):
-        L = 1 + cap * self.W
-        cursors = [0] * nranks
+    S = 8  # KH_SEG_SUBS
+
+    def step_fixed(self, nranks, cap, reply_prev, send):
+        """Apply the previous round's replies (walker.pos -> reply_prev index), then emit.
+        Walker i fills sub-segment i % S (the GPU uses its block's index)."""
+        S, C8 = self.S, cap // self.S
+        L = S + cap * self.W
+        cursors = [[0] * S for _ in range(nranks)]
         sv = send.numpy()
-        qp = qperm.numpy()
+        rp = reply_prev.numpy() if reply_prev is not None else None
         for i, w in enumerate(self.walkers):
             if w[3]:
                 continue
+            if w[1] is None:                               # query in flight
+                r = rp[w[4]]
+                if r == 0xFF:
+                    raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
+                w[1] = chr(r)
             if w[1] == "F":
                 w[3] = True
                 continue
             rec = np.frombuffer(w[0] + b"X" + w[1].encode(), np.uint8)
             nk = bytes(ob.next_kmer(self.k, rec))          # kmer_t.hpp:51-53
-            q = self._owner(nk, nranks)
-            if cursors[q] >= cap:
-                continue                                   # segment full: retry next round
-            slot = cursors[q]
-            cursors[q] += 1
+            q, x = self._owner(nk, nranks), i % S
+            if cursors[q][x] >= C8:
+                continue                                   # sub-segment full: retry next round
+            slot = x * C8 + cursors[q][x]
+            cursors[q][x] += 1
             w[2] += w[1]                                   # extract_contig appends fwd ext
             w[0] = nk
-            w[1] = None                                    # pending
-            sv[q * L + 1 + slot * 2:q * L + 3 + slot * 2] = self._enc([nk]).numpy()[:2]
-            qp[q * cap + slot] = i
+            w[1] = None
+            w[4] = q * cap + slot
+            sv[q * L + S + slot * 2:q * L + S + 2 + slot * 2] = self._enc([nk]).numpy()[:2]
         for q in range(nranks):
-            sv[q * L] = cursors[q]
+            sv[q * L:q * L + S] = cursors[q]
 
     def find_ext_fixed(self, nranks, cap, recv, reply):
-        L = 1 + cap * self.W
+        S, C8 = self.S, cap // self.S
+        L = S + cap * self.W
         rv = recv.numpy()
         out = reply.numpy()
         for q in range(nranks):
-            m = int(rv[q * L])
-            keys = self._dec(torch.from_numpy(rv[q * L + 1:q * L + 1 + m * 2].copy()), m, self.P)
-            for j, key in enumerate(keys):
-                rec = self.table.get(key)
-                out[q * cap + j] = rec[self.P + 1] if rec is not None else 0xFF
-
-    def apply_fixed(self, nranks, cap, send, qperm, reply):
-        L = 1 + cap * self.W
-        sv, qp, rp = send.numpy(), qperm.numpy(), reply.numpy()
-        for q in range(nranks):
-            for j in range(int(sv[q * L])):
-                if rp[q * cap + j] == 0xFF:
-                    raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
-                self.walkers[qp[q * cap + j]][1] = chr(rp[q * cap + j])
+            for x in range(S):
+                m = int(rv[q * L + x])
+                b = q * L + S + x * C8 * 2
+                keys = self._dec(torch.from_numpy(rv[b:b + m * 2].copy()), m, self.P)
+                for j, key in enumerate(keys):
+                    rec = self.table.get(key)
+                    out[q * cap + x * C8 + j] = rec[self.P + 1] if rec is not None else 0xFF
 
     def active(self):
         return torch.tensor([sum(not w[3] for w in self.walkers)], dtype=torch.int64)

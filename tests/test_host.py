@@ -25,6 +25,8 @@ def test_library_exports_every_declared_symbol():
     # every declared symbol is also bound with a signature in the Python stub
     assert sorted(_lib._SIGS) == declared
     assert L.kh_abi_version() == 1
+    hdr = open(os.path.join(os.path.dirname(GOLDEN), "..", "include", "kmer_hash_amd.h")).read()
+    assert f"#define KH_SEG_SUBS {_lib.SEG_SUBS}" in hdr
 
 
 @pytest.mark.parametrize("k", [1, 19, 29, 30, 31, 32, 51, 60])

@@ -3,7 +3,8 @@ import csv
 import glob
 import sys
 
-f = glob.glob(f"{sys.argv[1]}/**/*_kernel_trace.csv", recursive=True)[0]
+import os
+f = max(glob.glob(f"{sys.argv[1]}/**/*_kernel_trace.csv", recursive=True), key=os.path.getmtime)
 rows = list(csv.DictReader(open(f)))
 nr = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 
@@ -12,8 +13,8 @@ def spans(pat):
     return [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if pat in r["Kernel_Name"]]
 
 
-em = spans("k_rw_emit_fixed")[-nr:]
-for pat in ["k_rw_emit_fixed", "k_find_ext_fixed", "k_rw_apply_fixed", "rcclGenericKernel"]:
+em = spans("k_rw_step_fixed")[-nr:]
+for pat in ["k_rw_step_fixed", "k_find_ext_fixed", "rcclGenericKernel"]:
     sp = spans(pat)
     sp = [x for x in sp if x[0] >= em[0][0]]
     d = [(e - s) / 1e3 for s, e in sp]
