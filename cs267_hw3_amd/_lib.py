@@ -40,6 +40,8 @@ class KhStats(ctypes.Structure):
 
 # name -> (restype, argtypes)
 SEG_SUBS = 8  # KH_SEG_SUBS: sub-segments per peer segment of the fixed walk rounds
+MSG_WORDS = 5  # KH_MSG_WORDS: migrating-walker message
+TEXT_REC_WORDS = 2  # KH_TEXT_REC_WORDS
 
 _SIGS = {
     "kh_abi_version": (ctypes.c_int, []),
@@ -78,6 +80,11 @@ _SIGS = {
     "kh_find_ext_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp]),
     "kh_walk_active_dev": (ctypes.c_int, [c_vp, c_vp]),
     "kh_walk_signature": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
+    "kh_mwalk_begin": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u64, ctypes.POINTER(c_u64)]),
+    "kh_mwalk_round_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
+    "kh_mwalk_text_count": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
+    "kh_mwalk_text_dev": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "kh_mwalk_end_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_dev_malloc": (ctypes.c_int, [ctypes.POINTER(c_vp), c_u64, ctypes.c_int]),
     "kh_dev_free": (ctypes.c_int, [c_vp]),
     "kh_memcpy_htod": (ctypes.c_int, [c_vp, c_vp, c_u64]),

@@ -89,6 +89,10 @@ struct kh_table {
     bool last_insert_part = false;
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
     DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm, rw_pos, rw_ctl;  // round walker
+    DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
+    uint64_t mw_store_n = 0;   // text records in mw_store
+    uint32_t mw_P = 0, mw_rank = 0;
+    bool mw_live = false, mw_stepped = false;
     uint64_t rw_n = 0, rw_total = 0;
     bool rw_live = false;
     bool rw_stepped = false;   // a fixed-round step has run since kh_walk_begin
@@ -202,6 +206,7 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
 }  // namespace
 
 static_assert(KH_SEG_SUBS == kh::SEG_SUBS, "segment layout");
+static_assert(KH_MSG_WORDS == kh::MSG_WORDS, "message layout");
 
 extern "C" {
 
@@ -267,6 +272,8 @@ int kh_destroy(kh_table* t) {
                       &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->rw_hi, &t->rw_lo,
                       &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm, &t->rw_pos, &t->rw_ctl,
+                      &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
+                      &t->mw_misc, &t->mw_store,
                       &t->pb_buf1, &t->pb_buf2, &t->pb_hist1, &t->pb_off1, &t->pb_hist2,
                       &t->pb_off2, &t->pb_scratch, &t->pb_ovf};
     for (auto* b : bufs) b->release();
@@ -777,6 +784,156 @@ int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* rec
     if (int rc = clean_slots(t)) return rc;
     KH_HIP(kh::launch_find_ext_fixed(t->kp, (const uint64_t*)recv, (uint32_t)nranks, cap, view(t),
                                      (uint8_t*)reply, t->stream));
+    return KH_OK;
+}
+
+// ---- migrating-walker rounds --------------------------------------------------------------------
+namespace {
+// Grow b to >= want bytes keeping its first `used` bytes.
+int grow_keep(DevBuf& b, uint64_t want, uint64_t used, hipStream_t s) {
+    if (want <= b.bytes && b.p) return KH_OK;
+    uint64_t nb = b.bytes + b.bytes / 2;
+    if (nb < want) nb = want;
+    DevBuf n;
+    if (int rc = n.ensure(nb)) return rc;
+    if (used) KH_HIP(hipMemcpyAsync(n.p, b.p, used, hipMemcpyDeviceToDevice, s));
+    KH_HIP(hipStreamSynchronize(s));
+    b.release();
+    b.p = n.p;
+    b.bytes = n.bytes;
+    n.p = nullptr;
+    return KH_OK;
+}
+}  // namespace
+
+int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t* n_walkers) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (nranks < 1 || nranks > kh::MAX_RANKS || rank < 0 || rank >= nranks)
+        return fail(KH_ERR_ARG, "bad rank %d of %d", rank, nranks);
+    if (int rc = set_device(t)) return rc;
+    if (int rc = clean_slots(t)) return rc;
+    int rc;
+    uint64_t ns = 0;
+    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
+    if (ns >= (1ull << 31)) return fail(KH_ERR_ARG, "%llu start k-mers on one rank (max 2^31)", (unsigned long long)ns);
+    if ((rc = t->mw_init.ensure((ns + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_misc.ensure(64)) ||
+        (rc = t->mw_store.ensure((ns + 1024) * 16)))
+        return rc;
+    t->mw_P = (uint32_t)nranks;
+    t->mw_rank = (uint32_t)rank;
+    t->rw_n = ns;
+    t->rw_total = total_kmers > ns ? total_kmers : ns;
+    t->mw_store_n = 0;
+    KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
+    KH_HIP(kh::launch_mw_init(t->kp, t->starts.as<uint64_t>(), ns, (uint32_t)rank, t->mw_init.as<uint64_t>(),
+                              t->stream));
+    t->mw_live = true;
+    t->mw_stepped = false;
+    t->assembled = false;
+    if (n_walkers) *n_walkers = ns;
+    return KH_OK;
+}
+
+int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, void* counts) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (!counts) return fail(KH_ERR_ARG, "null counts");
+    const uint64_t* src = (const uint64_t*)in;
+    uint64_t n = n_in;
+    if (!t->mw_stepped) {
+        src = t->mw_init.as<uint64_t>();
+        n = t->rw_n;
+    } else if (n && !in) {
+        return fail(KH_ERR_ARG, "null input messages");
+    }
+    if (n && !out) return fail(KH_ERR_ARG, "null output messages");
+    if (int rc = set_device(t)) return rc;
+    int rc;
+    if ((rc = t->mw_tmp.ensure((n + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_dst.ensure(n + 1)) ||
+        (rc = t->mw_stage.ensure((n + 1) * kh::MW_REC_SLOTS * 16)) || (rc = t->mw_nrec.ensure(n + 1)) ||
+        (rc = t->mw_off.ensure((n + 1) * 8)) || (rc = t->scratch.ensure(kh::scan_scratch_words(n) * 8 + 64)) ||
+        (rc = ensure_route(t, n, (int)t->mw_P)))
+        return rc;
+    kh::MWalkRound mw;
+    mw.P = t->mw_P;
+    mw.rank = t->mw_rank;
+    mw.max_steps = t->rw_total;
+    mw.in = src;
+    mw.n_in = n;
+    mw.tmp = t->mw_tmp.as<uint64_t>();
+    mw.dst = t->mw_dst.as<uint8_t>();
+    mw.stage = t->mw_stage.as<uint64_t>();
+    mw.nrec = t->mw_nrec.as<uint8_t>();
+    KH_HIP(kh::launch_mw_run(t->kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
+    // text records of this round -> the rank-local store (the host needs their count to size it)
+    unsigned long long* tot = t->mw_misc.as<unsigned long long>();
+    KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), tot, t->stream));
+    uint64_t m = 0;
+    KH_HIP(hipMemcpyAsync(&m, tot, 8, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    if ((rc = grow_keep(t->mw_store, (t->mw_store_n + m) * 16, t->mw_store_n * 16, t->stream))) return rc;
+    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>() + t->mw_store_n * 2,
+                                 t->stream));
+    t->mw_store_n += m;
+    KH_HIP(kh::launch_mw_group(mw, t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
+                               t->route_scratch.as<uint64_t>(), (uint64_t*)out, (uint64_t*)counts, t->stream));
+    t->mw_stepped = true;
+    return KH_OK;
+}
+
+int kh_mwalk_text_count(kh_table* t, uint64_t* n_records) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (!n_records) return fail(KH_ERR_ARG, "null output");
+    *n_records = t->mw_store_n;
+    return KH_OK;
+}
+
+int kh_mwalk_text_dev(kh_table* t, void* out, void* counts) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (!counts || (t->mw_store_n && !out)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, t->mw_store_n, (int)t->mw_P)) return rc;
+    KH_HIP(kh::launch_mw_group_text(t->mw_store.as<uint64_t>(), t->mw_store_n, t->mw_P, t->route_hist.as<uint64_t>(),
+                                    t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(), (uint64_t*)out,
+                                    (uint64_t*)counts, t->stream));
+    return KH_OK;
+}
+
+int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (n && !recs) return fail(KH_ERR_ARG, "null records");
+    if (int rc = set_device(t)) return rc;
+    const uint64_t nc = t->rw_n;
+    int rc;
+    if ((rc = t->contig_len.ensure((nc + 1) * 4)) || (rc = t->contig_off.ensure((nc + 1) * 8)) ||
+        (rc = t->scratch.ensure(kh::scan_scratch_words(nc) * 8 + 64)))
+        return rc;
+    unsigned long long* ctr = t->ctr.as<unsigned long long>();
+    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
+    KH_HIP(hipMemsetD32Async((hipDeviceptr_t)t->contig_len.p, 1, nc + 1, t->stream));
+    KH_HIP(hipMemsetAsync(ctr + kh::CT_MW_FIN, 0, 8, t->stream));
+    KH_HIP(kh::launch_mw_lens((const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(), ctr + kh::CT_MW_FIN,
+                              t->stream));
+    KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
+                                     t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
+    if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
+    uint64_t hv[3] = {0, 0, 0};
+    static_assert(kh::CT_MW_FIN == kh::CT_OUT_BYTES + 2, "counter layout");
+    KH_HIP(hipMemcpyAsync(hv, ctr + kh::CT_OUT_BYTES, 24, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    const uint64_t bytes = hv[0], fin = hv[2];
+    if (fin != nc)
+        return fail(KH_ERR_NOT_FOUND, "%llu of %llu walkers did not finish (records lost in transit?)",
+                    (unsigned long long)(nc - fin), (unsigned long long)nc);
+    if ((rc = t->text.ensure(bytes + 64))) return rc;
+    KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
+                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+    KH_HIP(kh::launch_mw_words(t->kp.K, (const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(),
+                               t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+    KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
+    t->walk_timed = true;
+    t->last_contigs = nc;
+    t->assembled = true;
+    t->mw_live = false;
     return KH_OK;
 }
 

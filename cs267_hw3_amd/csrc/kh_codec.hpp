@@ -47,7 +47,13 @@ struct KParams {
     int W;          // slot words (1 or 2)
     uint64_t hi_mask;   // mask for hi after a shift (2K-62 bits, 0 when K <= 31)
     uint64_t v_mask;    // W=1: mask of V (2K bits)
+    int M;              // minimizer length (bases) of the sharded owner function
 };
+
+// Minimizer length for owner_key: consecutive k-mers of a contig share their minimizer for
+// ~(K-M+2)/2 steps on random sequence, so a walk stays on one rank for that long; 4^M distinct
+// values keep the shards balanced.
+inline int minimizer_len(int K) { return K >= 31 ? 15 : K >= 20 ? 12 : K >= 10 ? 10 : K; }
 
 inline KParams make_params(int K) {
     KParams p;
@@ -59,6 +65,7 @@ inline KParams make_params(int K) {
     int hib = 2 * K - 62;
     p.hi_mask = hib > 0 ? ((1ull << hib) - 1) : 0ull;
     p.v_mask = (2 * K >= 64) ? ~0ull : ((1ull << (2 * K)) - 1);
+    p.M = minimizer_len(K);
     return p;
 }
 
@@ -151,9 +158,32 @@ KH_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
 // kmer_hash.cpp:108-109) without a power-of-two round-up.
 KH_HD uint64_t home_slot(uint64_t h, uint64_t cap) { return mulhi64(h, cap); }
 
-// Owner rank for the sharded table: independent low bits of the same hash.
-KH_HD uint32_t owner_of(uint64_t h, uint32_t nranks) {
-    return (uint32_t)(((h & 0xffffffffull) * (uint64_t)nranks) >> 32);
+
+KH_HD uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// Owner rank of a k-mer in the sharded table: a hash of its minimizer (the M-mer of smallest
+// mix32 value among its K-M+1 windows), not of the whole key. Placement never changes the
+// output (the reference's owner is std::hash<string> % P, hash_map.hpp:28-30); this one keeps
+// runs of consecutive k-mers on one rank so a walker migrates only at minimizer changes.
+KH_HD uint32_t owner_key(Key k, const KParams& p, uint32_t nranks) {
+    if (nranks == 1) return 0;
+    const uint32_t mask = (uint32_t)((1ull << (2 * p.M)) - 1);
+    uint64_t lo = k.lo, hi = k.hi;  // V = hi * 2^62 + lo; windows from the last M bases upward
+    uint32_t best = 0xffffffffu;
+    for (int j = 0; j <= p.K - p.M; ++j) {
+        const uint32_t h = mix32(((uint32_t)lo & mask) ^ 0x5bd1e995u);
+        best = h < best ? h : best;
+        lo = (lo >> 2) | ((hi & 3u) << 60);
+        hi >>= 2;
+    }
+    return (uint32_t)(((uint64_t)mix32(best ^ 0x9e3779b9u) * nranks) >> 32);
 }
 
 // ---- slot encode/decode ---------------------------------------------------------------

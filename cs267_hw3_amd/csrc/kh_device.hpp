@@ -237,4 +237,80 @@ __device__ __forceinline__ bool probe(Key k, const KParams& p, const uint64_t* _
     return false;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Owner-major view of a [blocks][ranks] histogram for the exclusive scan.
+struct HistF {
+    const uint64_t* hist;
+    uint64_t nb;
+    uint32_t P;
+    __device__ uint64_t operator()(uint64_t i) const { return hist[(i % nb) * P + i / nb]; }
+};
+
+template <int Unused = 0>
+__global__ void k_route_counts(const uint64_t* off, uint64_t nb, uint32_t P,
+                               const unsigned long long* total, uint64_t* counts) {
+    const uint32_t q = threadIdx.x;
+    if (q < P) {
+        const uint64_t a = off[(uint64_t)q * nb];
+        const uint64_t b = (q + 1 < P) ? off[(uint64_t)(q + 1) * nb] : (uint64_t)*total;
+        counts[q] = b - a;
+    }
+    if (q == 0) counts[P] = (uint64_t)*total;
+}
+
+// Generic two-kernel owner grouping. Op must provide:
+//   int owner(uint64_t i)             -> rank in [0,P) or -1 to skip (read-only)
+//   void emit(uint64_t i, int q, uint64_t dst)   (may mutate per-item state; called once)
+template <class Op>
+__global__ __launch_bounds__(BLOCK) void k_group_hist(Op op, uint64_t n, uint32_t P, uint64_t* hist) {
+    __shared__ uint32_t h[MAX_RANKS];
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+    for (uint32_t j = threadIdx.x; j < ROUTE_TILE; j += BLOCK) {
+        const uint64_t i = b0 + j;
+        if (i < n) {
+            const int q = op.owner(i);
+            if (q >= 0) atomicAdd(&h[q], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) hist[(uint64_t)blockIdx.x * P + q] = h[q];
+}
+
+template <class Op>
+__global__ __launch_bounds__(BLOCK) void k_group_scatter(Op op, uint64_t n, uint32_t P,
+                                                         const uint64_t* off, uint64_t nb) {
+    __shared__ uint32_t h[MAX_RANKS];
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+    for (uint32_t j = threadIdx.x; j < ROUTE_TILE; j += BLOCK) {
+        const uint64_t i = b0 + j;
+        int q = -1;
+        if (i < n) q = op.owner(i);
+        uint64_t dst = 0;
+        if (q >= 0) dst = off[(uint64_t)q * nb + blockIdx.x] + atomicAdd(&h[q], 1u);
+        if (i < n) op.emit(i, q, dst);
+    }
+}
+
+template <class Op>
+static inline hipError_t group_by_owner(Op op, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
+                                 uint64_t* scratch, uint64_t* counts, unsigned long long* total,
+                                 hipStream_t s) {
+    const uint64_t nb = route_blocks(n);
+    if (nb == 0) {
+        hipError_t e = hipMemsetAsync(counts, 0, (P + 1) * 8, s);
+        return e;
+    }
+    k_group_hist<Op><<<(unsigned)nb, BLOCK, 0, s>>>(op, n, P, hist);
+    hipError_t e = scan_exclusive(HistF{hist, nb, P}, nb * P, off, scratch,
+                                  (unsigned long long*)nullptr, total, s);
+    if (e != hipSuccess) return e;
+    k_route_counts<0><<<1, MAX_RANKS, 0, s>>>(off, nb, P, total, counts);
+    k_group_scatter<Op><<<(unsigned)nb, BLOCK, 0, s>>>(op, n, P, off, nb);
+    return hipGetLastError();
+}
+
 }  // namespace kh

@@ -393,6 +393,23 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* c
     }
 }
 
+hipError_t launch_contig_offsets(int K, const uint32_t* len, uint64_t nc, uint64_t* offsets,
+                                 uint64_t* scratch, unsigned long long* total, hipStream_t s) {
+    return scan_exclusive(ContigBytesF{len, (uint64_t)K}, nc, offsets, scratch, (unsigned long long*)nullptr,
+                          total, s);
+}
+
+hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t nc, const uint32_t* len,
+                              const uint64_t* offsets, char* out, hipStream_t s) {
+    if (nc == 0) return hipSuccess;
+    const unsigned gh = (unsigned)hmin((nc + BLOCK - 1) / BLOCK, 8192);
+    if (p.W == 1)
+        k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, starts, nc, len, offsets, out);
+    else
+        k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, starts, nc, len, offsets, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
                               uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s) {
     const uint64_t nc = wb.n_starts;
@@ -413,7 +430,7 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
 }
 
 // =============================================================================================
-// Sharded multi-GPU path. The key space is split by owner_of(key_hash); records
+// Sharded multi-GPU path. The key space is split by owner_key (minimizer owner, kh_codec.hpp); records
 // are routed to their owner once (insert), then contigs are walked in rounds: every home rank
 // emits the next k-mer of each live walker to its owner, owners answer with the ext byte, homes
 // apply the answers. The exchange between emit and apply is the caller's (RCCL all-to-all).
@@ -439,80 +456,6 @@ hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, 
     return hipGetLastError();
 }
 
-// Owner-major view of a [blocks][ranks] histogram for the exclusive scan.
-struct HistF {
-    const uint64_t* hist;
-    uint64_t nb;
-    uint32_t P;
-    __device__ uint64_t operator()(uint64_t i) const { return hist[(i % nb) * P + i / nb]; }
-};
-
-__global__ void k_route_counts(const uint64_t* off, uint64_t nb, uint32_t P,
-                               const unsigned long long* total, uint64_t* counts) {
-    const uint32_t q = threadIdx.x;
-    if (q < P) {
-        const uint64_t a = off[(uint64_t)q * nb];
-        const uint64_t b = (q + 1 < P) ? off[(uint64_t)(q + 1) * nb] : (uint64_t)*total;
-        counts[q] = b - a;
-    }
-    if (q == 0) counts[P] = (uint64_t)*total;
-}
-
-// Generic two-kernel owner grouping. Op must provide:
-//   int owner(uint64_t i)             -> rank in [0,P) or -1 to skip (read-only)
-//   void emit(uint64_t i, int q, uint64_t dst)   (may mutate per-item state; called once)
-template <class Op>
-__global__ __launch_bounds__(BLOCK) void k_group_hist(Op op, uint64_t n, uint32_t P, uint64_t* hist) {
-    __shared__ uint32_t h[MAX_RANKS];
-    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
-    __syncthreads();
-    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
-    for (uint32_t j = threadIdx.x; j < ROUTE_TILE; j += BLOCK) {
-        const uint64_t i = b0 + j;
-        if (i < n) {
-            const int q = op.owner(i);
-            if (q >= 0) atomicAdd(&h[q], 1u);
-        }
-    }
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) hist[(uint64_t)blockIdx.x * P + q] = h[q];
-}
-
-template <class Op>
-__global__ __launch_bounds__(BLOCK) void k_group_scatter(Op op, uint64_t n, uint32_t P,
-                                                         const uint64_t* off, uint64_t nb) {
-    __shared__ uint32_t h[MAX_RANKS];
-    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
-    __syncthreads();
-    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
-    for (uint32_t j = threadIdx.x; j < ROUTE_TILE; j += BLOCK) {
-        const uint64_t i = b0 + j;
-        int q = -1;
-        if (i < n) q = op.owner(i);
-        uint64_t dst = 0;
-        if (q >= 0) dst = off[(uint64_t)q * nb + blockIdx.x] + atomicAdd(&h[q], 1u);
-        if (i < n) op.emit(i, q, dst);
-    }
-}
-
-template <class Op>
-static hipError_t group_by_owner(Op op, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
-                                 uint64_t* scratch, uint64_t* counts, unsigned long long* total,
-                                 hipStream_t s) {
-    const uint64_t nb = route_blocks(n);
-    if (nb == 0) {
-        hipError_t e = hipMemsetAsync(counts, 0, (P + 1) * 8, s);
-        return e;
-    }
-    k_group_hist<Op><<<(unsigned)nb, BLOCK, 0, s>>>(op, n, P, hist);
-    hipError_t e = scan_exclusive(HistF{hist, nb, P}, nb * P, off, scratch,
-                                  (unsigned long long*)nullptr, total, s);
-    if (e != hipSuccess) return e;
-    k_route_counts<<<1, MAX_RANKS, 0, s>>>(off, nb, P, total, counts);
-    k_group_scatter<Op><<<(unsigned)nb, BLOCK, 0, s>>>(op, n, P, off, nb);
-    return hipGetLastError();
-}
-
 template <int W>
 struct RouteOp {
     KParams p;
@@ -521,7 +464,7 @@ struct RouteOp {
     uint64_t* out;
     __device__ int owner(uint64_t i) const {
         const Key k = key_from_packed(recs + i * (uint64_t)p.R, p);
-        return (int)owner_of(key_hash(k), P);
+        return (int)owner_key(k, p, P);
     }
     __device__ void emit(uint64_t i, int q, uint64_t dst) const {
         Key k;
@@ -612,7 +555,7 @@ struct EmitOp {
         const uint8_t st = rw.state[i];
         if (st > 3) return -1;
         const Key k = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
-        return (int)owner_of(key_hash(k), P);
+        return (int)owner_key(k, p, P);
     }
     __device__ void emit(uint64_t i, int q, uint64_t dst) const {
         const uint8_t st = rw.state[i];
@@ -800,7 +743,7 @@ __global__ __launch_bounds__(BLOCK) void k_rw_step_fixed(KParams p, RoundWalk rw
                 st = RW_DONE;
             } else if (st <= 3) {
                 nk[j] = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
-                const uint32_t q = owner_of(key_hash(nk[j]), P);
+                const uint32_t q = owner_key(nk[j], p, P);
                 qo[j] = (int8_t)q;
                 lr[j] = atomicAdd(&lc[q], 1u);
             }

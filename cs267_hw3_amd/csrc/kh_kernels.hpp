@@ -26,6 +26,7 @@ enum CtrIdx : int {
     CT_CHUNK_NEXT = 2, // chunk allocator head
     CT_OUT_BYTES = 3,  // total contig bytes (incl. '\n')
     CT_OVF = 4,        // partitioned build: keys whose probe run left their region
+    CT_MW_FIN = 5,     // migrating walk: finish records received by the origin
     CT_NUM = 8
 };
 
@@ -78,6 +79,46 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
                               uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s);
 
+// ---- migrating-walker rounds (kh_mwalk.hip) -------------------------------------------------
+// message: MSG_WORDS words [key.hi, key.lo, partial word, idx << 32 | bases appended,
+// origin | state << 8]; text record: 2 words [origin << 56 | fin << 55 | word_no << 31 | idx,
+// word (or bases appended, fin)].
+static constexpr int MSG_WORDS = 5;
+static constexpr int MW_RUN_WORDS = 6;                  // words a walker may flush per round
+static constexpr int MW_REC_SLOTS = MW_RUN_WORDS + 2;   // + final partial word + finish record
+struct MWalkRound {
+    uint32_t P, rank;
+    uint64_t max_steps;
+    const uint64_t* in;   // n_in messages
+    uint64_t n_in;
+    uint64_t* tmp;        // n_in * MSG_WORDS: outgoing message of input j
+    uint8_t* dst;         // n_in: its destination rank (0xFF = finished)
+    uint64_t* stage;      // n_in * MW_REC_SLOTS * 2: text records of input j
+    uint8_t* nrec;        // n_in
+};
+hipError_t launch_mw_init(const KParams& p, const uint64_t* starts, uint64_t n, uint32_t rank, uint64_t* msgs,
+                          hipStream_t s);
+hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
+                         hipStream_t s);
+hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
+                                  unsigned long long* total, hipStream_t s);
+hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, hipStream_t s);
+hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, uint64_t* scratch,
+                           uint64_t* out, uint64_t* counts, hipStream_t s);
+hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
+                                uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s);
+hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,
+                          unsigned long long* fin, hipStream_t s);
+hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
+                           const uint64_t* off, char* out, hipStream_t s);
+
+// Pieces of the materialisation for other walkers: offsets (+ total bytes) and start k-mer heads
+// (with the trailing '\n' at off + K + len - 1).
+hipError_t launch_contig_offsets(int K, const uint32_t* len, uint64_t nc, uint64_t* offsets,
+                                 uint64_t* scratch, unsigned long long* total, hipStream_t s);
+hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t nc, const uint32_t* len,
+                              const uint64_t* offsets, char* out, hipStream_t s);
+
 // Scratch words needed by the scans for m elements.
 uint64_t scan_scratch_words(uint64_t m);
 
@@ -95,7 +136,7 @@ inline uint64_t route_blocks(uint64_t n) { return (n + ROUTE_TILE - 1) / ROUTE_T
 hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, uint64_t* start_mask,
                              hipStream_t s);
 
-// Records -> internal words (W per record) grouped by owner rank (owner_of(key_hash)).
+// Records -> internal words (W per record) grouped by owner rank (owner_key).
 // hist/off: route_blocks(n) * nranks words each; counts: nranks + 1 words (last = n).
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
                         uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out_words,

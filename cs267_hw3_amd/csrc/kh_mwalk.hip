@@ -1,0 +1,296 @@
+// kh_mwalk.hip — sharded contig walk with migrating walkers (the multi-GPU walk path).
+//
+// Reference: assemble_contigs (kmer_hash.cpp:38-55) walks every start k-mer of its rank with one
+// DistributedHashMap::find per step, a blocking RPC to the owner for (P-1)/P of the steps
+// (hash_map.hpp:83-107). Here the table is sharded by owner_key, a hash of the k-mer's minimizer,
+// so consecutive k-mers of a contig mostly live on the same rank. A walker therefore moves to the
+// data instead of querying it: on the rank that owns its current k-mer it keeps walking through
+// the local shard until the next k-mer belongs to another rank, then it is sent there (one
+// all-to-all per round, done by the caller between kernels). Rounds ~ longest contig / minimizer
+// run length instead of longest contig.
+//
+// Bases appended by a walker are flushed as 32-base words tagged (origin rank, walker, word
+// number) into a rank-local text store; after the last round the store is routed to the origin
+// ranks, which materialise their test_<rank>.dat bytes (extract_contig, read_kmers.hpp:81-92).
+#include "kh_device.hpp"
+
+namespace kh {
+
+static constexpr uint32_t MW_LOOKUP = 0xFF;  // message state: key must be looked up by its owner
+static constexpr uint8_t MW_NONE = 0xFF;     // destination: walker finished this round
+
+__device__ __forceinline__ uint64_t rec_tag(uint32_t origin, bool fin, uint64_t word_no, uint32_t idx) {
+    return ((uint64_t)origin << 56) | ((uint64_t)fin << 55) | (word_no << 31) | idx;
+}
+
+// One lane per input message (static stride, no work-queue atomics), one table probe per loop
+// iteration, like k_walk. A lane's run ends when the walker finishes, migrates, or has flushed
+// MW_RUN_WORDS words this round (it then re-sends itself, bounding the per-input text region).
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __restrict__ slots, uint64_t cap,
+                                                  MWalkRound mw, unsigned long long* stats) {
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    bool active = false, probing = false;
+    Key k{0, 0};
+    uint64_t s = 0, buf = 0;
+    uint32_t steps = 0, idx = 0, origin = 0, st = 0, nrec = 0, nwords = 0;
+    uint64_t* rec = nullptr;
+    while (true) {
+        if (!active && j < mw.n_in) {
+            const uint64_t* m = mw.in + j * MSG_WORDS;
+            k.hi = m[0];
+            k.lo = m[1];
+            buf = m[2];
+            steps = (uint32_t)m[3];
+            idx = (uint32_t)(m[3] >> 32);
+            origin = (uint32_t)m[4] & 0xFFu;
+            st = (uint32_t)(m[4] >> 8) & 0xFFu;
+            rec = mw.stage + j * (MW_REC_SLOTS * 2);
+            nrec = 0;
+            nwords = 0;
+            active = true;
+            probing = st == MW_LOOKUP;
+            if (probing) s = home_slot(key_hash(k), cap);
+        }
+        if (!__any(active)) break;
+        if (active && !probing) {
+            bool fin = false, ovf = false;
+            if (st > 3) {
+                if (st != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+                fin = true;
+            } else if (steps > mw.max_steps) {
+                atomicAdd(&stats[ST_CYCLE], 1ull);
+                fin = true;
+            } else {
+                buf |= (uint64_t)st << (2 * (steps & 31));
+                ++steps;
+                if ((steps & 31) == 0) {
+                    rec[2 * nrec] = rec_tag(origin, false, (steps >> 5) - 1, idx);
+                    rec[2 * nrec + 1] = buf;
+                    ++nrec;
+                    ++nwords;
+                    buf = 0;
+                }
+                k = key_next(k, st, p);
+                const uint32_t q = owner_key(k, p, mw.P);
+                if (q != mw.rank || nwords >= MW_RUN_WORDS) {
+                    uint64_t* o = mw.tmp + j * MSG_WORDS;
+                    o[0] = k.hi;
+                    o[1] = k.lo;
+                    o[2] = buf;
+                    o[3] = ((uint64_t)idx << 32) | steps;
+                    o[4] = origin | (MW_LOOKUP << 8);
+                    mw.dst[j] = (uint8_t)q;
+                    ovf = true;
+                } else {
+                    probing = true;
+                    s = home_slot(key_hash(k), cap);
+                }
+            }
+            if (fin) {
+                if (steps & 31) {
+                    rec[2 * nrec] = rec_tag(origin, false, steps >> 5, idx);
+                    rec[2 * nrec + 1] = buf;
+                    ++nrec;
+                }
+                rec[2 * nrec] = rec_tag(origin, true, 0, idx);
+                rec[2 * nrec + 1] = steps;
+                ++nrec;
+                mw.dst[j] = MW_NONE;
+            }
+            if (fin || ovf) {
+                mw.nrec[j] = (uint8_t)nrec;
+                active = false;
+                j += stride;
+            }
+        }
+        if (active && probing) {
+            uint64_t w0, w1;
+            load_slot<W>(slots, s, w0, w1);
+            const bool empty = w0 == EMPTY;
+            const bool hit = !empty & ((w0 >> 6) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
+            if (hit) {
+                st = ext_fwd(slot_ext(w0));
+                probing = false;
+            } else if (empty) {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
+                atomicAdd(&stats[ST_MISSING], 1ull);
+                if (steps & 31) {
+                    rec[2 * nrec] = rec_tag(origin, false, steps >> 5, idx);
+                    rec[2 * nrec + 1] = buf;
+                    ++nrec;
+                }
+                rec[2 * nrec] = rec_tag(origin, true, 0, idx);
+                rec[2 * nrec + 1] = steps;
+                ++nrec;
+                mw.dst[j] = MW_NONE;
+                mw.nrec[j] = (uint8_t)nrec;
+                active = false;
+                j += stride;
+            } else {
+                s = (s + 1 == cap) ? 0 : s + 1;
+            }
+        }
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p, const uint64_t* starts, uint64_t n, uint32_t rank,
+                                                   uint64_t* msgs) {
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t w0 = starts[i * W];
+        const uint64_t w1 = (W == 2) ? starts[i * W + 1] : 0;
+        const Key k = slot_key(w0, w1, p);
+        const uint32_t f = ext_fwd(slot_ext(w0));
+        uint64_t* m = msgs + i * MSG_WORDS;
+        m[0] = k.hi;
+        m[1] = k.lo;
+        m[2] = 0;
+        m[3] = i << 32;
+        m[4] = rank | ((uint64_t)(f > 4 ? EXT_BAD : f) << 8);
+    }
+}
+
+struct NrecF {
+    const uint8_t* n;
+    __device__ uint64_t operator()(uint64_t i) const { return n[i]; }
+};
+
+__global__ __launch_bounds__(BLOCK) void k_mw_compact(const uint64_t* stage, const uint8_t* nrec,
+                                                      const uint64_t* off, uint64_t n, uint64_t* store) {
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
+        const uint32_t c = nrec[j];
+        const ulonglong2* src = reinterpret_cast<const ulonglong2*>(stage + j * (MW_REC_SLOTS * 2));
+        ulonglong2* dst = reinterpret_cast<ulonglong2*>(store + off[j] * 2);
+        for (uint32_t r = 0; r < c; ++r) dst[r] = src[r];
+    }
+}
+
+struct MsgOp {
+    const uint8_t* dst;
+    const uint64_t* tmp;
+    uint64_t* out;
+    __device__ int owner(uint64_t i) const { return dst[i] == MW_NONE ? -1 : (int)dst[i]; }
+    __device__ void emit(uint64_t i, int q, uint64_t d) const {
+        if (q < 0) return;
+        const uint64_t* a = tmp + i * MSG_WORDS;
+        uint64_t* b = out + d * MSG_WORDS;
+#pragma unroll
+        for (int w = 0; w < MSG_WORDS; ++w) b[w] = a[w];
+    }
+};
+
+struct RecOp {
+    const uint64_t* recs;
+    uint64_t* out;
+    __device__ int owner(uint64_t i) const { return (int)(recs[2 * i] >> 56); }
+    __device__ void emit(uint64_t i, int q, uint64_t d) const {
+        (void)q;
+        reinterpret_cast<ulonglong2*>(out)[d] = reinterpret_cast<const ulonglong2*>(recs)[i];
+    }
+};
+
+// Origin side: finish records -> contig lengths (k-mers = bases appended + 1); *fin counts them
+// (one atomic per block) so the host can check that every walker came home.
+__global__ __launch_bounds__(BLOCK) void k_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,
+                                                   unsigned long long* fin) {
+    uint64_t f = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t t = recs[2 * i];
+        if (!((t >> 55) & 1)) continue;
+        const uint32_t c = (uint32_t)(t & 0x7FFFFFFFull);
+        if (c < nc) {
+            len[c] = (uint32_t)recs[2 * i + 1] + 1;
+            ++f;
+        }
+    }
+    uint64_t tot;
+    block_excl_scan(f, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(fin, (unsigned long long)tot);
+}
+
+// Origin side: word records -> characters.
+__global__ __launch_bounds__(BLOCK) void k_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc,
+                                                    const uint32_t* len, const uint64_t* off, char* out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t t = recs[2 * i];
+        if ((t >> 55) & 1) continue;
+        const uint32_t c = (uint32_t)(t & 0x7FFFFFFFull);
+        if (c >= nc) continue;
+        const uint64_t wn = (t >> 31) & 0xFFFFFFull;
+        const uint64_t app = (uint64_t)len[c] - 1;
+        const uint64_t j0 = wn * 32;
+        if (j0 >= app) continue;
+        const uint32_t cnt = (uint32_t)(app - j0 < 32 ? app - j0 : 32);
+        const uint64_t word = recs[2 * i + 1];
+        char* o = out + off[c] + K + j0;
+        for (uint32_t b = 0; b < cnt; ++b) o[b] = (char)code_char((uint32_t)(word >> (2 * b)) & 3u);
+    }
+}
+
+static unsigned grid_for(uint64_t n, uint64_t cap_blocks) {
+    const uint64_t g = (n + BLOCK - 1) / BLOCK;
+    return (unsigned)(g == 0 ? 1 : (g < cap_blocks ? g : cap_blocks));
+}
+
+hipError_t launch_mw_init(const KParams& p, const uint64_t* starts, uint64_t n, uint32_t rank, uint64_t* msgs,
+                          hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (p.W == 1)
+        k_mw_init<1><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs);
+    else
+        k_mw_init<2><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs);
+    return hipGetLastError();
+}
+
+hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
+                         hipStream_t s) {
+    if (mw.n_in == 0) return hipSuccess;
+    // ~4 inputs per lane keeps lanes busy through the run-length tail without a work queue
+    const unsigned g = grid_for((mw.n_in + 3) / 4, 4096);
+    if (p.W == 1)
+        k_mw_run<1><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats);
+    else
+        k_mw_run<2><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
+                                  unsigned long long* total, hipStream_t s) {
+    if (mw.n_in == 0) return hipMemsetAsync(total, 0, 8, s);
+    return scan_exclusive(NrecF{mw.nrec}, mw.n_in, off, scratch, (unsigned long long*)nullptr, total, s);
+}
+
+hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, hipStream_t s) {
+    if (mw.n_in == 0) return hipSuccess;
+    k_mw_compact<<<grid_for(mw.n_in, 8192), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store);
+    return hipGetLastError();
+}
+
+hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, uint64_t* scratch,
+                           uint64_t* out, uint64_t* counts, hipStream_t s) {
+    unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
+    return group_by_owner(MsgOp{mw.dst, mw.tmp, out}, mw.n_in, mw.P, hist, off, scratch + 1, counts, total, s);
+}
+
+hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
+                                uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s) {
+    unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
+    return group_by_owner(RecOp{recs, out}, n, P, hist, off, scratch + 1, counts, total, s);
+}
+
+hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len, unsigned long long* fin,
+                          hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_mw_lens<<<grid_for(n, 1024), BLOCK, 0, s>>>(recs, n, nc, len, fin);
+    return hipGetLastError();
+}
+
+hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
+                           const uint64_t* off, char* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_mw_words<<<grid_for(n, 8192), BLOCK, 0, s>>>(K, recs, n, nc, len, off, out);
+    return hipGetLastError();
+}
+
+}  // namespace kh

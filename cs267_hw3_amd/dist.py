@@ -175,6 +175,35 @@ class GpuShard:
     def find_ext_fixed(self, nranks, cap, recv, reply):
         check(self.L.kh_find_ext_fixed_dev(self.h, nranks, cap, self._p(recv), self._p(reply)))
 
+    # migrating-walker rounds
+    MSG_WORDS = _lib.MSG_WORDS
+    TEXT_REC_WORDS = _lib.TEXT_REC_WORDS
+
+    def mw_begin(self, nranks, rank, total_kmers):
+        nw = ctypes.c_uint64(0)
+        check(self.L.kh_mwalk_begin(self.h, nranks, rank, total_kmers, ctypes.byref(nw)))
+        self.nranks = nranks
+        return nw.value
+
+    def mw_round(self, inp, n_in, out):
+        counts = self.zeros(self.nranks + 1, torch.int64)
+        check(self.L.kh_mwalk_round_dev(self.h, self._p(inp) if inp is not None else None, n_in,
+                                        self._p(out), self._p(counts)))
+        return counts
+
+    def mw_text_count(self):
+        v = ctypes.c_uint64(0)
+        check(self.L.kh_mwalk_text_count(self.h, ctypes.byref(v)))
+        return v.value
+
+    def mw_text(self, out):
+        counts = self.zeros(self.nranks + 1, torch.int64)
+        check(self.L.kh_mwalk_text_dev(self.h, self._p(out), self._p(counts)))
+        return counts
+
+    def mw_end(self, recs, n):
+        check(self.L.kh_mwalk_end_dev(self.h, self._p(recs), n))
+
     def signature(self):
         v = ctypes.c_uint64()
         check(self.L.kh_walk_signature(self.h, ctypes.byref(v)))
@@ -206,12 +235,14 @@ class DistributedKmerHashMap:
     """
 
     CHECK_EVERY = 8  # rounds between host-side termination checks (fixed protocol)
-    # Capture CHECK_EVERY rounds (kernels + RCCL all-to-alls) into one hipGraph per segment
-    # capacity and replay it; None = on for a TorchComm over nccl (RCCL) unless KH_DIST_GRAPH=0.
+    # fixed protocol: capture CHECK_EVERY rounds (kernels + RCCL all-to-alls) into one hipGraph
+    # per segment capacity and replay it. Opt-in (KH_DIST_GRAPH=1, TorchComm over nccl only):
+    # torch's NCCL watchdog can query an event recorded inside the capture and abort
+    # (hipErrorCapturedEvent), seen on ROCm 7 / torch 2.10.
     GRAPH = None
 
-    def __init__(self, comm, shard, protocol="fixed"):
-        assert protocol in ("fixed", "variable")
+    def __init__(self, comm, shard, protocol="migrate"):
+        assert protocol in ("migrate", "fixed", "variable")
         self.comm = comm
         self.shard = shard
         self.P = comm.world
@@ -233,7 +264,7 @@ class DistributedKmerHashMap:
             return self.GRAPH
         import os
         return (isinstance(self.comm, TorchComm) and self.comm.backend == "nccl"
-                and os.environ.get("KH_DIST_GRAPH", "1") != "0")
+                and os.environ.get("KH_DIST_GRAPH", "0") == "1")
 
     def _round_buffers(self, C, dev):
         """send/recv (P segments of SEG_SUBS + C*W words) and reply/reply_recv (P*C bytes),
@@ -341,6 +372,8 @@ class DistributedKmerHashMap:
 
     def assemble(self, total_kmers):
         """Walk this rank's start k-mers (collective); returns the number of rounds."""
+        if self.protocol == "migrate":
+            return self._assemble_migrate(total_kmers)
         if self.protocol == "variable":
             return self._assemble_variable(total_kmers)
         sh, P, W = self.shard, self.P, self.shard.W
@@ -385,6 +418,48 @@ class DistributedKmerHashMap:
         sh.sync()
         return self.rounds
 
+    def _grow(self, name, n, dtype, device):
+        t = getattr(self, name, None)
+        if t is None or t.numel() < n or t.dtype != dtype or t.device != device:
+            t = torch.empty(max(int(n * 1.25), 16), dtype=dtype, device=device)
+            setattr(self, name, t)
+        return t
+
+    def _assemble_migrate(self, total_kmers):
+        """Walkers move to the rank owning their next k-mer (minimizer sharding keeps runs of
+        consecutive k-mers on one rank): round = local walk -> one all-to-all of migrating
+        walkers; then the text records go home in one more all-to-all."""
+        sh, P = self.shard, self.P
+        M, T = sh.MSG_WORDS, sh.TEXT_REC_WORDS
+        n_in = sh.mw_begin(P, self.comm.rank, total_kmers)
+        inp = None
+        self.rounds = 0
+        while True:
+            counts = sh.mw_round(inp, n_in, self._grow("_mw_out", max(n_in, 1) * M, torch.int64,
+                                                       sh.zeros(1, torch.int64).device))
+            out = self._mw_out
+            send_splits, recv_splits, totals, gmax = self._exchange_counts(counts)
+            self.rounds += 1
+            if sum(totals) == 0:
+                break
+            m = sum(recv_splits)
+            nxt = self._grow("_mw_in", max(m, 1) * M, torch.int64, out.device)
+            self._all_to_all(nxt[:m * M], out[:sum(send_splits) * M], [c * M for c in recv_splits],
+                             [c * M for c in send_splits], gmax * M)
+            # ping-pong: the next round reads _mw_in and writes _mw_out
+            inp, n_in = nxt, m
+        nrec = sh.mw_text_count()
+        tout = sh.zeros(max(nrec, 1) * T, torch.int64)
+        counts = sh.mw_text(tout)
+        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
+        r = sum(recv_splits)
+        trecv = sh.zeros(max(r, 1) * T, torch.int64)
+        self._all_to_all(trecv[:r * T], tout[:nrec * T], [c * T for c in recv_splits],
+                         [c * T for c in send_splits], gmax * T)
+        sh.mw_end(trecv, r)
+        sh.sync()
+        return self.rounds
+
     def _assemble_variable(self, total_kmers):
         """Variable-size rounds: exact per-peer counts exchanged (and read on the host) every
         round before the keys move."""
@@ -415,8 +490,9 @@ class DistributedKmerHashMap:
 
 
 # --------------------------------------------------------------------------------------------
-def run_threaded(k, recs_np, nranks, device=0, protocol="fixed", cap_limit=None):
-    """P logical ranks on one GPU (threads): returns the per-rank contig texts."""
+def run_threaded(k, recs_np, nranks, device=0, protocol="migrate", cap_limit=None, info=None):
+    """P logical ranks on one GPU (threads): returns the per-rank contig texts. `info` (a dict)
+    receives the round count and per-rank table stats."""
     import numpy as np
     comms = ThreadComm.group(nranks)
     n = recs_np.shape[0]
@@ -439,6 +515,9 @@ def run_threaded(k, recs_np, nranks, device=0, protocol="fixed", cap_limit=None)
                 comms[r].barrier()
                 dm.assemble(n)
                 out[r] = dm.contigs_text()
+                if info is not None:
+                    info.setdefault("rounds", dm.rounds)
+                    info.setdefault("stats", {})[r] = shard.stats()
             shard.table.close()
         except BaseException as ex:  # surface thread failures
             errs.append(ex)
@@ -481,7 +560,7 @@ def bench_main(args, w, world, rank):
           flush=True)
     # each shard holds ~n_total/world keys; hash imbalance is tiny at this size, give 2% slack
     shard = GpuShard(k, int(n_per * 1.02) + 4096, device=local)
-    protocol = os.environ.get("KH_DIST_PROTOCOL", "fixed")
+    protocol = os.environ.get("KH_DIST_PROTOCOL", "migrate")
     dm = DistributedKmerHashMap(comm, shard, protocol=protocol)
     R = record_size(k)
 

@@ -146,6 +146,26 @@ int kh_walk_active_dev(kh_table* t, void* dev_u64_out);
  * caller's buffers and cap are unchanged). */
 int kh_walk_signature(kh_table* t, uint64_t* sig);
 
+/* Migrating-walker rounds (what cs267_hw3_amd/dist.py runs by default). The table is sharded by
+ * a hash of each k-mer's minimizer, so consecutive k-mers of a contig mostly share an owner; a
+ * walker walks the local shard until its next k-mer is owned elsewhere and is then sent there:
+ *   begin -> loop { round(in, n_in -> out grouped by destination, counts[P+1])
+ *                   -> exchange counts, all-to-all out -> next in }   until every rank's total is 0
+ *   -> text_count / text_dev (text records grouped by origin rank) -> all-to-all
+ *   -> end_dev(records received): this rank's contig text (kh_contigs_text*).
+ * Messages are KH_MSG_WORDS int64 words, text records KH_TEXT_REC_WORDS. The first round reads
+ * this rank's start k-mers (in may be NULL); out needs room for one message per input (the
+ * first round: one per walker). Routing by minimizer must also be used for the inserts: this
+ * sharding and kh_route_dev agree (both use the minimizer owner). */
+#define KH_MSG_WORDS 5
+#define KH_TEXT_REC_WORDS 2
+int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t* n_walkers);
+int kh_mwalk_round_dev(kh_table* t, const void* dev_in, uint64_t n_in, void* dev_out,
+                       void* dev_counts_out);
+int kh_mwalk_text_count(kh_table* t, uint64_t* n_records);
+int kh_mwalk_text_dev(kh_table* t, void* dev_out, void* dev_counts_out);
+int kh_mwalk_end_dev(kh_table* t, const void* dev_recs, uint64_t n);
+
 /* ---- device memory helpers (for hosts without an allocator of their own) --------------------*/
 int kh_dev_malloc(void** p, uint64_t bytes, int device);
 int kh_dev_free(void* p);

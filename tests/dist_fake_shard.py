@@ -159,6 +159,101 @@ class FakeShard:
     def active(self):
         return torch.tensor([sum(not w[3] for w in self.walkers)], dtype=torch.int64)
 
+    # -- migrating walkers (same contract as kh_mwalk_*; messages and records are opaque words) --
+    MSG_WORDS = 5
+    TEXT_REC_WORDS = 2
+
+    def zeros(self, n, dtype):
+        return torch.zeros(max(int(n), 1), dtype=dtype)
+
+    def mw_begin(self, nranks, rank, total_kmers):
+        self.nranks, self.rank = nranks, rank
+        self.store = []                                    # (origin, fin, pos, idx, value)
+        self.first = True
+        return len(self.starts)
+
+    def _msg(self, key, fwd, steps, idx, origin):
+        kw = self._enc([key]).numpy()[:2]
+        return [int(kw[0]), int(kw[1]), steps, idx, origin | (fwd << 8)]
+
+    def mw_round(self, inp, n_in, out):
+        if self.first:
+            msgs = [self._msg(s[:self.P], s[self.P + 1], 0, i, self.rank) for i, s in enumerate(self.starts)]
+            self.first = False
+        else:
+            a = inp[:n_in * 5].numpy().reshape(n_in, 5)
+            msgs = [list(map(int, r)) for r in a]
+        outs = []
+        for m in msgs:
+            key = bytes(np.array(m[:2], np.int64).view(np.uint8)[:self.P])
+            steps, idx, origin, fwd = m[2], m[3], m[4] & 0xFF, (m[4] >> 8) & 0xFF
+            if fwd == 0xFF:                                # look the key up here (its owner)
+                rec = self.table.get(key)
+                if rec is None:
+                    raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
+                fwd = rec[self.P + 1]
+            while True:
+                if fwd == ord("F"):
+                    self.store.append((origin, 1, 0, idx, steps))
+                    break
+                self.store.append((origin, 0, steps, idx, fwd))   # base `steps` of the contig
+                steps += 1
+                rec = np.frombuffer(key + b"X" + bytes([fwd]), np.uint8)
+                key = bytes(ob.next_kmer(self.k, rec))     # kmer_t.hpp:51-53
+                q = self._owner(key, self.nranks)
+                if q != self.rank:
+                    outs.append((q, self._msg(key, 0xFF, steps, idx, origin)))
+                    break
+                rec = self.table.get(key)
+                if rec is None:
+                    raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
+                fwd = rec[self.P + 1]
+        outs.sort(key=lambda x: x[0])
+        o = out.numpy()
+        for j, (_, m) in enumerate(outs):
+            o[j * 5:(j + 1) * 5] = m
+        counts = np.zeros(self.nranks + 1, np.int64)
+        for q, _ in outs:
+            counts[q] += 1
+        counts[self.nranks] = len(outs)
+        return torch.from_numpy(counts)
+
+    def _rec_words(self, r):
+        origin, fin, pos, idx, val = r
+        return [(origin << 56) | (fin << 55) | (pos << 31) | idx, val]
+
+    def mw_text_count(self):
+        return len(self.store)
+
+    def mw_text(self, out):
+        recs = sorted(self.store, key=lambda r: r[0])
+        o = out.numpy()
+        for j, r in enumerate(recs):
+            w = self._rec_words(r)
+            o[2 * j], o[2 * j + 1] = w                     # origin < 64: tag < 2^62
+        counts = np.zeros(self.nranks + 1, np.int64)
+        for r in recs:
+            counts[r[0]] += 1
+        counts[self.nranks] = len(recs)
+        return torch.from_numpy(counts)
+
+    def mw_end(self, recs, n):
+        a = recs[:2 * n].numpy().view(np.uint64).reshape(n, 2) if n else np.zeros((0, 2), np.uint64)
+        lens, bases = {}, {}
+        for t, v in a:
+            t, v = int(t), int(v)
+            idx, pos, fin = t & 0x7FFFFFFF, (t >> 31) & 0xFFFFFF, (t >> 55) & 1
+            if fin:
+                lens[idx] = v
+            else:
+                bases[(idx, pos)] = chr(v)
+        out = []
+        for i, s in enumerate(self.starts):
+            assert i in lens, "walker did not come home"
+            head = ob.unpack(self.k, np.frombuffer(s[:self.P], np.uint8))
+            out.append(head + "".join(bases[(i, j)] for j in range(lens[i])) + "\n")
+        self.text = "".join(out).encode()
+
     def walk_end(self):
         self.text = "".join(w[2] + "\n" for w in self.walkers).encode()
 

@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="fixed", cap=None):
+def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="migrate", cap=None):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -51,6 +51,9 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="fixe
 
 
 @pytest.mark.parametrize("name,world,chunk,protocol,cap", [
+    ("mixed19", 2, None, "migrate", None), ("small51", 2, None, "migrate", None),
+    ("singles51", 2, None, "migrate", None), ("small51", 3, None, "migrate", None),
+    ("small51", 3, 64, "migrate", None), ("mixed19", 3, 1000, "migrate", None),
     ("mixed19", 2, None, "fixed", None), ("small51", 2, None, "fixed", None),
     ("singles51", 2, None, "fixed", None), ("small51", 3, None, "fixed", None),
     ("small51", 3, 64, "fixed", None), ("small51", 3, None, "fixed", 2),

@@ -21,7 +21,8 @@ def check_ranks(g, texts, P):
         assert got == g.truth(b, e), f"rank {r}"
 
 
-@pytest.mark.parametrize("protocol,cap", [("fixed", None), ("fixed", 3), ("variable", None)])
+@pytest.mark.parametrize("protocol,cap", [("migrate", None), ("fixed", None), ("fixed", 3),
+                                          ("variable", None)])
 @pytest.mark.parametrize("name", ["mixed19", "small51", "singles51", "k30", "k60", "tiny19"])
 @pytest.mark.parametrize("P", [1, 2, 3, 4])
 def test_sharded_golden(name, P, protocol, cap):
@@ -37,7 +38,7 @@ def test_sharded_golden(name, P, protocol, cap):
     assert sorted(b"".join(texts).splitlines()) == sorted(want.splitlines())
 
 
-@pytest.mark.parametrize("protocol", ["fixed", "variable"])
+@pytest.mark.parametrize("protocol", ["migrate", "fixed", "variable"])
 @pytest.mark.parametrize("k,n,P", [(51, 2_000_000, 8), (19, 1_000_000, 4)])
 def test_sharded_generated(k, n, P, protocol):
     from cs267_hw3_amd.dist import run_threaded
@@ -46,7 +47,7 @@ def test_sharded_generated(k, n, P, protocol):
     check_ranks(g, texts, P)
 
 
-@pytest.mark.parametrize("protocol", ["fixed", "variable"])
+@pytest.mark.parametrize("protocol", ["migrate", "fixed", "variable"])
 def test_sharded_missing_kmer_raises(protocol):
     from cs267_hw3_amd.dist import run_threaded
     m = MANIFEST["tiny19"]
@@ -58,7 +59,7 @@ def test_sharded_missing_kmer_raises(protocol):
 
 
 @pytest.mark.parametrize("mode", ["cas", "part"])
-@pytest.mark.parametrize("P", [1, 2])
+@pytest.mark.parametrize("P", [1, 2, 5])
 def test_sharded_large_both_insert_paths(monkeypatch, mode, P):
     """>= 1M routed words per rank: the partitioned build consumes words, not records."""
     from cs267_hw3_amd.dist import run_threaded
@@ -82,3 +83,12 @@ def test_insert_words_direct(monkeypatch, mode):
         sh.sync()
     s = sh.stats()
     assert s["n_dup"] == 0 and s["n_inserted"] == 3_000_000
+
+
+def test_sharded_long_contigs_migrate():
+    """C2-like chains (hundreds of k-mers): many self-migrations (run word budget) and
+    cross-rank hops per walker."""
+    from cs267_hw3_amd.dist import run_threaded
+    g = kh.SyntheticKmers(19, 2_000_000, 200, 1374, 0, seed=11)
+    for P in (1, 3):
+        check_ranks(g, run_threaded(19, g.records(), P), P)
