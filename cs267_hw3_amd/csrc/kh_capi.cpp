@@ -84,7 +84,7 @@ struct kh_table {
     DevBuf stage;                            // host-API staging of records / keys
     DevBuf stage2, stage3;
     DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text;
-    DevBuf route_hist, route_off, route_scratch;                          // sharded path
+    DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_hist1, pb_off1, pb_hist2, pb_off2, pb_scratch, pb_ovf;  // part build
     bool last_insert_part = false;
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
@@ -270,7 +270,7 @@ int kh_destroy(kh_table* t) {
     DevBuf* bufs[] = {&t->slots, &t->starts, &t->ctr, &t->stats, &t->mask, &t->mask_off,
                       &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
                       &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
-                      &t->route_hist, &t->route_off, &t->route_scratch, &t->rw_hi, &t->rw_lo,
+                      &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->rw_hi, &t->rw_lo,
                       &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm, &t->rw_pos, &t->rw_ctl,
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store,
@@ -620,11 +620,13 @@ int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
     if (!counts_out || (n && (!dev_recs || !words_out))) return fail(KH_ERR_ARG, "null buffer");
+    if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
     if (int rc = set_device(t)) return rc;
     if (int rc = ensure_route(t, n, nranks)) return rc;
+    if (int rc = t->route_own.ensure(n + 16)) return rc;
     KH_HIP(kh::launch_route(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks,
                             t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
-                            t->route_scratch.as<uint64_t>(), (uint64_t*)words_out,
+                            t->route_scratch.as<uint64_t>(), t->route_own.as<uint8_t>(), (uint64_t*)words_out,
                             (uint64_t*)counts_out, t->stream));
     return KH_OK;
 }

@@ -456,36 +456,86 @@ hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, 
     return hipGetLastError();
 }
 
+// Route = records -> owner-grouped words in two streaming passes over the records (the owner,
+// a minimizer hash, is computed once and kept as one byte per record). Records are staged
+// through LDS with 16-B loads (15-/7-byte records are unaligned for per-lane loads).
+__device__ __forceinline__ void stage_records(const uint8_t* recs, uint64_t sub, uint32_t cnt, uint32_t R,
+                                              uint8_t* st) {
+    const uint32_t bytes = cnt * R, nvec = bytes >> 4;
+    const uint4* src = reinterpret_cast<const uint4*>(recs + sub * R);
+    for (uint32_t v = threadIdx.x; v < nvec; v += BLOCK) reinterpret_cast<uint4*>(st)[v] = src[v];
+    for (uint32_t x = (nvec << 4) + threadIdx.x; x < bytes; x += BLOCK) st[x] = recs[sub * R + x];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
+                                                     uint32_t P, uint8_t* own, uint64_t* hist) {
+    __shared__ uint32_t h[MAX_RANKS];
+    __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+    for (uint32_t j = 0; j < ROUTE_TILE / BLOCK; ++j) {
+        const uint64_t sub = b0 + (uint64_t)j * BLOCK;
+        if (sub >= n) break;  // uniform
+        const uint32_t cnt = n - sub < (uint64_t)BLOCK ? (uint32_t)(n - sub) : (uint32_t)BLOCK;
+        __syncthreads();
+        stage_records(recs, sub, cnt, (uint32_t)p.R, st);
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            const Key k = key_from_packed(st + threadIdx.x * p.R, p);
+            const uint32_t q = owner_key(k, p, P);
+            own[sub + threadIdx.x] = (uint8_t)q;
+            atomicAdd(&h[q], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) hist[(uint64_t)blockIdx.x * P + q] = h[q];
+}
+
 template <int W>
-struct RouteOp {
-    KParams p;
-    const uint8_t* recs;
-    uint32_t P;
-    uint64_t* out;
-    __device__ int owner(uint64_t i) const {
-        const Key k = key_from_packed(recs + i * (uint64_t)p.R, p);
-        return (int)owner_key(k, p, P);
+__global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
+                                                         uint32_t P, const uint8_t* __restrict__ own,
+                                                         const uint64_t* off, uint64_t nb, uint64_t* out) {
+    __shared__ uint32_t h[MAX_RANKS];
+    __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+    for (uint32_t j = 0; j < ROUTE_TILE / BLOCK; ++j) {
+        const uint64_t sub = b0 + (uint64_t)j * BLOCK;
+        if (sub >= n) break;  // uniform
+        const uint32_t cnt = n - sub < (uint64_t)BLOCK ? (uint32_t)(n - sub) : (uint32_t)BLOCK;
+        __syncthreads();
+        stage_records(recs, sub, cnt, (uint32_t)p.R, st);
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            Key k;
+            uint32_t ext;
+            parse_record(st + threadIdx.x * p.R, p, k, ext);
+            const uint32_t q = own[sub + threadIdx.x];
+            const uint64_t d = off[(uint64_t)q * nb + blockIdx.x] + atomicAdd(&h[q], 1u);
+            if (W == 2)
+                *reinterpret_cast<ulonglong2*>(out + d * 2) = make_ulonglong2(slot_w0(k, ext, p), k.lo);
+            else
+                out[d] = slot_w0(k, ext, p);
+        }
     }
-    __device__ void emit(uint64_t i, int q, uint64_t dst) const {
-        Key k;
-        uint32_t ext;
-        parse_record(recs + i * (uint64_t)p.R, p, k, ext);
-        out[dst * W] = slot_w0(k, ext, p);
-        if (W == 2) out[dst * W + 1] = k.lo;
-    }
-};
+}
 
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
-                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out_words,
+                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint8_t* own, uint64_t* out_words,
                         uint64_t* counts, hipStream_t s) {
-    // the scan's total goes to counts[nranks] via a device word: reuse the last hist entry slot
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    uint64_t* sc = scratch + 1;
+    const uint64_t nb = route_blocks(n);
+    if (nb == 0) return hipMemsetAsync(counts, 0, (nranks + 1) * 8, s);
+    k_route_own<<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist);
+    hipError_t e = scan_exclusive(HistF{hist, nb, nranks}, nb * nranks, off, scratch + 1,
+                                  (unsigned long long*)nullptr, total, s);
+    if (e != hipSuccess) return e;
+    k_route_counts<0><<<1, MAX_RANKS, 0, s>>>(off, nb, nranks, total, counts);
     if (p.W == 1)
-        return group_by_owner(RouteOp<1>{p, recs, nranks, out_words}, n, nranks, hist, off, sc, counts,
-                              total, s);
-    return group_by_owner(RouteOp<2>{p, recs, nranks, out_words}, n, nranks, hist, off, sc, counts,
-                          total, s);
+        k_route_scatter<1><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, off, nb, out_words);
+    else
+        k_route_scatter<2><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, off, nb, out_words);
+    return hipGetLastError();
 }
 
 template <int W>

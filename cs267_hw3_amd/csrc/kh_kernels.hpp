@@ -84,7 +84,7 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
 // origin | state << 8]; text record: 2 words [origin << 56 | fin << 55 | word_no << 31 | idx,
 // word (or bases appended, fin)].
 static constexpr int MSG_WORDS = 5;
-static constexpr int MW_RUN_WORDS = 6;                  // words a walker may flush per round
+static constexpr int MW_RUN_WORDS = 8;                  // words a walker may flush per round
 static constexpr int MW_REC_SLOTS = MW_RUN_WORDS + 2;   // + final partial word + finish record
 struct MWalkRound {
     uint32_t P, rank;
@@ -139,7 +139,7 @@ hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, 
 // Records -> internal words (W per record) grouped by owner rank (owner_key).
 // hist/off: route_blocks(n) * nranks words each; counts: nranks + 1 words (last = n).
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
-                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out_words,
+                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint8_t* own, uint64_t* out_words,
                         uint64_t* counts, hipStream_t s);
 
 // Insert routed internal words.

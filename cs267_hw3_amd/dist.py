@@ -42,6 +42,12 @@ class TorchComm:
     def all_to_all(self, out, inp, out_splits, in_splits):
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
+    def all_to_all_list(self, outs, inps):
+        """Per-peer views in and out (no packing copies); RCCL runs it as grouped send/recv."""
+        if self.backend != "nccl":
+            raise NotImplementedError
+        self.dist.all_to_all(outs, inps, group=self.group)
+
     def barrier(self):
         self.dist.barrier(group=self.group)
 
@@ -318,6 +324,16 @@ class DistributedKmerHashMap:
         for q in range(1, P):
             in_off[q] = in_off[q - 1] + in_splits[q - 1]
             out_off[q] = out_off[q - 1] + out_splits[q - 1]
+        if getattr(self.comm, "backend", None) == "nccl":
+            # views straight into the packed buffers: no staging copies
+            for r in range(rounds):
+                lo = r * limit
+                sc = [max(0, min(limit, in_splits[q] - lo)) for q in range(P)]
+                rc = [max(0, min(limit, out_splits[q] - lo)) for q in range(P)]
+                self.comm.all_to_all_list(
+                    [out[out_off[q] + lo:out_off[q] + lo + rc[q]] for q in range(P)],
+                    [inp[in_off[q] + lo:in_off[q] + lo + sc[q]] for q in range(P)])
+            return
         for r in range(rounds):
             lo = r * limit
             sc = [max(0, min(limit, in_splits[q] - lo)) for q in range(P)]
@@ -339,9 +355,12 @@ class DistributedKmerHashMap:
         send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
         W = sh.W
         m = sum(recv_splits)
-        recv = self._int64(words, m * W)
-        self._all_to_all(recv[:m * W], words[:sum(send_splits) * W],
-                         [c * W for c in recv_splits], [c * W for c in send_splits], gmax * W)
+        if P == 1:
+            recv = words                       # one rank: nothing to exchange
+        else:
+            recv = self._int64(words, m * W)
+            self._all_to_all(recv[:m * W], words[:sum(send_splits) * W],
+                             [c * W for c in recv_splits], [c * W for c in send_splits], gmax * W)
         sh.insert_words(recv, m)
         return m
 
@@ -443,9 +462,12 @@ class DistributedKmerHashMap:
             if sum(totals) == 0:
                 break
             m = sum(recv_splits)
-            nxt = self._grow("_mw_in", max(m, 1) * M, torch.int64, out.device)
-            self._all_to_all(nxt[:m * M], out[:sum(send_splits) * M], [c * M for c in recv_splits],
-                             [c * M for c in send_splits], gmax * M)
+            if P == 1:
+                nxt = out      # the round kernel reads its input before the grouping rewrites it
+            else:
+                nxt = self._grow("_mw_in", max(m, 1) * M, torch.int64, out.device)
+                self._all_to_all(nxt[:m * M], out[:sum(send_splits) * M], [c * M for c in recv_splits],
+                                 [c * M for c in send_splits], gmax * M)
             # ping-pong: the next round reads _mw_in and writes _mw_out
             inp, n_in = nxt, m
         nrec = sh.mw_text_count()
@@ -453,9 +475,12 @@ class DistributedKmerHashMap:
         counts = sh.mw_text(tout)
         send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
         r = sum(recv_splits)
-        trecv = sh.zeros(max(r, 1) * T, torch.int64)
-        self._all_to_all(trecv[:r * T], tout[:nrec * T], [c * T for c in recv_splits],
-                         [c * T for c in send_splits], gmax * T)
+        if P == 1:
+            trecv = tout
+        else:
+            trecv = sh.zeros(max(r, 1) * T, torch.int64)
+            self._all_to_all(trecv[:r * T], tout[:nrec * T], [c * T for c in recv_splits],
+                             [c * T for c in send_splits], gmax * T)
         sh.mw_end(trecv, r)
         sh.sync()
         return self.rounds
