@@ -5,7 +5,7 @@ the C-ABI library libkmerhash_amd.so (include/kmer_hash_amd.h) with hand-written
 this package is its Python host mirror (ctypes).
 """
 from .hashmap import (KmerHashError, KmerHashTable, SyntheticKmers, device_count, djb2,  # noqa: F401
-                      kmer_size, next_kmer, pack_kmer, pack_text, packed_size, read_kmers,
+                      kmer_size, next_kmer, pack_kmer, pack_text, packed_size, read_kmer_lines, read_kmers,
                       record_size, unpack_kmer)
 
 __version__ = "0.1.0"

@@ -32,7 +32,7 @@ class KhStats(ctypes.Structure):
         "capacity", "n_inserted", "n_starts", "n_contigs", "n_lookups", "out_bytes", "n_chunks",
         "n_dup", "n_full", "n_bad_ext", "n_missing", "n_cycle", "n_spin", "n_chunk_ovf")] + [
         (name, ctypes.c_double) for name in (
-            "ms_insert", "ms_insert_kernel", "ms_walk", "ms_materialize")]
+            "ms_insert", "ms_insert_kernel", "ms_walk", "ms_materialize")] + [("n_bad_base", c_u64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -80,6 +80,7 @@ _SIGS = {
     "kh_find_ext_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp]),
     "kh_walk_active_dev": (ctypes.c_int, [c_vp, c_vp]),
     "kh_walk_signature": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
+    "kh_pack_text_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, ctypes.POINTER(c_u64)]),
     "kh_mwalk_begin": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u64, ctypes.POINTER(c_u64)]),
     "kh_mwalk_round_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
     "kh_mwalk_text_count": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),

@@ -158,6 +158,8 @@ int check_stats(kh_table* t) {
     if (st[kh::ST_CYCLE]) return fail(KH_ERR_CYCLE, "%llu walks exceeded the table size", st[kh::ST_CYCLE]);
     if (st[kh::ST_SPIN]) return fail(KH_ERR_HIP, "%llu inserts timed out on a slot", st[kh::ST_SPIN]);
     if (st[kh::ST_CHUNK_OVF]) return fail(KH_ERR_NOMEM, "walker chunk pool overflow");
+    if (st[kh::ST_BAD_BASE])
+        return fail(KH_ERR_BAD_BASE, "%llu k-mer lines with a base outside {A,C,G,T}", st[kh::ST_BAD_BASE]);
     return KH_OK;
 }
 
@@ -525,6 +527,7 @@ int kh_get_stats(kh_table* t, kh_stats* s) {
     s->n_cycle = st[kh::ST_CYCLE];
     s->n_spin = st[kh::ST_SPIN];
     s->n_chunk_ovf = st[kh::ST_CHUNK_OVF];
+    s->n_bad_base = st[kh::ST_BAD_BASE];
     float ms = 0.f;
     if (t->ins_timed) {
         if (hipEventElapsedTime(&ms, t->ev_ins0, t->ev_ins2) == hipSuccess) s->ms_insert = ms;
@@ -612,6 +615,19 @@ int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n) {
                                      t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(),
                                      t->stream));
     t->assembled = false;
+    return KH_OK;
+}
+
+int kh_pack_text_dev(kh_table* t, const void* dev_text, uint64_t len, void* dev_recs, uint64_t* n_out) {
+    if (!t || !n_out) return fail(KH_ERR_ARG, "null argument");
+    const uint64_t n = len / ((uint64_t)t->kp.K + 4);  // read_kmers.hpp:64 fixed line length
+    *n_out = n;
+    if (!dev_recs || n == 0) return KH_OK;
+    if (!dev_text) return fail(KH_ERR_ARG, "null text");
+    if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_pack_text(t->kp, (const char*)dev_text, n, (uint8_t*)dev_recs,
+                                t->stats.as<unsigned long long>(), t->stream));
     return KH_OK;
 }
 

@@ -393,6 +393,73 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* c
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Text parse (read_kmers.hpp:62-76 + packKmer, packing.hpp:77-92). A block stages 256 lines
+// through LDS with aligned 16-B loads (lines are K+4 bytes, unaligned), packs each line's K
+// bases in a register pair, and stores its 256 records back with 16-B stores.
+static constexpr int TXT_MAX_LINE = KMAX + 4;
+
+__global__ __launch_bounds__(BLOCK) void k_pack_text(KParams p, const char* __restrict__ text, uint64_t n,
+                                                     uint8_t* __restrict__ recs, unsigned long long* stats) {
+    __shared__ uint4 in_st[(BLOCK * TXT_MAX_LINE + 32) / 16];
+    __shared__ uint4 out_st[(BLOCK * 17 + 16) / 16];
+    __shared__ uint32_t bad;
+    const uint32_t Lb = (uint32_t)p.K + 4, R = (uint32_t)p.R;
+    const uint64_t end = n * Lb;  // bytes of complete lines: never read past them
+    if (threadIdx.x == 0) bad = 0;
+    for (uint64_t sub = (uint64_t)blockIdx.x * BLOCK; sub < n; sub += (uint64_t)gridDim.x * BLOCK) {
+        const uint32_t cnt = n - sub < (uint64_t)BLOCK ? (uint32_t)(n - sub) : (uint32_t)BLOCK;
+        const int64_t a = (int64_t)(sub * Lb), b = a + (int64_t)cnt * Lb, e = (int64_t)end;
+        const uint32_t mis = (uint32_t)((uintptr_t)(text + a) & 15u);
+        const int64_t a0 = a - mis;                    // precedes the buffer only when a == 0
+        const uint32_t nv = (uint32_t)((b - a0 + 15) / 16);
+        __syncthreads();
+        for (uint32_t v = threadIdx.x; v < nv; v += BLOCK) {
+            const int64_t lo = a0 + (int64_t)v * 16;
+            if (lo >= a && lo + 16 <= e) {
+                in_st[v] = *reinterpret_cast<const uint4*>(text + lo);
+            } else {  // partial vector at either edge of the text: byte loads inside [a, end)
+                uint8_t* d = reinterpret_cast<uint8_t*>(&in_st[v]);
+                for (int x = 0; x < 16; ++x) d[x] = (lo + x >= a && lo + x < e) ? (uint8_t)text[lo + x] : 0;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            const uint8_t* l = reinterpret_cast<const uint8_t*>(in_st) + mis + threadIdx.x * Lb;
+            uint64_t hi = 0, lo = 0;  // V = hi:lo, 2 bits per base, base 0 most significant
+            uint32_t badl = 0;
+            for (int i = 0; i < p.K; ++i) {
+                const uint32_t c = base_code(l[i]);
+                badl |= c > 3;
+                hi = (hi << 2) | (lo >> 62);
+                lo = (lo << 2) | (c & 3u);
+            }
+            if (badl) atomicAdd(&bad, 1u);
+            const Key k{(hi << 2) | (lo >> 62), lo & LO_MASK};
+            uint8_t* o = reinterpret_cast<uint8_t*>(out_st) + threadIdx.x * R;
+            key_to_packed(k, o, p);
+            o[p.P] = l[p.K + 1];
+            o[p.P + 1] = l[p.K + 2];
+        }
+        __syncthreads();
+        const uint32_t ob = cnt * R, onv = ob >> 4;
+        uint8_t* dst = recs + sub * R;  // 16-B aligned: sub is a multiple of 256, recs aligned
+        for (uint32_t v = threadIdx.x; v < onv; v += BLOCK) reinterpret_cast<uint4*>(dst)[v] = out_st[v];
+        for (uint32_t x = (onv << 4) + threadIdx.x; x < ob; x += BLOCK)
+            dst[x] = reinterpret_cast<const uint8_t*>(out_st)[x];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && bad) atomicAdd(&stats[ST_BAD_BASE], (unsigned long long)bad);
+}
+
+hipError_t launch_pack_text(const KParams& p, const char* text, uint64_t n, uint8_t* recs,
+                            unsigned long long* stats, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)hmin((n + BLOCK - 1) / BLOCK, 4096);
+    k_pack_text<<<g, BLOCK, 0, s>>>(p, text, n, recs, stats);
+    return hipGetLastError();
+}
+
 hipError_t launch_contig_offsets(int K, const uint32_t* len, uint64_t nc, uint64_t* offsets,
                                  uint64_t* scratch, unsigned long long* total, hipStream_t s) {
     return scan_exclusive(ContigBytesF{len, (uint64_t)K}, nc, offsets, scratch, (unsigned long long*)nullptr,

@@ -16,6 +16,7 @@ enum StatIdx : int {
     ST_CYCLE = 4,      // walk: more steps than k-mers in the table (no 'F' terminator)
     ST_SPIN = 5,       // insert: gave up waiting for a half-published 16 B slot
     ST_CHUNK_OVF = 6,  // walk: contig chunk pool exhausted (sized as an upper bound; never expected)
+    ST_BAD_BASE = 7,   // text parse: k-mer character outside {A,C,G,T}
     ST_NUM = 8
 };
 
@@ -111,6 +112,11 @@ hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_
                           unsigned long long* fin, hipStream_t s);
 hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
                            const uint64_t* off, char* out, hipStream_t s);
+
+// read_kmers.hpp:62-76 on the device: n fixed-width "KMER BF\n" lines (K+4 bytes) -> kmer_pair
+// records; lines with a non-ACGT k-mer character count in stats[ST_BAD_BASE].
+hipError_t launch_pack_text(const KParams& p, const char* text, uint64_t n, uint8_t* recs,
+                            unsigned long long* stats, hipStream_t s);
 
 // Pieces of the materialisation for other walkers: offsets (+ total bytes) and start k-mer heads
 // (with the trailing '\n' at off + K + len - 1).

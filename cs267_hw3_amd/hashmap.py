@@ -48,8 +48,8 @@ def kmer_size(fname):
         return len(f.readline().split()[0])
 
 
-def read_kmers(fname, k, nprocs=1, rank=0):
-    """read_kmers.hpp:54-79 block split: rank r gets lines [r*ceil(n/P), ...)."""
+def read_kmer_lines(fname, k, nprocs=1, rank=0):
+    """read_kmers.hpp:54-68 block split: the raw text of lines [r*ceil(n/P), ...) of rank r."""
     line = k + 4
     size = os.path.getsize(fname)
     n = size // line
@@ -58,8 +58,12 @@ def read_kmers(fname, k, nprocs=1, rank=0):
     cnt = min(split, n - start)
     with open(fname, "rb") as f:
         f.seek(start * line)
-        data = f.read(cnt * line)
-    return pack_text(k, data)
+        return f.read(cnt * line)
+
+
+def read_kmers(fname, k, nprocs=1, rank=0):
+    """read_kmers.hpp:54-79: rank r's block of the file as kmer_pair records (host codec)."""
+    return pack_text(k, read_kmer_lines(fname, k, nprocs, rank))
 
 
 def pack_kmer(k, kmer):
@@ -155,6 +159,14 @@ class KmerHashTable:
 
     insert = insert_all
 
+    def pack_text_dev(self, text_ptr, nbytes, recs_ptr=None):
+        """read_kmers.hpp:62-76 on the GPU (device text -> device records at recs_ptr, 16-B
+        aligned); returns the record count. Bad bases surface at the next sync()."""
+        n = ctypes.c_uint64(0)
+        check(self._L.kh_pack_text_dev(self._h, ctypes.c_void_p(text_ptr), nbytes,
+                                       ctypes.c_void_p(recs_ptr) if recs_ptr else None, ctypes.byref(n)))
+        return n.value
+
     def insert_dev(self, dev_ptr, n):
         """Asynchronous insert of n records already in device memory (16-B aligned)."""
         check(self._L.kh_insert_dev(self._h, ctypes.c_void_p(dev_ptr), int(n)))
@@ -244,6 +256,6 @@ class SyntheticKmers:
         return out.tobytes()
 
 
-__all__ = ["KmerHashTable", "SyntheticKmers", "KmerHashError", "pack_text", "read_kmers",
+__all__ = ["KmerHashTable", "SyntheticKmers", "KmerHashError", "pack_text", "read_kmers", "read_kmer_lines",
            "kmer_size", "pack_kmer", "unpack_kmer", "djb2", "next_kmer", "device_count",
            "packed_size", "record_size"]

@@ -63,6 +63,7 @@ typedef struct kh_stats {
     double ms_insert_kernel; /* device ms, k_insert alone, last insert call */
     double ms_walk;          /* device ms, k_walk, last assemble */
     double ms_materialize;   /* device ms, offsets scan + contig text, last assemble */
+    uint64_t n_bad_base;     /* kh_pack_text_dev lines with a k-mer base outside {A,C,G,T} */
 } kh_stats;
 
 /* ---- sizes / info --------------------------------------------------------------------------*/
@@ -113,6 +114,11 @@ int kh_contigs_offsets(kh_table* t, uint64_t* host_offsets, uint64_t n); /* line
  * nranks + 1 uint64 on the device: per-destination counts, then their total. All async. */
 int kh_word_count(int k);
 int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n); /* local start k-mers */
+/* read_kmers.hpp:62-76 on the GPU: len bytes of fixed-width "KMER BF\n" lines (k+4 bytes each)
+ * in device memory -> *n_out = len / (k+4) kmer_pair records at dev_recs (16-byte aligned; NULL:
+ * count only), on the table's stream. A line whose k-mer has a base outside {A,C,G,T} makes the
+ * next kh_sync fail with KH_ERR_BAD_BASE (the host kh_pack_text fails at once). */
+int kh_pack_text_dev(kh_table* t, const void* dev_text, uint64_t len, void* dev_recs, uint64_t* n_out);
 int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
                  void* dev_counts_out);
 int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);

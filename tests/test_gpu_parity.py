@@ -228,3 +228,55 @@ def test_part_build_detects_duplicates(monkeypatch):
         t.insert_all(dup)
     assert e.value.code == _lib.KH_ERR_DUPLICATE
     assert t.stats()["n_dup"] == 1000
+
+
+# ---- §8(f)2: the text parser on the GPU ---------------------------------------------------------
+@pytest.mark.parametrize("name", ["mixed19", "small51", "k30", "k60", "tiny19"])
+def test_gpu_pack_text_golden(name):
+    """kh_pack_text_dev == the host codec (pinned by the reference KATs) on the golden text."""
+    import torch
+    m = MANIFEST[name]
+    raw = open(os.path.join(GOLDEN, f"{name}.txt"), "rb").read()
+    want = kh.pack_text(m["k"], raw)
+    t = kh.KmerHashTable(m["k"], 16)
+    R = kh.record_size(m["k"])
+    for off in (0, 1, 7):  # unaligned text starts
+        buf = torch.zeros(len(raw) + 16, dtype=torch.uint8)
+        buf[off:off + len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        d = buf.cuda()
+        recs = torch.empty(len(want) * R + 16, dtype=torch.uint8, device="cuda")
+        n = t.pack_text_dev(d.data_ptr() + off, len(raw), recs.data_ptr())
+        t.sync()
+        assert n == len(want)
+        assert bytes(recs[:n * R].cpu().numpy()) == want.tobytes()
+
+
+@pytest.mark.parametrize("k", [19, 51])
+def test_gpu_pack_text_large_and_bad_base(k):
+    import torch
+    g = kh.SyntheticKmers(k, 300_001, 8, 200, 10, seed=3)
+    recs = g.records()
+    line = k + 4
+    text = np.empty((len(recs), line), np.uint8)
+    # text from records through the host codec (unpack) -- vectorised per base
+    P = (k + 3) // 4
+    packed = recs[:, :P]
+    bits = np.unpackbits(packed, axis=1)[:, :2 * k].reshape(len(recs), k, 2)
+    codes = bits[:, :, 0] * 2 + bits[:, :, 1]
+    text[:, :k] = np.frombuffer(b"ACGT", np.uint8)[codes]
+    text[:, k] = ord(" ")
+    text[:, k + 1] = recs[:, P]
+    text[:, k + 2] = recs[:, P + 1]
+    text[:, k + 3] = ord("\n")
+    t = kh.KmerHashTable(k, 16)
+    d = torch.from_numpy(text.reshape(-1)).cuda()
+    out = torch.empty(len(recs) * (P + 2) + 16, dtype=torch.uint8, device="cuda")
+    n = t.pack_text_dev(d.data_ptr(), d.numel(), out.data_ptr())
+    t.sync()
+    assert n == len(recs)
+    assert np.array_equal(out[:n * (P + 2)].cpu().numpy().reshape(n, P + 2), recs)
+    text[12345, 3] = ord("N")
+    d = torch.from_numpy(text.reshape(-1)).cuda()
+    t.pack_text_dev(d.data_ptr(), d.numel(), out.data_ptr())
+    with pytest.raises(kh.KmerHashError):
+        t.sync()
