@@ -201,7 +201,7 @@ __device__ __forceinline__ void sorted_write(const uint64_t (&a)[PITEMS], const 
 template <int W>
 __global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* __restrict__ recs,
                                                       uint64_t n, uint64_t* words_out, uint64_t* hist1,
-                                                      uint64_t* start_mask) {
+                                                      uint64_t* start_mask, uint64_t* split_mask) {
     __shared__ uint32_t h[NB1];
     __shared__ __attribute__((aligned(16))) uint8_t stage[2][PB * 17];
     for (int i = threadIdx.x; i < NB1; i += PB) h[i] = 0;
@@ -232,9 +232,15 @@ __global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* 
         Key k{0, 0};
         uint32_t ext = 0;
         if (valid) parse_record(st + threadIdx.x * R, p, k, ext);
-        const uint64_t bal = __ballot(valid && ext_bwd(ext) == EXT_F);
+        const bool is_start = valid && ext_bwd(ext) == EXT_F;
+        const uint64_t bal = __ballot(is_start);
         const uint64_t wb = sub + (threadIdx.x & ~63u);
         if ((threadIdx.x & 63) == 0 && wb < b1 && start_mask) start_mask[wb >> 6] = bal;
+        const uint64_t hk = key_hash(k);
+        if (split_mask) {
+            const uint64_t sb = __ballot(valid && !is_start && is_splitter(hk, p));
+            if ((threadIdx.x & 63) == 0 && wb < b1) split_mask[wb >> 6] = sb;
+        }
         if (valid) {
             const uint64_t w0 = slot_w0(k, ext, p), i = sub + threadIdx.x;
             if (W == 2) {
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* 
             } else {
                 words_out[i] = w0;
             }
-            atomicAdd(&h[key_hash(k) >> (64 - B1)], 1u);
+            atomicAdd(&h[hk >> (64 - B1)], 1u);
         }
     }
     __syncthreads();
@@ -503,6 +509,7 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
 template <int W, bool REC>
 static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
                               TableView t, bool table_empty, const PartBuffers& B, uint64_t* start_mask,
+                              uint64_t* split_mask,
                               unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
     static bool attrs = false;  // per template instance
     hipError_t e;
@@ -516,7 +523,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     const unsigned nb1 = (unsigned)pl.nb1;
     if (REC) {
         // records -> words (input order) in buf2, which pass 2 only writes after pass 1 is done
-        k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, B.hist1, start_mask);
+        k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, B.hist1, start_mask, split_mask);
         words = B.buf2;
     } else {
         k_part1_hist<W, false><<<nb1, PB, 0, s>>>(p, nullptr, words, n, B.hist1, nullptr);
@@ -543,15 +550,17 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
 
 hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
                               TableView t, bool table_empty, const PartBuffers& b,
-                              uint64_t* start_mask, unsigned long long* ctr,
+                              uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
                               unsigned long long* stats, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (recs) {
-        return p.W == 1 ? part_insert<1, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, ctr, stats, s)
-                        : part_insert<2, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, ctr, stats, s);
+        return p.W == 1 ? part_insert<1, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
+                                               stats, s)
+                        : part_insert<2, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
+                                               stats, s);
     }
-    return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, ctr, stats, s)
-                    : part_insert<2, false>(p, nullptr, words, n, t, table_empty, b, nullptr, ctr, stats, s);
+    return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s)
+                    : part_insert<2, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s);
 }
 
 }  // namespace kh

@@ -80,6 +80,8 @@ struct kh_table {
     hipStream_t stream = nullptr;
 
     DevBuf slots, starts, ctr, stats;
+    DevBuf splits, splits_w;                 // splitter k-mers (walk segments) / walk subset
+    DevBuf seg_next, seg_key, seg_contig, seg_off, clen, stab, stab_id;  // splitter segments
     DevBuf mask, mask_off, scratch;          // per insert batch
     DevBuf stage;                            // host-API staging of records / keys
     DevBuf stage2, stage3;
@@ -97,6 +99,8 @@ struct kh_table {
     bool rw_live = false;
     bool rw_stepped = false;   // a fixed-round step has run since kh_walk_begin
     uint64_t starts_cap = 0;                 // start entries the starts buffer holds
+    uint64_t splits_cap = 0, splits_w_cap = 0;
+    bool split_ok = true;                    // every inserted k-mer was checked for splitters
     uint64_t chunk_cap = 0;
 
     uint64_t n_inserted = 0;                 // host-side count (what was submitted)
@@ -117,22 +121,24 @@ int set_device(const kh_table* t) {
 
 kh::TableView view(const kh_table* t) { return kh::TableView{t->slots.as<uint64_t>(), t->cap}; }
 
-int ensure_starts(kh_table* t, uint64_t need) {
-    if (need <= t->starts_cap) return KH_OK;
+int ensure_list(kh_table* t, DevBuf& buf, uint64_t& cap, uint64_t need) {
+    if (need <= cap) return KH_OK;
     const uint64_t W = (uint64_t)t->kp.W;
     uint64_t newcap = need < 1024 ? 1024 : need;
     DevBuf nb;
     int rc = nb.ensure(newcap * W * 8);
     if (rc) return rc;
-    if (t->starts.p && t->starts_cap)
-        KH_HIP(hipMemcpyAsync(nb.p, t->starts.p, t->starts_cap * W * 8, hipMemcpyDeviceToDevice,
-                              t->stream));
+    if (buf.p && cap)
+        KH_HIP(hipMemcpyAsync(nb.p, buf.p, cap * W * 8, hipMemcpyDeviceToDevice, t->stream));
     KH_HIP(hipStreamSynchronize(t->stream));
-    t->starts.release();
-    t->starts = nb;
-    t->starts_cap = newcap;
+    buf.release();
+    buf = nb;
+    nb.p = nullptr;
+    cap = newcap;
     return KH_OK;
 }
+
+int ensure_starts(kh_table* t, uint64_t need) { return ensure_list(t, t->starts, t->starts_cap, need); }
 
 int read_ctr(kh_table* t, int idx, uint64_t* v) {
     unsigned long long x = 0;
@@ -239,6 +245,17 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     t->device = device;
     t->kp = kh::make_params(k);
     t->n_kmers = n_kmers;
+    // splitter density: ~1 per 2^bits k-mers; enough extra walkers for long-chain inputs (C2, C5)
+    // at a few % more walkers on short-contig inputs. KH_SPLIT_BITS overrides (0 = off).
+    // Collected at insert: 1 per 2^bits k-mers, bits = clamp(log2(n / 2^20) + 1, 4, 12); the walk
+    // then uses a subset sized from the start count (kh_assemble_dev).
+    {
+        int bits = 1;
+        while (bits < 12 && (n_kmers >> (20 + bits)) != 0) ++bits;
+        bits = bits < 4 ? 4 : bits;
+        if (const char* e = getenv("KH_SPLIT_BITS")) bits = atoi(e);
+        t->kp.split_bits = bits < 0 ? 0 : (bits > 30 ? 30 : bits);
+    }
     double c = (double)(n_kmers ? n_kmers : 1) / load_factor;
     t->cap = (uint64_t)c;
     if ((double)t->cap < c) t->cap++;
@@ -272,7 +289,8 @@ int kh_destroy(kh_table* t) {
     DevBuf* bufs[] = {&t->slots, &t->starts, &t->ctr, &t->stats, &t->mask, &t->mask_off,
                       &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
                       &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
-                      &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->rw_hi, &t->rw_lo,
+                      &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->splits, &t->splits_w, &t->seg_next,
+                      &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id, &t->rw_hi, &t->rw_lo,
                       &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm, &t->rw_pos, &t->rw_ctl,
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store,
@@ -295,6 +313,7 @@ int kh_clear(kh_table* t) {
     KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
     t->n_inserted = 0;
     t->assembled = false;
+    t->split_ok = true;
     return KH_OK;
 }
 
@@ -325,10 +344,13 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     if (int rc = set_device(t)) return rc;
     int rc;
     const uint64_t nw = (n + 63) / 64;
-    if ((rc = t->mask.ensure(nw * 8))) return rc;
+    const bool split = t->kp.split_bits > 0;
+    if ((rc = t->mask.ensure(nw * 8 * (split ? 2 : 1)))) return rc;
     if ((rc = t->mask_off.ensure(nw * 8))) return rc;
     if ((rc = t->scratch.ensure(kh::scan_scratch_words(nw > n ? nw : n) * 8 + 64))) return rc;
     if ((rc = ensure_starts(t, t->n_inserted + n))) return rc;
+    if (split && (rc = ensure_list(t, t->splits, t->splits_cap, t->n_inserted + n))) return rc;
+    uint64_t* split_mask = split ? t->mask.as<uint64_t>() + nw : nullptr;
     const bool part = use_part_build(t, n);
     kh::PartBuffers pb{};
     if (part && (rc = ensure_part(t, n, pb))) return rc;
@@ -339,18 +361,23 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
     if (part)
         KH_HIP(kh::launch_part_insert(t->kp, (const uint8_t*)dev_recs, nullptr, n, view(t),
-                                      fresh, pb, t->mask.as<uint64_t>(),
+                                      fresh, pb, t->mask.as<uint64_t>(), split_mask,
                                       t->ctr.as<unsigned long long>(),
                                       t->stats.as<unsigned long long>(), t->stream));
     else
         KH_HIP(kh::launch_insert(t->kp, (const uint8_t*)dev_recs, n, view(t), t->mask.as<uint64_t>(),
-                                 t->stats.as<unsigned long long>(), t->stream));
+                                 split_mask, t->stats.as<unsigned long long>(), t->stream));
     t->last_insert_part = part;
     KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
     KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
                                      t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
                                      t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(),
                                      t->stream));
+    if (split)
+        KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, split_mask,
+                                         t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                         t->splits.as<uint64_t>(), t->ctr.as<unsigned long long>(),
+                                         t->stream, kh::CT_N_SPLIT));
     KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
     t->ins_timed = true;
     t->n_inserted += n;
@@ -413,6 +440,7 @@ int kh_set_starts(kh_table* t, const uint8_t* recs, uint64_t n) {
                                   t->ctr.as<unsigned long long>(), t->stream));
     KH_HIP(hipStreamSynchronize(t->stream));
     t->assembled = false;
+    t->split_ok = false;  // caller's starts may share segments (e.g. two starts on one contig)
     return KH_OK;
 }
 
@@ -421,13 +449,46 @@ int kh_assemble_dev(kh_table* t) {
     if (int rc = set_device(t)) return rc;
     if (int rc = clean_slots(t)) return rc;
     int rc;
-    uint64_t ns = 0;
     // The start count decides buffer sizes and the grid (the reference also knows
     // start_nodes.size() on the host before walking, kmer_hash.cpp:41).
-    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
+    unsigned long long cv[kh::CT_NUM];
+    KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    const uint64_t ns = cv[kh::CT_N_STARTS];
+    uint64_t nsp = 0;
+    const unsigned long long* nsp_dev = nullptr;
+    kh::KParams kp = t->kp;
+    if (kp.split_bits && t->split_ok)
+        nsp = cv[kh::CT_N_SPLIT];
+    else
+        kp.split_bits = 0;
+    // Walk density: enough segments for ~1M walkers in all (few, long contigs: C2, C5) but at
+    // least 1 splitter per 4096 k-mers so that no single chain dominates the critical path.
+    const uint64_t* splits = t->splits.as<uint64_t>();
+    if (kp.split_bits && !getenv("KH_SPLIT_BITS")) {
+        const uint64_t want = ns < (1ull << 20) ? (1ull << 20) - ns : 0;
+        const uint64_t floor_cnt = t->n_inserted >> 12;
+        const uint64_t d = want > floor_cnt ? want : floor_cnt;
+        int bw = kp.split_bits;
+        while (bw < 12 && d && (t->n_inserted >> (bw + 1)) >= d) ++bw;
+        if (bw > kp.split_bits && nsp) {
+            if ((rc = ensure_list(t, t->splits_w, t->splits_w_cap, nsp))) return rc;
+            if ((rc = t->scratch.ensure(kh::scan_scratch_words(nsp) * 8 + 64)) ||
+                (rc = t->mask_off.ensure((nsp + 1) * 8)))
+                return rc;
+            KH_HIP(kh::launch_filter_splits(kp, splits, nsp, bw, t->mask_off.as<uint64_t>(),
+                                            t->scratch.as<uint64_t>(), t->splits_w.as<uint64_t>(),
+                                            t->ctr.as<unsigned long long>() + kh::CT_N_SPLIT_W, t->stream));
+            // nsp stays the bound for sizes; kernels read the exact count (no host round trip)
+            nsp_dev = t->ctr.as<unsigned long long>() + kh::CT_N_SPLIT_W;
+            splits = t->splits_w.as<uint64_t>();
+        }
+        kp.split_bits = bw;
+    }
+    const uint64_t nseg = ns + nsp;
     const uint64_t n = t->n_inserted > ns ? t->n_inserted : ns;
-    const uint64_t chunk_cap = n / kh::CHUNK_BASES + ns + 64;
-    if ((rc = t->contig_len.ensure((ns + 1) * 4))) return rc;
+    const uint64_t chunk_cap = n / kh::CHUNK_BASES + nseg + 64;
+    if ((rc = t->contig_len.ensure((nseg + 1) * 4))) return rc;
     if ((rc = t->contig_off.ensure((ns + 1) * 8))) return rc;
     if ((rc = t->chunk_data.ensure(chunk_cap * kh::CHUNK_WORDS * 8))) return rc;
     if ((rc = t->chunk_owner.ensure(chunk_cap * 4))) return rc;
@@ -435,7 +496,7 @@ int kh_assemble_dev(kh_table* t) {
     if ((rc = t->text.ensure(n + ns * ((uint64_t)t->kp.K + 1) + 64))) return rc;
     if ((rc = t->scratch.ensure(kh::scan_scratch_words(ns) * 8 + 64))) return rc;
     t->chunk_cap = chunk_cap;
-    kh::WalkBuffers wb;
+    kh::WalkBuffers wb{};
     wb.starts = t->starts.as<uint64_t>();
     wb.n_starts = ns;
     wb.contig_len = t->contig_len.as<uint32_t>();
@@ -444,13 +505,42 @@ int kh_assemble_dev(kh_table* t) {
     wb.chunk_seq = t->chunk_seq.as<uint32_t>();
     wb.chunk_cap = chunk_cap;
     wb.max_steps = n;
+    kh::SegBuffers sb{};
+    if (kp.split_bits) {
+        // walkers may stop before a splitter k-mer even when none was collected (then the link
+        // step reports it missing), so the segment arrays exist whenever splitting is on
+        const uint64_t cap2 = 2 * nsp + 64;
+        if ((rc = t->seg_next.ensure((nseg + 1) * 4)) || (rc = t->seg_key.ensure((nseg + 1) * 16)) ||
+            (rc = t->seg_contig.ensure((nseg + 1) * 4)) || (rc = t->seg_off.ensure((nseg + 1) * 4)) ||
+            (rc = t->clen.ensure((ns + 1) * 4)) || (rc = t->stab.ensure(cap2 * 16)) ||
+            (rc = t->stab_id.ensure(cap2 * 4)))
+            return rc;
+        wb.splits = splits;
+        wb.n_splits = nsp;
+        wb.n_splits_dev = nsp_dev;
+        wb.seg_next = t->seg_next.as<uint32_t>();
+        wb.seg_key = t->seg_key.as<uint64_t>();
+        sb.stab = t->stab.as<uint64_t>();
+        sb.stab_id = t->stab_id.as<uint32_t>();
+        sb.cap2 = cap2;
+        sb.seg_contig = t->seg_contig.as<uint32_t>();
+        sb.seg_off = t->seg_off.as<uint32_t>();
+        sb.clen = t->clen.as<uint32_t>();
+        KH_HIP(hipMemsetAsync(wb.seg_next, 0xff, nseg * 4, t->stream));
+    }
     unsigned long long* ctr = t->ctr.as<unsigned long long>();
     KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
-    KH_HIP(kh::launch_walk(t->kp, view(t), wb, ctr, t->stats.as<unsigned long long>(), 0, t->stream));
+    KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, t->stats.as<unsigned long long>(), 0, t->stream));
+    if (kp.split_bits)
+        KH_HIP(kh::launch_segments(kp, wb, sb, t->stats.as<unsigned long long>(), t->stream));
     KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
-    KH_HIP(kh::launch_materialize(t->kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                  t->text.as<char>(), ctr, t->stream));
+    if (kp.split_bits)
+        KH_HIP(kh::launch_materialize_seg(kp, wb, sb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                          t->text.as<char>(), ctr, t->stream));
+    else
+        KH_HIP(kh::launch_materialize(kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                      t->text.as<char>(), ctr, t->stream));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = ns;
@@ -656,6 +746,7 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
                     (unsigned long long)m, (unsigned long long)t->n_kmers,
                     (unsigned long long)t->n_inserted);
     if (int rc = set_device(t)) return rc;
+    t->split_ok = false;  // routed words carry no splitter marks: walks on this table use none
     const bool part = use_part_build(t, m);
     kh::PartBuffers pb{};
     if (part)
@@ -667,7 +758,7 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
     if (part)
         KH_HIP(kh::launch_part_insert(t->kp, nullptr, (const uint64_t*)words, m, view(t),
-                                      fresh, pb, nullptr, t->ctr.as<unsigned long long>(),
+                                      fresh, pb, nullptr, nullptr, t->ctr.as<unsigned long long>(),
                                       t->stats.as<unsigned long long>(), t->stream));
     else
         KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
@@ -756,7 +847,7 @@ int kh_walk_apply_dev(kh_table* t, const void* ext, uint64_t m) {
 int kh_walk_end_dev(kh_table* t) {
     if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
     if (int rc = set_device(t)) return rc;
-    kh::WalkBuffers wb;
+    kh::WalkBuffers wb{};
     wb.starts = t->starts.as<uint64_t>();
     wb.n_starts = t->rw_n;
     wb.contig_len = t->contig_len.as<uint32_t>();

@@ -48,6 +48,8 @@ struct KParams {
     uint64_t hi_mask;   // mask for hi after a shift (2K-62 bits, 0 when K <= 31)
     uint64_t v_mask;    // W=1: mask of V (2K bits)
     int M;              // minimizer length (bases) of the sharded owner function
+    int split_bits;     // walk splitters: k-mers with (key_hash & (2^split_bits - 1)) == 0 and a
+                        // predecessor start extra walkers (0 = off); see kh_kernels.hip k_walk
 };
 
 // Minimizer length for owner_key: consecutive k-mers of a contig share their minimizer for
@@ -66,6 +68,7 @@ inline KParams make_params(int K) {
     p.hi_mask = hib > 0 ? ((1ull << hib) - 1) : 0ull;
     p.v_mask = (2 * K >= 64) ? ~0ull : ((1ull << (2 * K)) - 1);
     p.M = minimizer_len(K);
+    p.split_bits = 0;
     return p;
 }
 
@@ -184,6 +187,11 @@ KH_HD uint32_t owner_key(Key k, const KParams& p, uint32_t nranks) {
         hi >>= 2;
     }
     return (uint32_t)(((uint64_t)mix32(best ^ 0x9e3779b9u) * nranks) >> 32);
+}
+
+// Splitter k-mer: cuts long contigs into independently walked segments (sparse ruling set).
+KH_HD bool is_splitter(uint64_t h, const KParams& p) {
+    return p.split_bits && (h & ((1ull << p.split_bits) - 1)) == 0;
 }
 
 // ---- slot encode/decode ---------------------------------------------------------------

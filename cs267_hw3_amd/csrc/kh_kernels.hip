@@ -22,7 +22,7 @@ uint64_t scan_scratch_words(uint64_t m) { return (m + SCAN_TILE - 1) / SCAN_TILE
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_insert(KParams p, const uint8_t* __restrict__ recs,
                                                   uint64_t n, uint64_t* slots, uint64_t cap,
-                                                  uint64_t* start_mask,
+                                                  uint64_t* start_mask, uint64_t* split_mask,
                                                   unsigned long long* stats) {
     __shared__ __attribute__((aligned(16))) uint8_t tile[BLOCK * MAX_R];
     const uint32_t R = (uint32_t)p.R;
@@ -46,6 +46,10 @@ __global__ __launch_bounds__(BLOCK) void k_insert(KParams p, const uint8_t* __re
         const uint64_t bal = __ballot(is_start);
         const uint64_t wbase = base + (threadIdx.x & ~63u);
         if ((threadIdx.x & 63) == 0 && wbase < n) start_mask[wbase >> 6] = bal;
+        if (split_mask) {
+            const uint64_t sb = __ballot(valid && !is_start && is_splitter(key_hash(k), p));
+            if ((threadIdx.x & 63) == 0 && wbase < n) split_mask[wbase >> 6] = sb;
+        }
         if (valid) {
             if (ext_bwd(ext) == EXT_BAD || ext_fwd(ext) == EXT_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
             insert_one<W>(k, ext, p, slots, cap, stats);
@@ -54,14 +58,14 @@ __global__ __launch_bounds__(BLOCK) void k_insert(KParams p, const uint8_t* __re
 }
 
 hipError_t launch_insert(const KParams& p, const uint8_t* recs, uint64_t n, TableView t,
-                         uint64_t* start_mask, unsigned long long* stats, hipStream_t s) {
+                         uint64_t* start_mask, uint64_t* split_mask, unsigned long long* stats, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint64_t ntiles = (n + BLOCK - 1) / BLOCK;
     const unsigned grid = (unsigned)hmin(ntiles, 256ull * 32);
     if (p.W == 1)
-        k_insert<1><<<grid, BLOCK, 0, s>>>(p, recs, n, t.slots, t.cap, start_mask, stats);
+        k_insert<1><<<grid, BLOCK, 0, s>>>(p, recs, n, t.slots, t.cap, start_mask, split_mask, stats);
     else
-        k_insert<2><<<grid, BLOCK, 0, s>>>(p, recs, n, t.slots, t.cap, start_mask, stats);
+        k_insert<2><<<grid, BLOCK, 0, s>>>(p, recs, n, t.slots, t.cap, start_mask, split_mask, stats);
     return hipGetLastError();
 }
 
@@ -94,10 +98,10 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_starts(KParams p, const uint8
 hipError_t launch_collect_starts(const KParams& p, const uint8_t* recs, uint64_t n,
                                  const uint64_t* start_mask, uint64_t* mask_offsets,
                                  uint64_t* scratch, uint64_t* starts, unsigned long long* ctr,
-                                 hipStream_t s) {
+                                 hipStream_t s, int ctr_idx) {
     if (n == 0) return hipSuccess;
     const uint64_t nw = (n + 63) >> 6;
-    hipError_t e = scan_exclusive(PopcF{start_mask}, nw, mask_offsets, scratch, &ctr[CT_N_STARTS],
+    hipError_t e = scan_exclusive(PopcF{start_mask}, nw, mask_offsets, scratch, &ctr[ctr_idx],
                                   (unsigned long long*)nullptr, s);
     if (e != hipSuccess) return e;
     const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK, 4096);
@@ -220,14 +224,18 @@ __device__ __forceinline__ void finish_contig(const LaneOut& o, uint64_t c, uint
         o.chunk_data[(uint64_t)chunk * CHUNK_WORDS + ((steps >> 5) & 7)] = buf;
 }
 
+__device__ __forceinline__ uint64_t walk_splits(const WalkBuffers& wb) {
+    return wb.n_splits_dev ? (uint64_t)*wb.n_splits_dev : wb.n_splits;
+}
+
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __restrict__ slots,
                                                 uint64_t cap, WalkBuffers wb,
                                                 unsigned long long* ctr,
                                                 unsigned long long* stats) {
     const uint32_t lane = lane_id();
-    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, wb.n_starts};
-    const uint64_t n = wb.n_starts;
+    const uint64_t n = wb.n_starts + walk_splits(wb);  // walkers: contig starts, then splitter segments
+    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
     // wave-uniform batch window: contigs [bbase, bbase + WALK_GRAB), bused of them handed out
     uint64_t bbase = 0;
     uint32_t bused = WALK_GRAB;
@@ -260,8 +268,10 @@ __global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __res
                         if (bbase >= n) bdry = true;
                         const uint64_t mi = bbase + lane;
                         if (mi < n) {
-                            bw0 = wb.starts[mi * W];
-                            bw1 = (W == 2) ? wb.starts[mi * W + 1] : 0;
+                            const uint64_t* src = mi < wb.n_starts ? wb.starts + mi * W
+                                                                   : wb.splits + (mi - wb.n_starts) * W;
+                            bw0 = src[0];
+                            bw1 = (W == 2) ? src[1] : 0;
                         }
                         const uint32_t src_new = min(rank - min(rank, avail), (uint32_t)WALK_GRAB - 1);
                         n0 = __shfl(bw0, (int)src_new, 64);
@@ -309,8 +319,17 @@ __global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __res
         if (active && resolved) {
             append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
             k = key_next(k, fwd, p);
-            s = home_slot(key_hash(k), cap);
-            resolved = false;
+            const uint64_t h = key_hash(k);
+            if (is_splitter(h, p)) {  // the next k-mer heads a segment of its own walker
+                finish_contig(o, c, steps, chunk, buf);
+                wb.seg_next[c] = SEG_AT_SPLIT;
+                wb.seg_key[2 * c] = k.hi;
+                wb.seg_key[2 * c + 1] = k.lo;
+                active = false;
+            } else {
+                s = home_slot(h, cap);
+                resolved = false;
+            }
         }
         // -- one table load per active lane ---------------------------------------------------
         if (active) {
@@ -339,8 +358,9 @@ __global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __res
 
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s) {
-    if (wb.n_starts == 0) return hipSuccess;
-    uint64_t want = (wb.n_starts + BLOCK - 1) / BLOCK;
+    const uint64_t nw = wb.n_starts + wb.n_splits;
+    if (nw == 0) return hipSuccess;
+    uint64_t want = (nw + BLOCK - 1) / BLOCK;
     unsigned grid = (unsigned)hmin(want, (uint64_t)(grid_blocks > 0 ? grid_blocks : 2048));
     if (p.W == 1)
         k_walk<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
@@ -493,6 +513,163 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
         (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr,
                                         wb.chunk_cap, nc, wb.contig_len, offsets, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Splitter segments (sparse ruling set). With p.split_bits > 0 every k-mer whose hash has
+// split_bits low zero bits (and that is not a contig start) heads a segment walked by its own
+// lane, and walkers stop before such a k-mer. A contig of L k-mers then costs ~L / 2^split_bits
+// dependent steps on its critical path instead of L (C5 chains of 10^6 k-mers;
+// C2 chains of ~800 walked by only ~13 K lanes). Afterwards each segment's successor is looked
+// up in a small splitter table and each contig's chain of segments is followed once.
+__global__ __launch_bounds__(BLOCK) void k_stab_build(KParams p, WalkBuffers wb, uint64_t* stab, uint32_t* id,
+                                                      uint64_t cap2) {
+    const uint64_t* splits = wb.splits;
+    const uint64_t nsp = walk_splits(wb);
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nsp; i += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t w0 = splits[i * p.W], w1 = p.W == 2 ? splits[i * p.W + 1] : 0;
+        const Key k = slot_key(w0, w1, p);
+        uint64_t s = mulhi64(fmix64(key_hash(k)), cap2);
+        while (true) {  // lo < 2^62 is never EMPTY; keys are unique (table invariant)
+            const unsigned long long old =
+                atomicCAS((unsigned long long*)&stab[2 * s], (unsigned long long)EMPTY, (unsigned long long)k.lo);
+            if (old == EMPTY) {
+                stab[2 * s + 1] = k.hi;
+                id[s] = (uint32_t)i;
+                break;
+            }
+            s = (s + 1 == cap2) ? 0 : s + 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, const uint64_t* stab, const uint32_t* id,
+                                                    uint64_t cap2, unsigned long long* stats) {
+    const uint64_t nseg = wb.n_starts + walk_splits(wb);
+    for (uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; g < nseg; g += (uint64_t)gridDim.x * BLOCK) {
+        if (wb.seg_next[g] != SEG_AT_SPLIT) continue;
+        const Key k{wb.seg_key[2 * g], wb.seg_key[2 * g + 1]};
+        uint64_t s = mulhi64(fmix64(key_hash(k)), cap2);
+        uint32_t nx = SEG_NONE;
+        for (uint64_t pr = 0; pr < cap2; ++pr) {
+            const uint64_t lo = stab[2 * s];
+            if (lo == EMPTY) break;
+            if (lo == k.lo && stab[2 * s + 1] == k.hi) {
+                nx = (uint32_t)(wb.n_starts + id[s]);
+                break;
+            }
+            s = (s + 1 == cap2) ? 0 : s + 1;
+        }
+        if (nx == SEG_NONE) atomicAdd(&stats[ST_MISSING], 1ull);  // the splitter k-mer is absent
+        wb.seg_next[g] = nx;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
+    const uint64_t nseg = wb.n_starts + walk_splits(wb);
+    for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < wb.n_starts; c += (uint64_t)gridDim.x * BLOCK) {
+        uint32_t g = (uint32_t)c;
+        uint64_t off = 0, hops = 0;
+        while (true) {
+            sb.seg_contig[g] = (uint32_t)c;
+            sb.seg_off[g] = (uint32_t)off;
+            off += wb.contig_len[g] - 1;
+            g = wb.seg_next[g];
+            if (g == SEG_NONE) break;
+            if (++hops > nseg || off > wb.max_steps) {  // segments in a cycle
+                atomicAdd(&stats[ST_CYCLE], 1ull);
+                break;
+            }
+        }
+        sb.clen[c] = (uint32_t)(off + 1);
+    }
+}
+
+struct SplitKeepF {
+    KParams p;
+    const uint64_t* splits;
+    uint64_t mask;
+    __device__ uint64_t operator()(uint64_t i) const {
+        const uint64_t w0 = splits[i * p.W], w1 = p.W == 2 ? splits[i * p.W + 1] : 0;
+        return (key_hash(slot_key(w0, w1, p)) & mask) == 0;
+    }
+};
+
+__global__ __launch_bounds__(BLOCK) void k_filter_splits(SplitKeepF f, uint64_t n, const uint64_t* off, uint64_t* out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+        if (!f(i)) continue;
+        for (int w = 0; w < f.p.W; ++w) out[off[i] * f.p.W + w] = f.splits[i * f.p.W + w];
+    }
+}
+
+hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64_t n, int bits, uint64_t* off,
+                                uint64_t* scratch, uint64_t* out, unsigned long long* count, hipStream_t s) {
+    if (n == 0) return hipMemsetAsync(count, 0, 8, s);
+    const SplitKeepF f{p, splits, (1ull << bits) - 1};
+    hipError_t e = scan_exclusive(f, n, off, scratch, (unsigned long long*)nullptr, count, s);
+    if (e != hipSuccess) return e;
+    k_filter_splits<<<(unsigned)hmin((n + BLOCK - 1) / BLOCK, 8192), BLOCK, 0, s>>>(f, n, off, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
+                           unsigned long long* stats, hipStream_t s) {
+    const uint64_t nseg = wb.n_starts + wb.n_splits;
+    if (nseg == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(sb.stab, 0xff, sb.cap2 * 16, s);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(sb.seg_contig, 0xff, nseg * 4, s)) != hipSuccess) return e;
+    if (wb.n_splits)
+        k_stab_build<<<(unsigned)hmin((wb.n_splits + BLOCK - 1) / BLOCK, 4096), BLOCK, 0, s>>>(
+            p, wb, sb.stab, sb.stab_id, sb.cap2);
+    k_seg_link<<<(unsigned)hmin((nseg + BLOCK - 1) / BLOCK, 8192), BLOCK, 0, s>>>(wb, sb.stab, sb.stab_id, sb.cap2,
+                                                                                   stats);
+    if (wb.n_starts)
+        k_seg_chain<<<(unsigned)hmin((wb.n_starts + BLOCK - 1) / BLOCK, 8192), BLOCK, 0, s>>>(wb, sb, stats);
+    return hipGetLastError();
+}
+
+// Chunk words of segment g go to contig seg_contig[g] at base offset seg_off[g].
+__global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_t* chunk_data, const uint32_t* owner,
+                                                            const uint32_t* seq, const unsigned long long* ctr,
+                                                            uint64_t chunk_cap, uint64_t n_starts,
+                                                            const unsigned long long* nsp_dev, uint64_t nsp,
+                                                            const uint32_t* seg_len, const uint32_t* seg_contig,
+                                                            const uint32_t* seg_off, const uint64_t* off,
+                                                            char* out) {
+    const uint64_t nseg = n_starts + (nsp_dev ? (uint64_t)*nsp_dev : nsp);
+    const uint64_t nchunks = min(nseg + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
+    const uint64_t nwords = nchunks * CHUNK_WORDS;
+    for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nwords; t += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t ch = t / CHUNK_WORDS;
+        const uint32_t w = (uint32_t)(t % CHUNK_WORDS);
+        const uint32_t g = ch < nseg ? (uint32_t)ch : owner[ch];
+        const uint32_t c = seg_contig[g];
+        if (c == SEG_NONE) continue;  // a segment no contig reached
+        const uint64_t j0 = (ch < nseg ? 0ull : (uint64_t)seq[ch] * CHUNK_BASES) + (uint64_t)w * 32;
+        const uint64_t app = (uint64_t)seg_len[g] - 1;
+        if (j0 >= app) continue;
+        const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
+        const uint64_t word = chunk_data[t];
+        char* o = out + off[c] + K + seg_off[g] + j0;
+        for (uint32_t i = 0; i < cntb; ++i) o[i] = (char)code_char((uint32_t)(word >> (2 * i)) & 3u);
+    }
+}
+
+hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
+                                  uint64_t* offsets, uint64_t* scratch, char* out, unsigned long long* ctr,
+                                  hipStream_t s) {
+    const uint64_t nc = wb.n_starts;
+    if (nc == 0) return hipSuccess;
+    hipError_t e = scan_exclusive(ContigBytesF{sb.clen, (uint64_t)p.K}, nc, offsets, scratch,
+                                  (unsigned long long*)nullptr, &ctr[CT_OUT_BYTES], s);
+    if (e != hipSuccess) return e;
+    if ((e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s)) != hipSuccess) return e;
+    const unsigned gc = (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
+    k_write_chunks_seg<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr, wb.chunk_cap,
+                                            nc, wb.n_splits_dev, wb.n_splits, wb.contig_len, sb.seg_contig,
+                                            sb.seg_off, offsets, out);
     return hipGetLastError();
 }
 

@@ -28,6 +28,8 @@ enum CtrIdx : int {
     CT_OUT_BYTES = 3,  // total contig bytes (incl. '\n')
     CT_OVF = 4,        // partitioned build: keys whose probe run left their region
     CT_MW_FIN = 5,     // migrating walk: finish records received by the origin
+    CT_N_SPLIT = 6,    // splitter k-mers collected (walk segments beyond the contig starts)
+    CT_N_SPLIT_W = 7,  // splitters of the walk subset (denser collection filtered at assemble)
     CT_NUM = 8
 };
 
@@ -43,14 +45,14 @@ struct TableView {
 // Insert records (reference kmer_pair layout, R bytes each, 16-B aligned base) into the table.
 // Writes one start bit per record (bwd == 'F') into start_mask[i/64].
 hipError_t launch_insert(const KParams& p, const uint8_t* recs, uint64_t n, TableView t,
-                         uint64_t* start_mask, unsigned long long* stats, hipStream_t s);
+                         uint64_t* start_mask, uint64_t* split_mask, unsigned long long* stats, hipStream_t s);
 
 // Append start k-mers of a batch, in record order, to starts (W words each) at
 // ctr[CT_N_STARTS]. scratch must hold >= scan_scratch_words(ceil(n/64)) words.
 hipError_t launch_collect_starts(const KParams& p, const uint8_t* recs, uint64_t n,
                                  const uint64_t* start_mask, uint64_t* mask_offsets,
                                  uint64_t* scratch, uint64_t* starts, unsigned long long* ctr,
-                                 hipStream_t s);
+                                 hipStream_t s, int ctr_idx = CT_N_STARTS);
 
 // Explicit start list (caller's start_nodes): R-byte records -> start words, sets CT_N_STARTS.
 hipError_t launch_load_starts(const KParams& p, const uint8_t* recs, uint64_t n, uint64_t* starts,
@@ -63,7 +65,14 @@ hipError_t launch_find(const KParams& p, const uint8_t* keys, uint64_t n, TableV
 struct WalkBuffers {
     const uint64_t* starts;
     uint64_t n_starts;
-    uint32_t* contig_len;     // k-mers per contig (>= 1)
+    // splitter walkers (segments n_starts .. n_starts + n_splits - 1); contig_len/chunks are then
+    // per segment and seg_next/seg_key record where a segment stopped (see k_walk)
+    const uint64_t* splits;
+    uint64_t n_splits;                         // host bound (sizes, grids)
+    const unsigned long long* n_splits_dev;    // exact count on the device when set
+    uint32_t* seg_next;       // next segment, SEG_NONE, or SEG_AT_SPLIT (resolved by k_seg_link)
+    uint64_t* seg_key;        // 2 words per segment: the splitter k-mer it stopped before
+    uint32_t* contig_len;     // k-mers per contig (>= 1); per segment when n_splits > 0
     uint64_t* chunk_data;     // chunk_cap * CHUNK_WORDS
     uint32_t* chunk_owner;    // contig id of each chunk
     uint32_t* chunk_seq;      // chunk index within its contig
@@ -75,6 +84,28 @@ struct WalkBuffers {
 // from a wave-batched work queue.
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s);
+
+static constexpr uint32_t SEG_NONE = 0xFFFFFFFFu, SEG_AT_SPLIT = 0xFFFFFFFEu;
+
+// Splitter segments -> contigs: a small open-addressing table of the splitter k-mers (key -> id),
+// segment links, then per contig the chain of its segments (contig_len = final k-mers per contig,
+// seg_contig/seg_off = where each segment's bases go).
+struct SegBuffers {
+    uint64_t* stab;        // cap2 * 2 words (key lo, key hi)
+    uint32_t* stab_id;     // cap2
+    uint64_t cap2;
+    uint32_t* seg_contig;  // nseg
+    uint32_t* seg_off;     // nseg: bases of the contig before this segment
+    uint32_t* clen;        // n_starts: final contig k-mers
+};
+// splits with (hash & (2^bits - 1)) == 0 -> out (count to *count)
+hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64_t n, int bits, uint64_t* off,
+                                uint64_t* scratch, uint64_t* out, unsigned long long* count, hipStream_t s);
+hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
+                           unsigned long long* stats, hipStream_t s);
+hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
+                                  uint64_t* offsets, uint64_t* scratch, char* out, unsigned long long* ctr,
+                                  hipStream_t s);
 
 // Contig bytes: offsets = exclusive scan of (K + len) (K + len-1 bases + '\n'), then write chars.
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
@@ -244,7 +275,7 @@ struct PartBuffers {
 // internal words (words, W each). table_empty: skip loading the current region contents.
 hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words,
                               uint64_t n, TableView t, bool table_empty, const PartBuffers& b,
-                              uint64_t* start_mask, unsigned long long* ctr,
+                              uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
                               unsigned long long* stats, hipStream_t s);
 
 }  // namespace kh

@@ -280,3 +280,33 @@ def test_gpu_pack_text_large_and_bad_base(k):
     t.pack_text_dev(d.data_ptr(), d.numel(), out.data_ptr())
     with pytest.raises(kh.KmerHashError):
         t.sync()
+
+
+# ---- long chains: splitter segments (SURVEY §8(d) C5 / §8(e) long-tail strategy) --------------
+@pytest.mark.parametrize("k,n,lmin,lmax,bits", [
+    (51, 3_000_000, 200_000, 1_000_000, None),   # C5-like: a handful of very long chains
+    (51, 3_000_000, 200_000, 1_000_000, "4"),    # dense splitters: many segments per contig
+    (19, 2_000_000, 200, 1374, None),            # C2-like chain lengths
+    (29, 1_000_000, 1, 3000, "3"),               # W=1 keys, single-k-mer contigs, dense splitters
+    (60, 1_000_000, 1, 400, None),
+])
+def test_gpu_splitter_segments_vs_truth(monkeypatch, k, n, lmin, lmax, bits):
+    if bits is not None:
+        monkeypatch.setenv("KH_SPLIT_BITS", bits)
+    g = kh.SyntheticKmers(k, n, lmin, lmax, 5, seed=k * 7 + lmin)
+    with kh.KmerHashTable(k, n) as t:
+        t.insert_all(g.records())
+        t.assemble()
+        assert t.contigs_text() == g.truth()
+
+
+def test_gpu_splitters_off_equals_on(monkeypatch):
+    g = kh.SyntheticKmers(51, 1_000_000, 50, 5000, 0, seed=99)
+    texts = []
+    for bits in ("0", "6"):
+        monkeypatch.setenv("KH_SPLIT_BITS", bits)
+        with kh.KmerHashTable(51, 1_000_000) as t:
+            t.insert_all(g.records())
+            t.assemble()
+            texts.append(t.contigs_text())
+    assert texts[0] == texts[1] == g.truth()
