@@ -154,7 +154,7 @@ __device__ __forceinline__ uint32_t scan_bins(const uint32_t* hist, uint32_t* st
         if (i < NB) start[i] = (uint32_t)pre;
         pre += v[q];
     }
-    __syncthreads();
+    lds_barrier();
     return (uint32_t)tot;
 }
 
@@ -166,11 +166,11 @@ __device__ __forceinline__ void sorted_write(const uint64_t (&a)[PITEMS], const 
                                              uint16_t* sbin, uint32_t* hist, uint32_t* start,
                                              const uint64_t* gbase, uint64_t* out) {
     for (int i = threadIdx.x; i < NB; i += PB) hist[i] = 0;
-    __syncthreads();
+    lds_barrier();
     uint32_t rank[PITEMS];
 #pragma unroll
     for (int j = 0; j < PITEMS; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
-    __syncthreads();
+    lds_barrier();
     const uint32_t total = scan_bins<NB>(hist, start);
 #pragma unroll
     for (int j = 0; j < PITEMS; ++j) {
@@ -181,7 +181,7 @@ __device__ __forceinline__ void sorted_write(const uint64_t (&a)[PITEMS], const 
             sbin[pos] = (uint16_t)bin[j];
         }
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t t = threadIdx.x; t < total; t += PB) {
         const uint32_t q = sbin[t];
         const uint64_t g = gbase[q] + (t - start[q]);
@@ -191,7 +191,7 @@ __device__ __forceinline__ void sorted_write(const uint64_t (&a)[PITEMS], const 
             out[g] = items[t];
         }
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // ---- pass 1: bin = top 9 hash bits --------------------------------------------------------------

@@ -23,6 +23,11 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
 
 // ---------------------------------------------------------------------------------------------
 // Block-wide exclusive scan of one uint64 per thread (256 threads = 4 waves of 64).
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads/stores (HIP's __syncthreads also drains vmcnt, which serialises a tile's stores
+// with the next tile's loads and kills any prefetch).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total) {
     __shared__ uint64_t wsum[BLOCK / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -33,14 +38,14 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total)
         if (lane >= o) x += y;
     }
     if (lane == 63) wsum[w] = x;
-    __syncthreads();
+    lds_barrier();
     uint64_t pre = 0, tot = 0;
 #pragma unroll
     for (int i = 0; i < BLOCK / 64; ++i) {
         if (i < w) pre += wsum[i];
         tot += wsum[i];
     }
-    __syncthreads();
+    lds_barrier();
     total = tot;
     return pre + x - v;
 }
