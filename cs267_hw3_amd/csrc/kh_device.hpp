@@ -243,6 +243,35 @@ __device__ __forceinline__ bool probe(Key k, const KParams& p, const uint64_t* _
 }
 
 // ---------------------------------------------------------------------------------------------
+// Characters are produced 4 at a time (little-endian u32) and stored as aligned dwords: the
+// leading/trailing bytes of a run that does not start/end on a dword boundary are byte stores,
+// the inside is funnel-shifted (alignbyte) whole dwords. Byte-per-char stores made the two
+// materialisation kernels ~1 ms at C3 (296 MB of text).
+__device__ __forceinline__ uint32_t codes4_chars(uint32_t c8) {  // 4 2-bit codes, code 0 in bits 0-1
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) r |= ((0x54474341u >> (8 * ((c8 >> (2 * b)) & 3u))) & 0xFFu) << (8 * b);
+    return r;
+}
+
+template <class Gen>
+__device__ __forceinline__ void store_chars(char* dst, uint32_t n, Gen gen) {
+    const uint32_t a = (4u - (uint32_t)((uintptr_t)dst & 3u)) & 3u;
+    uint32_t cur = gen(0);
+    const uint32_t lead = a < n ? a : n;
+    for (uint32_t b = 0; b < lead; ++b) dst[b] = (char)(cur >> (8 * b));
+    if (n <= a) return;
+    uint32_t i = 0;
+    for (; a + 4 * i + 4 <= n; ++i) {
+        const uint32_t nxt = gen(i + 1);
+        const uint32_t v = a ? __builtin_amdgcn_alignbyte(nxt, cur, a) : cur;
+        *reinterpret_cast<uint32_t*>(dst + a + 4 * i) = v;
+        cur = nxt;
+    }
+    for (uint32_t x = a + 4 * i; x < n; ++x) dst[x] = (char)(gen(x >> 2) >> (8 * (x & 3)));
+}
+
+// ---------------------------------------------------------------------------------------------
 // Owner-major view of a [blocks][ranks] histogram for the exclusive scan.
 struct HistF {
     const uint64_t* hist;

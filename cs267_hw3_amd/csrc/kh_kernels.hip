@@ -382,7 +382,16 @@ __global__ __launch_bounds__(BLOCK) void k_write_heads(KParams p, const uint64_t
         const uint64_t w1 = (W == 2) ? starts[c * W + 1] : 0;
         const Key k = slot_key(w0, w1, p);
         char* o = out + off[c];
-        for (int i = 0; i < p.K; ++i) o[i] = (char)code_char(key_base(k, i, p));
+        // base j of the k-mer sits at bit 2(K-1-j) of V = hi:lo
+        store_chars(o, (uint32_t)p.K, [&](uint32_t i) {
+            uint32_t c8 = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * (int)i + b;
+                c8 |= (j < p.K ? key_base(k, j, p) : 0u) << (2 * b);
+            }
+            return codes4_chars(c8);
+        });
         o[p.K + len[c] - 1] = '\n';
     }
 }
@@ -409,7 +418,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* c
         const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
         const uint64_t word = chunk_data[t];
         char* o = out + off[c] + K + j0;
-        for (uint32_t i = 0; i < cntb; ++i) o[i] = (char)code_char((uint32_t)(word >> (2 * i)) & 3u);
+        store_chars(o, cntb, [&](uint32_t i) { return codes4_chars((uint32_t)(word >> (8 * i)) & 0xFFu); });
     }
 }
 
@@ -653,7 +662,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
         const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
         const uint64_t word = chunk_data[t];
         char* o = out + off[c] + K + seg_off[g] + j0;
-        for (uint32_t i = 0; i < cntb; ++i) o[i] = (char)code_char((uint32_t)(word >> (2 * i)) & 3u);
+        store_chars(o, cntb, [&](uint32_t i) { return codes4_chars((uint32_t)(word >> (8 * i)) & 0xFFu); });
     }
 }
 

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_words(int K, const uint64_t* recs,
         const uint32_t cnt = (uint32_t)(app - j0 < 32 ? app - j0 : 32);
         const uint64_t word = recs[2 * i + 1];
         char* o = out + off[c] + K + j0;
-        for (uint32_t b = 0; b < cnt; ++b) o[b] = (char)code_char((uint32_t)(word >> (2 * b)) & 3u);
+        store_chars(o, cnt, [&](uint32_t x) { return codes4_chars((uint32_t)(word >> (8 * x)) & 0xFFu); });
     }
 }
 
