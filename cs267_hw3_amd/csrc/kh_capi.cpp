@@ -245,6 +245,7 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     t->device = device;
     t->kp = kh::make_params(k);
     t->n_kmers = n_kmers;
+    if (const char* e = getenv("KH_OWNER")) t->kp.owner_mode = strcmp(e, "hash") == 0 ? 1 : 0;
     // splitter density: ~1 per 2^bits k-mers; enough extra walkers for long-chain inputs (C2, C5)
     // at a few % more walkers on short-contig inputs. KH_SPLIT_BITS overrides (0 = off).
     // Collected at insert: 1 per 2^bits k-mers, bits = clamp(log2(n / 2^20) + 1, 4, 12); the walk

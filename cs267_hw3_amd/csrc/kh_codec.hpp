@@ -48,6 +48,7 @@ struct KParams {
     uint64_t hi_mask;   // mask for hi after a shift (2K-62 bits, 0 when K <= 31)
     uint64_t v_mask;    // W=1: mask of V (2K bits)
     int M;              // minimizer length (bases) of the sharded owner function
+    int owner_mode;     // sharded owner: 0 = minimizer hash (default), 1 = low key_hash bits
     int split_bits;     // walk splitters: k-mers with (key_hash & (2^split_bits - 1)) == 0 and a
                         // predecessor start extra walkers (0 = off); see kh_kernels.hip k_walk
 };
@@ -69,6 +70,7 @@ inline KParams make_params(int K) {
     p.v_mask = (2 * K >= 64) ? ~0ull : ((1ull << (2 * K)) - 1);
     p.M = minimizer_len(K);
     p.split_bits = 0;
+    p.owner_mode = 0;
     return p;
 }
 
@@ -177,6 +179,8 @@ KH_HD uint32_t mix32(uint32_t x) {
 // runs of consecutive k-mers on one rank so a walker migrates only at minimizer changes.
 KH_HD uint32_t owner_key(Key k, const KParams& p, uint32_t nranks) {
     if (nranks == 1) return 0;
+    if (p.owner_mode == 1)  // SURVEY §8(e) proposal: hash bits independent of the home slot's
+        return (uint32_t)(((key_hash(k) & 0xffffffffull) * nranks) >> 32);
     const uint32_t mask = (uint32_t)((1ull << (2 * p.M)) - 1);
     uint64_t lo = k.lo, hi = k.hi;  // V = hi * 2^62 + lo; windows from the last M bases upward
     uint32_t best = 0xffffffffu;

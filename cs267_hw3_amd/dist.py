@@ -18,6 +18,7 @@ The SPMD driver below is written against two small interfaces so that the same c
   * on CPUs: a test double shard + TorchComm over gloo (tests/test_dist_cpu.py).
 """
 import ctypes
+import os
 import threading
 
 import torch  # before the C ABI library is loaded: one HIP runtime for both
@@ -291,7 +292,9 @@ class DistributedKmerHashMap:
     # RCCL as shipped with this torch build corrupts all_to_all_single messages of >= 2 GiB per
     # peer (tools/dbg_a2a.py: half the elements wrong at 2.0 and 3.2 GiB, exact at 1 GiB), so no
     # single call moves more than A2A_CHUNK_BYTES per peer.
-    A2A_CHUNK_BYTES = 512 << 20
+    A2A_CHUNK_BYTES = int(os.environ.get("KH_A2A_CHUNK_MB", "512")) << 20
+    # one rank: exchanges are skipped (KH_DIST_SELF_EXCHANGE=1 runs them anyway, for tests)
+    SELF_EXCHANGE = os.environ.get("KH_DIST_SELF_EXCHANGE") == "1"
 
     def _exchange_counts(self, counts, elems_per_item=1):
         """counts: [P+1] int64 (per-destination, total) -> (send_splits, recv_splits, totals,
@@ -355,7 +358,7 @@ class DistributedKmerHashMap:
         send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
         W = sh.W
         m = sum(recv_splits)
-        if P == 1:
+        if P == 1 and not self.SELF_EXCHANGE:
             recv = words                       # one rank: nothing to exchange
         else:
             recv = self._int64(words, m * W)
@@ -462,7 +465,7 @@ class DistributedKmerHashMap:
             if sum(totals) == 0:
                 break
             m = sum(recv_splits)
-            if P == 1:
+            if P == 1 and not self.SELF_EXCHANGE:
                 nxt = out      # the round kernel reads its input before the grouping rewrites it
             else:
                 nxt = self._grow("_mw_in", max(m, 1) * M, torch.int64, out.device)
@@ -475,7 +478,7 @@ class DistributedKmerHashMap:
         counts = sh.mw_text(tout)
         send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
         r = sum(recv_splits)
-        if P == 1:
+        if P == 1 and not self.SELF_EXCHANGE:
             trecv = tout
         else:
             trecv = sh.zeros(max(r, 1) * T, torch.int64)

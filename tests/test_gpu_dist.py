@@ -92,3 +92,12 @@ def test_sharded_long_contigs_migrate():
     g = kh.SyntheticKmers(19, 2_000_000, 200, 1374, 0, seed=11)
     for P in (1, 3):
         check_ranks(g, run_threaded(19, g.records(), P), P)
+
+
+@pytest.mark.parametrize("protocol", ["migrate", "fixed", "variable"])
+def test_sharded_hash_owner(monkeypatch, protocol):
+    """SURVEY §8(e)'s owner (hash bits) instead of the minimizer owner: same outputs."""
+    from cs267_hw3_amd.dist import run_threaded
+    monkeypatch.setenv("KH_OWNER", "hash")
+    g = kh.SyntheticKmers(51, 500_000, 8, 200, 10, seed=123)
+    check_ranks(g, run_threaded(51, g.records(), 4, protocol=protocol), 4)
