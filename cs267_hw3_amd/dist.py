@@ -32,13 +32,25 @@ from ._lib import check
 class TorchComm:
     """torch.distributed process group (nccl = RCCL over xGMI on MI355X, or gloo on CPU)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, ctrl=None):
+        """ctrl: optional gloo group for small host-side exchanges that must not queue behind
+        large RCCL transfers (the pipelined insert's per-chunk counts)."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
+        self.ctrl = ctrl
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+
+    def all_gather_host(self, t):
+        """CPU int64 tensor [m] from every rank -> [world, m] over the ctrl (gloo) group."""
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.ctrl)
+        return torch.stack(out)
+
+    def all_to_all_async(self, out, inp, out_splits, in_splits):
+        return self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=True)
 
     def all_to_all(self, out, inp, out_splits, in_splits):
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
@@ -78,6 +90,22 @@ class ThreadComm:
         self.sh = shared
         self.rank = rank
         self.world = shared.world
+        self.ctrl = None  # set to enable the pipelined insert (tests)
+
+    class _Done:
+        def wait(self):
+            pass
+
+    def all_gather_host(self, t):
+        self.sh.slots[self.rank] = t.clone()
+        self.sh.barrier.wait()
+        out = torch.stack([self.sh.slots[q] for q in range(self.world)])
+        self.sh.barrier.wait()
+        return out
+
+    def all_to_all_async(self, out, inp, out_splits, in_splits):
+        self.all_to_all(out, inp, out_splits, in_splits)
+        return ThreadComm._Done()
 
     def _sync(self, t):
         if t.is_cuda:
@@ -123,6 +151,7 @@ class GpuShard:
         self.L = _lib.lib()
         self.W = self.L.kh_word_count(k)
         self.h = self.table._h
+        self.n_kmers = n_kmers
         self.stream = torch.cuda.Stream(device=self.dev)
         self.table.set_stream(self.stream.cuda_stream)
 
@@ -139,9 +168,10 @@ class GpuShard:
     def collect_starts(self, recs):
         check(self.L.kh_collect_starts_dev(self.h, self._p(recs), recs.shape[0]))
 
-    def route(self, recs, nranks):
+    def route(self, recs, nranks, words=None):
         n = recs.shape[0]
-        words = self.zeros(n * self.W, torch.int64)
+        if words is None:
+            words = self.zeros(n * self.W, torch.int64)
         counts = self.zeros(nranks + 1, torch.int64)
         check(self.L.kh_route_dev(self.h, self._p(recs), n, nranks, self._p(words), self._p(counts)))
         return words, counts
@@ -351,9 +381,48 @@ class DistributedKmerHashMap:
                     out[out_off[q] + lo:out_off[q] + lo + rc[q]].copy_(recv[pos:pos + rc[q]])
                     pos += rc[q]
 
+    # pipelined insert: route chunk c+1 while chunk c is on the wire (KH_INSERT_CHUNKS=1: off)
+    INSERT_CHUNKS = int(os.environ.get("KH_INSERT_CHUNKS", "4"))
+    PIPELINE_MIN = 1 << 22  # records per rank below which the insert is one chunk
+
+    def _insert_pipelined(self, recs):
+        """Route and exchange the records in chunks: the route kernels of chunk c+1 run while
+        RCCL moves chunk c (counts go over the gloo ctrl group so they do not queue behind
+        the transfers). Words land back to back in one receive buffer sized by the shard."""
+        sh, P, W = self.shard, self.P, self.shard.W
+        n = recs.shape[0]
+        nch = self.INSERT_CHUNKS
+        bounds = [n * c // nch for c in range(nch + 1)]
+        words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
+        recv = self._grow("_ins_recv", max(sh.n_kmers, 1) * W, torch.int64, recs.device)
+        rank = self.comm.rank
+        works, pos = [], 0
+        for c in range(nch):
+            c0, c1 = bounds[c], bounds[c + 1]
+            w = words[c0 * W:max(c1, c0 + 1) * W]
+            _, counts = sh.route(recs[c0:c1], P, w)
+            send = counts[:P].cpu()                       # waits for this chunk's route only
+            mat = self.comm.all_gather_host(send)         # [src][dst]
+            recv_splits = mat[:, rank].tolist()
+            send_splits = send.tolist()
+            m = sum(recv_splits)
+            if pos + m > sh.n_kmers:
+                raise _lib.KmerHashError(_lib.KH_ERR_FULL, f"shard receives more than its {sh.n_kmers} k-mers")
+            works.append(self.comm.all_to_all_async(recv[pos * W:(pos + m) * W], w[:(c1 - c0) * W],
+                                                    [x * W for x in recv_splits],
+                                                    [x * W for x in send_splits]))
+            pos += m
+        for wk in works:
+            wk.wait()
+        sh.insert_words(recv, pos)
+        return pos
+
     def insert_all(self, recs):
         sh, P = self.shard, self.P
         sh.collect_starts(recs)
+        if (P > 1 and getattr(self.comm, "ctrl", None) is not None and self.INSERT_CHUNKS > 1
+                and recs.shape[0] >= self.PIPELINE_MIN):
+            return self._insert_pipelined(recs)
         words, counts = sh.route(recs, P)
         send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
         W = sh.W
@@ -518,7 +587,8 @@ class DistributedKmerHashMap:
 
 
 # --------------------------------------------------------------------------------------------
-def run_threaded(k, recs_np, nranks, device=0, protocol="migrate", cap_limit=None, info=None):
+def run_threaded(k, recs_np, nranks, device=0, protocol="migrate", cap_limit=None, info=None,
+                 insert_chunks=None):
     """P logical ranks on one GPU (threads): returns the per-rank contig texts. `info` (a dict)
     receives the round count and per-rank table stats."""
     import numpy as np
@@ -538,6 +608,10 @@ def run_threaded(k, recs_np, nranks, device=0, protocol="migrate", cap_limit=Non
                 recs = torch.from_numpy(np.ascontiguousarray(recs_np[b:e])).to(shard.dev)
                 dm = DistributedKmerHashMap(comms[r], shard, protocol=protocol)
                 dm.CAP_LIMIT = cap_limit
+                if insert_chunks:
+                    comms[r].ctrl = comms[r]
+                    dm.INSERT_CHUNKS = insert_chunks
+                    dm.PIPELINE_MIN = 0
                 dm.insert_all(recs)
                 shard.sync()
                 comms[r].barrier()
@@ -575,7 +649,7 @@ def bench_main(args, w, world, rank):
     local = int(os.environ.get("LOCAL_RANK", rank))
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    comm = TorchComm()
+    comm = TorchComm(ctrl=dist.new_group(backend="gloo"))
     k, n_per = w["k"], w["n"]
     n_total = n_per * world  # weak scaling: n k-mers per GPU
     t = time.time()

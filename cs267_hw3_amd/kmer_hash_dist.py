@@ -48,7 +48,8 @@ def main(argv):
         shard.table.sync()  # surfaces a bad base (KH_ERR_BAD_BASE) before the timed region
     recs = buf[:n_local * R].view(n_local, R)
     del text
-    dm = DistributedKmerHashMap(TorchComm(), shard)
+    ctrl = dist.new_group(backend="gloo") if backend == "nccl" else None
+    dm = DistributedKmerHashMap(TorchComm(ctrl=ctrl), shard)
     dist.barrier()
     with torch.cuda.stream(shard.stream):
         t0 = time.perf_counter()

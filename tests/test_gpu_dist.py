@@ -101,3 +101,11 @@ def test_sharded_hash_owner(monkeypatch, protocol):
     monkeypatch.setenv("KH_OWNER", "hash")
     g = kh.SyntheticKmers(51, 500_000, 8, 200, 10, seed=123)
     check_ranks(g, run_threaded(51, g.records(), 4, protocol=protocol), 4)
+
+
+@pytest.mark.parametrize("chunks", [2, 5])
+def test_sharded_pipelined_insert(chunks):
+    """Chunked route + exchange of the insert (counts over the ctrl group), P=4 logical ranks."""
+    from cs267_hw3_amd.dist import run_threaded
+    g = kh.SyntheticKmers(51, 6_000_000, 8, 200, 10, seed=321)
+    check_ranks(g, run_threaded(51, g.records(), 4, insert_chunks=chunks), 4)
