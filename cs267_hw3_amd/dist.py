@@ -711,14 +711,18 @@ def bench_main(args, w, world, rank):
             "scaling": "weak", "vs_baseline": value / 72.6e6, "dtype": "u64", "data": "synthetic",
             "config": {"workload": w["desc"], "k": k, "n_kmers_total": n_total,
                        "n_kmers_per_gpu": n_per, "contigs": nc, "lookups": nl,
-                       "parallelism": f"{world} GPUs, key space sharded by owner hash, "
-                                      f"RCCL all-to-all per walk round ({protocol} segments)",
+                       "parallelism": f"{world} GPUs, key space sharded by "
+                                      f"{'minimizer' if os.environ.get('KH_OWNER') != 'hash' else 'hash'} owner, "
+                                      f"RCCL all-to-all per walk round ({protocol} protocol)",
                        "walk_rounds": dm.rounds, "round_graphs": dm.graph_captures},
             "inserts_per_s": n_total / tmax, "lookups_per_s": nl / tmax,
             "contigs_per_s": nc / tmax, "verified_vs_truth": ok,
-            "roofline": {"bound": "hbm", "kernel": "k_insert_words (rank 0)", "achieved": achieved,
-                         "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0, "traffic": None,
-                         "alg_bytes_per_unit": b_alg, "avg_launch_ms": ins_ms},
+            "roofline": {"bound": "hbm", "kernel": "insert pipeline on the received words (rank 0: "
+                                                     "k_part1_hist .. k_part_build)",
+                         "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
+                         "traffic": None, "alg_bytes_per_unit": b_alg, "avg_launch_ms": ins_ms,
+                         "note": "achieved = inserts x 2*sizeof(kmer_pair) / HIP-event time of the "
+                                 "insert kernels of the last step; traffic: see profiles/pmc_traffic.json"},
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)
