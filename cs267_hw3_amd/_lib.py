@@ -122,6 +122,12 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        # torch ships its own libamdhip64: load it first so the library binds to that same HIP
+        # runtime (two runtimes in one process leave torch with "No HIP GPUs are available")
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)

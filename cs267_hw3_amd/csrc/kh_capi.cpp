@@ -194,7 +194,7 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     const kh::PartPlan pl = kh::part_plan(n);
     const uint64_t W = (uint64_t)t->kp.W, hw = kh::part_hist_words(pl);
     int rc;
-    if ((rc = t->pb_buf1.ensure(n * W * 8)) || (rc = t->pb_buf2.ensure(n * W * 8)) ||
+    if ((rc = t->pb_buf1.ensure(kh::part_buf1_words(t->kp, n) * 8)) || (rc = t->pb_buf2.ensure(kh::part_buf2_words(t->kp, n) * 8)) ||
         (rc = t->pb_hist1.ensure(hw * 8)) || (rc = t->pb_off1.ensure(hw * 8)) ||
         (rc = t->pb_hist2.ensure(hw * 8)) || (rc = t->pb_off2.ensure(hw * 8)) ||
         (rc = t->pb_scratch.ensure(kh::part_scratch_words(pl) * 8)) ||

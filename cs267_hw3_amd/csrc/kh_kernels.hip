@@ -356,16 +356,206 @@ __global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __res
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Cooperative walker: G lanes per contig, each probe fetches the whole G-slot block (64 or 128 B,
+// one memory line) that holds the probe position, G slots compared at once. The walk is bound by
+// the number of random line requests the memory system serves (~51 G/s whether a request is a
+// 16-B slot or a full 128-B line: tools/membench chase16 / chase64q / chase128o), and a per-lane
+// walker spends ~1.5 requests per lookup at load 0.5 (linear-probing displacement), a block
+// probe ~1 + P(the run crosses the block end).
+// Walker state is replicated in the G lanes of a group; the group's lane 0 (the leader) performs
+// every side effect (chunk allocation, base words, contig length, segment records).
+template <int W, int G>
+__global__ __launch_bounds__(BLOCK) void k_walk_g(KParams p, const uint64_t* __restrict__ slots,
+                                                  uint64_t cap, WalkBuffers wb,
+                                                  unsigned long long* ctr,
+                                                  unsigned long long* stats) {
+    static_assert(G >= 2 && G <= 16 && (G & (G - 1)) == 0, "group size");
+    const uint32_t lane = lane_id();
+    const uint32_t q = lane & (G - 1), gl = lane & ~(uint32_t)(G - 1);
+    const bool lead = q == 0;
+    constexpr uint64_t GM = (1ull << G) - 1;
+    uint64_t LM = 0;  // one bit per group leader
+#pragma unroll
+    for (int i = 0; i < 64; i += G) LM |= 1ull << i;
+    const uint64_t n = wb.n_starts + walk_splits(wb);
+    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
+    uint64_t bbase = 0;
+    uint32_t bused = WALK_GRAB;
+    bool bdry = false;
+    uint64_t bw0 = 0, bw1 = 0;
+
+    bool active = false, done = false, resolved = false;
+    uint64_t c = 0, s = 0, buf = 0;
+    Key k{0, 0};
+    uint32_t fwd = 0, steps = 0, chunk = 0;
+    while (true) {
+        while (true) {
+            const bool need = !active && !done;  // uniform within a group
+            const uint64_t m = __ballot(need) & LM;
+            if (m) {
+                const uint32_t cnt = (uint32_t)__popcll(m);
+                const uint32_t rank = (uint32_t)__popcll(m & ((1ull << gl) - 1));
+                const uint32_t avail = WALK_GRAB - bused;
+                const uint32_t src_old = min(bused + rank, (uint32_t)WALK_GRAB - 1);
+                const uint64_t o0 = __shfl(bw0, (int)src_old, 64);
+                const uint64_t o1 = __shfl(bw1, (int)src_old, 64);
+                const uint64_t oc = bbase + src_old;
+                uint64_t n0 = 0, n1 = 0, nc = ~0ull;
+                if (cnt > avail) {
+                    if (!bdry) {
+                        unsigned long long g = 0;
+                        if (lane == 0) g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB);
+                        bbase = __shfl(g, 0, 64);
+                        if (bbase >= n) bdry = true;
+                        const uint64_t mi = bbase + lane;
+                        if (mi < n) {
+                            const uint64_t* src = mi < wb.n_starts ? wb.starts + mi * W
+                                                                   : wb.splits + (mi - wb.n_starts) * W;
+                            bw0 = src[0];
+                            bw1 = (W == 2) ? src[1] : 0;
+                        }
+                        const uint32_t src_new = min(rank - min(rank, avail), (uint32_t)WALK_GRAB - 1);
+                        n0 = __shfl(bw0, (int)src_new, 64);
+                        n1 = __shfl(bw1, (int)src_new, 64);
+                        nc = bbase + src_new;
+                    }
+                    bused = cnt - avail;
+                } else {
+                    bused += cnt;
+                }
+                if (need) {
+                    uint64_t cc, x0, x1;
+                    if (rank < avail) {
+                        cc = oc;
+                        x0 = o0;
+                        x1 = o1;
+                    } else {
+                        cc = nc;
+                        x0 = n0;
+                        x1 = n1;
+                    }
+                    if (cc < n) {
+                        c = cc;
+                        k = slot_key(x0, x1, p);
+                        fwd = ext_fwd(slot_ext(x0));
+                        steps = 0;
+                        buf = 0;
+                        active = true;
+                        resolved = true;
+                    } else {
+                        done = true;
+                    }
+                }
+            }
+            const bool fin = active && resolved && fwd > 3;
+            if (fin) {
+                if (lead) {
+                    if (fwd != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+                    finish_contig(o, c, steps, chunk, buf);
+                }
+                active = false;
+            }
+            if (!__any(fin)) break;
+        }
+        if (!__any(active)) break;
+        if (active && resolved) {
+            if (lead) {
+                append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
+            } else {
+                ++steps;
+            }
+            k = key_next(k, fwd, p);
+            const uint64_t h = key_hash(k);
+            if (is_splitter(h, p)) {
+                if (lead) {
+                    finish_contig(o, c, steps, chunk, buf);
+                    wb.seg_next[c] = SEG_AT_SPLIT;
+                    wb.seg_key[2 * c] = k.hi;
+                    wb.seg_key[2 * c + 1] = k.lo;
+                }
+                active = false;
+            } else {
+                s = home_slot(h, cap);
+                resolved = false;
+            }
+        }
+        // -- one block load per active group: lane q reads slot (s & ~(G-1)) + q ------------------
+        const uint64_t lb = s & ~(uint64_t)(G - 1);
+        const uint64_t my = lb + q;
+        const bool valid = active && my >= s && my < cap;
+        uint64_t w0 = EMPTY, w1 = 0;
+        if (active && my < cap) load_slot<W>(slots, my, w0, w1);
+        const bool empty = w0 == EMPTY;
+        const bool hit = !empty & ((w0 >> 6) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
+        const uint64_t bh = (__ballot(valid && hit) >> gl) & GM;
+        const uint64_t be = (__ballot(valid && empty) >> gl) & GM;
+        const uint32_t fh = bh ? (uint32_t)__builtin_ctzll(bh) : (uint32_t)G;
+        const uint32_t fe = be ? (uint32_t)__builtin_ctzll(be) : (uint32_t)G;
+        const uint64_t hw0 = __shfl(w0, (int)(gl + (fh & (G - 1))), 64);
+        if (active) {
+            if (fh < fe) {
+                fwd = ext_fwd(slot_ext(hw0));
+                resolved = true;
+                if (steps > wb.max_steps) {
+                    if (lead) {
+                        atomicAdd(&stats[ST_CYCLE], 1ull);
+                        finish_contig(o, c, steps, chunk, buf);
+                    }
+                    active = false;
+                }
+            } else if (fe < (uint32_t)G) {
+                if (lead) {
+                    atomicAdd(&stats[ST_MISSING], 1ull);
+                    finish_contig(o, c, steps, chunk, buf);
+                }
+                active = false;
+            } else {
+                s = (lb + G >= cap) ? 0 : lb + G;
+            }
+        }
+    }
+}
+
+// Walker lanes per contig: KH_WALK_G = 1 (per-lane walker) or a block size in slots. Default 4
+// (C3: 5.36-5.9 ms vs 5.47 for per-lane walkers, 7.6 ms at 8: too few walkers resident to
+// cover the latency; C2: 0.68 vs 0.75 ms).
+static int walk_group(const KParams& p) {
+    const char* e = getenv("KH_WALK_G");
+    if (e && *e) return atoi(e);
+    (void)p;
+    return 4;
+}
+
+template <int W, int G>
+static void launch_walk_g(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
+                          unsigned long long* stats, unsigned grid, hipStream_t s) {
+    k_walk_g<W, G><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+}
+
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s) {
     const uint64_t nw = wb.n_starts + wb.n_splits;
     if (nw == 0) return hipSuccess;
-    uint64_t want = (nw + BLOCK - 1) / BLOCK;
+    const int G = walk_group(p);
+    const uint64_t lanes = nw * (uint64_t)(G > 1 ? G : 1);
+    uint64_t want = (lanes + BLOCK - 1) / BLOCK;
     unsigned grid = (unsigned)hmin(want, (uint64_t)(grid_blocks > 0 ? grid_blocks : 2048));
-    if (p.W == 1)
-        k_walk<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
-    else
-        k_walk<2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+    if (p.W == 1) {
+        switch (G) {
+            case 4: launch_walk_g<1, 4>(p, t, wb, ctr, stats, grid, s); break;
+            case 8: launch_walk_g<1, 8>(p, t, wb, ctr, stats, grid, s); break;
+            case 16: launch_walk_g<1, 16>(p, t, wb, ctr, stats, grid, s); break;
+            default: k_walk<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+        }
+    } else {
+        switch (G) {
+            case 2: launch_walk_g<2, 2>(p, t, wb, ctr, stats, grid, s); break;
+            case 4: launch_walk_g<2, 4>(p, t, wb, ctr, stats, grid, s); break;
+            case 8: launch_walk_g<2, 8>(p, t, wb, ctr, stats, grid, s); break;
+            default: k_walk<2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+        }
+    }
     return hipGetLastError();
 }
 

@@ -255,14 +255,18 @@ PartPlan part_plan(uint64_t n);
 uint64_t part_hist_words(const PartPlan& pl);     // words of each hist / offset buffer
 uint64_t part_scratch_words(const PartPlan& pl);  // words of scan scratch (+ one total word)
 uint64_t part_overflow_cap(uint64_t n);           // overflow entries
+uint32_t part_region_cap(uint64_t n);             // words per region window of pass 2
+uint64_t part_buf2_words(const KParams& p, uint64_t n);  // buf2 size (region windows or n * W)
+uint32_t part_win1_cap(uint64_t n);               // words per pass-1 window (k_part1_fused)
+uint64_t part_buf1_words(const KParams& p, uint64_t n);  // buf1 size (pass-1 windows or n * W)
 // True when the region slices fit LDS and the batch is large enough to be worth it.
 bool part_usable(const KParams& p, uint64_t cap, uint64_t n);
 // True when every region slice fits LDS (forced partitioned mode for tests of small batches).
 bool region_slots_fit(const KParams& p, uint64_t cap);
 
 struct PartBuffers {
-    uint64_t* buf1;      // n * W words
-    uint64_t* buf2;      // n * W words
+    uint64_t* buf1;      // part_buf1_words(p, n) words
+    uint64_t* buf2;      // part_buf2_words(p, n) words
     uint64_t* hist1;
     uint64_t* off1;
     uint64_t* hist2;

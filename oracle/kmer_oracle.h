@@ -7,7 +7,7 @@
  * Pinned by: (1) the codec KATs produced by compiling the reference's own packing.hpp /
  * pkmer_t.hpp / kmer_t.hpp / read_kmers.hpp (oracle/ref_harness.cpp -> oracle/_ref/), committed
  * as tests/golden/kat.json; (2) golden contig files produced by that reference-codec harness on
- * committed inputs (tests/golden/*.txt -> *_test_0.dat). See DESIGN.md "Oracle".
+ * committed inputs (the tests/golden txt inputs and their _test_0.dat solutions). See DESIGN.md "Oracle".
  */
 #ifndef KMER_ORACLE_H
 #define KMER_ORACLE_H

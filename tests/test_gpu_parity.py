@@ -310,3 +310,70 @@ def test_gpu_splitters_off_equals_on(monkeypatch):
             t.assemble()
             texts.append(t.contigs_text())
     assert texts[0] == texts[1] == g.truth()
+
+
+# ---- walker shapes: per-lane (G=1) and cooperative block probes (G lanes per contig) ----------
+@pytest.mark.parametrize("G", ["1", "2", "4", "8", "16"])
+@pytest.mark.parametrize("k,n,lmin,lmax,load", [
+    (51, 2_000_000, 8, 200, 0.5),
+    (19, 1_000_000, 1, 2000, 0.9),     # W=1 slots, long runs at high load (block-crossing probes)
+    (31, 500_000, 1, 300, 0.95),
+])
+def test_gpu_walk_group_sizes(monkeypatch, G, k, n, lmin, lmax, load):
+    W = 1 if k <= 29 else 2
+    if (W == 2 and G == "16") or (W == 1 and G == "2"):
+        pytest.skip("block larger than one 128-B line / not dispatched")
+    monkeypatch.setenv("KH_WALK_G", G)
+    g = kh.SyntheticKmers(k, n, lmin, lmax, 5, seed=k + int(G))
+    with kh.KmerHashTable(k, n, load) as t:
+        t.insert_all(g.records())
+        nc, _ = t.assemble()
+        assert nc == g.num_contigs
+        assert t.contigs_text() == g.truth()
+
+
+@pytest.mark.parametrize("G", ["1", "8"])
+def test_gpu_walk_group_missing_kmer(monkeypatch, G):
+    monkeypatch.setenv("KH_WALK_G", G)
+    g = kh.SyntheticKmers(51, 200_000, 20, 40, 0, seed=5)
+    recs = g.records()
+    # drop one k-mer that is not a contig start: its contig's walk misses (kmer_hash.cpp:47-49)
+    fb = recs[:, -2]
+    drop = int(np.nonzero(fb != ord("F"))[0][0])
+    with kh.KmerHashTable(51, len(recs)) as t:
+        t.insert_all(np.delete(recs, drop, axis=0))
+        with pytest.raises(kh.KmerHashError) as e:
+            t.assemble()
+        assert e.value.code == _lib.KH_ERR_NOT_FOUND
+
+
+# ---- partitioned-build pass variants (KH_P1: record re-parse / word copy; KH_P2: region windows
+# with atomic reservations / histogram + scan) ----------------------------------------------------
+@pytest.mark.parametrize("p1,p2", [("fused", "res"), ("rec", "res"), ("convert", "res"), ("rec", "scan"),
+                                   ("convert", "scan")])
+@pytest.mark.parametrize("k,n,batches", [(51, 3_000_000, 1), (60, 2_000_000, 2), (19, 2_000_000, 1),
+                                         (29, 1_500_000, 1)])
+def test_gpu_part_pass_variants(monkeypatch, p1, p2, k, n, batches):
+    monkeypatch.setenv("KH_INSERT", "part")
+    monkeypatch.setenv("KH_P1", p1)
+    monkeypatch.setenv("KH_P2", p2)
+    g = kh.SyntheticKmers(k, n, 8, 300, 10, seed=k * 3 + batches)
+    t, got, nc = run(k, g.records(), batches=batches)
+    assert got == g.truth() and nc == g.num_contigs
+    s = t.stats()
+    assert s["n_dup"] == 0 and s["n_full"] == 0 and s["n_inserted"] == n
+
+
+@pytest.mark.parametrize("p1,p2", [("fused", "res"), ("convert", "res"), ("convert", "scan")])
+def test_gpu_part_pass_variants_duplicates(monkeypatch, p1, p2):
+    monkeypatch.setenv("KH_INSERT", "part")
+    monkeypatch.setenv("KH_P1", p1)
+    monkeypatch.setenv("KH_P2", p2)
+    g = kh.SyntheticKmers(51, 2_000_000, 8, 200, 0, seed=3)
+    recs = g.records()
+    dup = np.concatenate([recs, recs[:1000]])
+    t = kh.KmerHashTable(51, len(dup))
+    with pytest.raises(kh.KmerHashError) as e:
+        t.insert_all(dup)
+    assert e.value.code == _lib.KH_ERR_DUPLICATE
+    assert t.stats()["n_dup"] == 1000

@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                              \
@@ -78,6 +79,25 @@ __global__ void k_store8(uint64_t* t, uint64_t nslots, int iters) {
     }
 }
 
+
+// dependent random loads of a G*16-B aligned block, G lanes per chain (lane q of the group loads
+// bytes 16q..16q+15): the cooperative-probe shape of a walk that fetches a whole bucket per step
+template <int G>
+__global__ void k_chaseg(const uint64_t* t, uint64_t nblocks, int iters, uint64_t* sink) {
+    const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint32_t q = threadIdx.x & (G - 1);
+    uint64_t x = mix(tid / G + 7);
+    for (int i = 0; i < iters; ++i) {
+        const uint64_t s = __umul64hi(mix(x), nblocks);
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(t + 2 * (s * G + q));
+        uint64_t y = v.x ^ v.y;
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) y ^= __shfl_xor(y, o, G);
+        x = y ^ i;
+    }
+    if (x == 42) sink[0] = x;
+}
+
 int main(int argc, char** argv) {
     const double gib[] = {0.25, 1, 2, 4, 6.4, 16};
     const uint64_t maxw = (uint64_t)(16.0 * (1ull << 30) / 8);
@@ -94,12 +114,17 @@ int main(int argc, char** argv) {
         const uint64_t nslots = (uint64_t)(g * (1ull << 30) / 16);
         struct Case { const char* name; int grid; int iters; } cases[] = {
             {"gather16", 16384, 64}, {"chase16", 2048, 256}, {"cas8", 16384, 16},
-            {"cas8w", 16384, 16}, {"store8sc1", 16384, 16}};
+            {"cas8w", 16384, 16}, {"store8sc1", 16384, 16},
+            {"chase32p", 4096, 256}, {"chase64q", 8192, 256}, {"chase128o", 16384, 256},
+            {"chase16w", 8192, 256}};
         for (auto& c : cases) {
             float best = 1e30f;
             for (int rep = 0; rep < 3; ++rep) {
                 CK(hipEventRecord(a));
                 if (c.name[0] == 'g') k_gather16<<<c.grid, threads>>>(t, nslots, c.iters, sink);
+                else if (!strcmp(c.name, "chase32p")) k_chaseg<2><<<c.grid, threads>>>(t, nslots / 2, c.iters, sink);
+                else if (!strcmp(c.name, "chase64q")) k_chaseg<4><<<c.grid, threads>>>(t, nslots / 4, c.iters, sink);
+                else if (!strcmp(c.name, "chase128o")) k_chaseg<8><<<c.grid, threads>>>(t, nslots / 8, c.iters, sink);
                 else if (c.name[1] == 'h') k_chase16<<<c.grid, threads>>>(t, nslots, c.iters, sink);
                 else if (c.name[0] == 'c') k_cas8<<<c.grid, threads>>>(t, nslots, c.iters, c.name[4] == 'w', sink);
                 else k_store8<<<c.grid, threads>>>(t, nslots, c.iters);
@@ -109,7 +134,9 @@ int main(int argc, char** argv) {
                 CK(hipEventElapsedTime(&ms, a, b));
                 if (ms < best) best = ms;
             }
-            const double ops = (double)c.grid * threads * c.iters;
+            int grp = !strcmp(c.name, "chase32p") ? 2 : !strcmp(c.name, "chase64q") ? 4
+                    : !strcmp(c.name, "chase128o") ? 8 : 1;
+            const double ops = (double)c.grid * threads / grp * c.iters;
             printf("{\"case\": \"%s\", \"table_gib\": %.2f, \"lanes\": %d, \"ops\": %.0f, \"ms\": %.3f, "
                    "\"gops\": %.3f}\n", c.name, g, c.grid * threads, ops, best, ops / best / 1e6);
             fflush(stdout);
