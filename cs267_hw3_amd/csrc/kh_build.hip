@@ -183,6 +183,59 @@ __device__ __forceinline__ void load_tile(const KParams& p, const uint8_t* recs,
     }
 }
 
+// Item j of thread t = words[base + j*PB + t] (EMPTY past end): 16-B loads, fully coalesced.
+// Loads are unconditional (index clamped to `last`, a valid index of the buffer) and the value
+// selected afterwards, so all PITEMS loads issue back to back without branches or waits.
+template <int W>
+__device__ __forceinline__ void load_words(const uint64_t* __restrict__ words, uint64_t base, uint64_t end,
+                                           uint64_t last, uint64_t (&a)[PITEMS], uint64_t (&b)[PITEMS]) {
+#pragma unroll
+    for (int j = 0; j < PITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
+        const uint64_t ii = i < end ? i : last;
+        uint64_t x0, x1 = 0;
+        if (W == 2) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(words + 2 * ii);
+            x0 = v.x;
+            x1 = v.y;
+        } else {
+            x0 = words[ii];
+        }
+        a[j] = i < end ? x0 : EMPTY;
+        b[j] = i < end ? x1 : 0;
+    }
+}
+
+// Same from the S1 pass-1 windows of bucket bk (pre = window prefix sums): virtual index v.
+template <int W>
+__device__ __forceinline__ void load_words_win(const uint64_t* __restrict__ buf1, uint32_t bk, uint32_t CAP1,
+                                               const uint32_t (&pre)[S1 + 1], uint64_t base, uint64_t end,
+                                               uint64_t (&a)[PITEMS], uint64_t (&b)[PITEMS]) {
+#pragma unroll
+    for (int j = 0; j < PITEMS; ++j) {
+        const uint32_t v = (uint32_t)(base + (uint64_t)j * PB + threadIdx.x);
+        const bool ok = v < (uint32_t)end;
+        uint32_t w = 0, pw = 0;
+#pragma unroll
+        for (uint32_t q = 1; q < S1; ++q)
+            if (v >= pre[q]) {
+                w = q;
+                pw = pre[q];
+            }
+        const uint64_t i = ok ? (uint64_t)(bk * S1 + w) * CAP1 + (v - pw) : (uint64_t)bk * S1 * CAP1;
+        uint64_t x0, x1 = 0;
+        if (W == 2) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(buf1 + 2 * i);
+            x0 = x.x;
+            x1 = x.y;
+        } else {
+            x0 = buf1[i];
+        }
+        a[j] = ok ? x0 : EMPTY;
+        b[j] = ok ? x1 : 0;
+    }
+}
+
 // Block-wide exclusive scan of NB (<= 512) LDS counters into start[]; returns the total.
 template <int NB>
 __device__ __forceinline__ uint32_t scan_bins(const uint32_t* hist, uint32_t* start) {
@@ -209,6 +262,46 @@ __device__ __forceinline__ uint32_t scan_bins(const uint32_t* hist, uint32_t* st
 
 // Counting-sort the tile's items by bin in LDS, then write them to out at gbase[bin] + rank
 // (gbase in LDS), so consecutive lanes store consecutive addresses of one bin.
+// sorted_write in two halves: sorted_place leaves the tile in LDS (a/b/bin dead afterwards, so a
+// caller can issue the next tile's loads into them), sorted_out writes it and advances nothing.
+template <int W, int NB>
+__device__ __forceinline__ uint32_t sorted_place(const uint64_t (&a)[PITEMS], const uint64_t (&b)[PITEMS],
+                                                 const uint32_t (&bin)[PITEMS], uint64_t* items,
+                                                 uint16_t* sbin, uint32_t* hist, uint32_t* start) {
+    for (int i = threadIdx.x; i < NB; i += PB) hist[i] = 0;
+    lds_barrier();
+    uint32_t rank[PITEMS];
+#pragma unroll
+    for (int j = 0; j < PITEMS; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
+    lds_barrier();
+    const uint32_t total = scan_bins<NB>(hist, start);
+#pragma unroll
+    for (int j = 0; j < PITEMS; ++j) {
+        if (a[j] != EMPTY) {
+            const uint32_t pos = start[bin[j]] + rank[j];
+            items[pos * W] = a[j];
+            if (W == 2) items[pos * W + 1] = b[j];
+            sbin[pos] = (uint16_t)bin[j];
+        }
+    }
+    return total;
+}
+
+template <int W>
+__device__ __forceinline__ void sorted_out(uint32_t total, const uint64_t* items, const uint16_t* sbin,
+                                           const uint32_t* start, const uint64_t* gbase, uint64_t* out) {
+#pragma unroll 4
+    for (uint32_t t = threadIdx.x; t < total; t += PB) {
+        const uint32_t q = sbin[t];
+        const uint64_t g = gbase[q] + (t - start[q]);
+        if (W == 2) {
+            *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(items[2 * t], items[2 * t + 1]);
+        } else {
+            out[g] = items[t];
+        }
+    }
+}
+
 template <int W, int NB>
 __device__ __forceinline__ void sorted_write(const uint64_t (&a)[PITEMS], const uint64_t (&b)[PITEMS],
                                              const uint32_t (&bin)[PITEMS], uint64_t* items,
@@ -471,6 +564,30 @@ __global__ __launch_bounds__(PB) void k_part1_scatter(KParams p, const uint8_t* 
     uint64_t* gbase = reinterpret_cast<uint64_t*>(start + NB1);          // NB1 (8-B aligned)
     for (int i = threadIdx.x; i < NB1; i += PB) gbase[i] = off1[(uint64_t)blockIdx.x * NB1 + i];
     __syncthreads();
+    if (!REC) {
+        // words: the next tile's loads are issued before this tile is sorted and written, and
+        // tiles are separated by LDS-only barriers, so loads, LDS work and stores overlap
+        uint64_t a[PITEMS], b[PITEMS];
+        const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
+        load_words<W>(words, b0, min(b0 + PART_TILE, n), b0 < n ? b0 : 0, a, b);
+        for (int tt = 0; tt < T1; ++tt) {
+            const uint64_t base = b0 + (uint64_t)tt * PART_TILE;
+            if (base >= n) break;  // uniform
+            uint32_t bin[PITEMS];
+#pragma unroll
+            for (int j = 0; j < PITEMS; ++j) bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - B1));
+            const uint32_t total = sorted_place<W, NB1>(a, b, bin, items, sbin, hist, start);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t nbase = base + PART_TILE;
+            load_words<W>(words, nbase, (tt + 1 < T1) ? min(nbase + PART_TILE, n) : nbase, base, a, b);
+            lds_barrier();
+            sorted_out<W>(total, items, sbin, start, gbase, buf1);
+            lds_barrier();
+            for (int i = threadIdx.x; i < NB1; i += PB) gbase[i] += hist[i];
+            lds_barrier();
+        }
+        return;
+    }
     for (int tt = 0; tt < T1; ++tt) {
         const uint64_t base = ((uint64_t)blockIdx.x * T1 + tt) * PART_TILE;
         if (base >= n) break;  // uniform
@@ -589,35 +706,18 @@ __global__ __launch_bounds__(PB) void k_part2_res(KParams p, const uint64_t* buf
     } else {
         bucket_range(off1, 0, n, bk, s, e);
     }
+    uint64_t a[PITEMS], b[PITEMS];
+#define KH_P2_LOAD(t)                                                                              \
+    do {                                                                                           \
+        const uint64_t t_ = (t);                                                                   \
+        const uint64_t e_ = t_ < e ? min(t_ + PART_TILE, e) : t_;                                  \
+        if (WIN)                                                                                   \
+            load_words_win<W>(buf1, bk, CAP1, pre, t_, e_, a, b);                                  \
+        else                                                                                       \
+            load_words<W>(buf1, t_, e_, s, a, b);                                                  \
+    } while (0)
+    KH_P2_LOAD(s + (uint64_t)g * PART_TILE);
     for (uint64_t t = s + (uint64_t)g * PART_TILE; t < e; t += G * PART_TILE) {
-        uint64_t a[PITEMS], b[PITEMS];
-        if (WIN) {
-#pragma unroll
-            for (int j = 0; j < PITEMS; ++j) {
-                const uint32_t v = (uint32_t)(t + (uint64_t)j * PB + threadIdx.x);
-                a[j] = EMPTY;
-                b[j] = 0;
-                if (v < (uint32_t)e) {
-                    uint32_t w = 0, pw = 0;
-#pragma unroll
-                    for (uint32_t q = 1; q < S1; ++q)
-                        if (v >= pre[q]) {
-                            w = q;
-                            pw = pre[q];
-                        }
-                    const uint64_t i = (uint64_t)(bk * S1 + w) * CAP1 + (v - pw);
-                    if (W == 2) {
-                        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(buf1 + 2 * i);
-                        a[j] = x.x;
-                        b[j] = x.y;
-                    } else {
-                        a[j] = buf1[i];
-                    }
-                }
-            }
-        } else {
-            load_tile<W, false, PART_TILE>(p, nullptr, buf1, t, min(t + PART_TILE, e), nullptr, nullptr, a, b);
-        }
         uint32_t bin[PITEMS];
 #pragma unroll
         for (int j = 0; j < PITEMS; ++j)
@@ -631,6 +731,7 @@ __global__ __launch_bounds__(PB) void k_part2_res(KParams p, const uint64_t* buf
         const uint32_t total = scan_bins<NB2>(hist, start);
         for (int i = threadIdx.x; i < NB2; i += PB)
             gpos[i] = hist[i] ? atomicAdd(&rcnt[(bk << B2) | i], hist[i]) : 0u;
+
 #pragma unroll
         for (int j = 0; j < PITEMS; ++j) {
             if (a[j] != EMPTY) {
@@ -640,7 +741,10 @@ __global__ __launch_bounds__(PB) void k_part2_res(KParams p, const uint64_t* buf
                 sbin[pos] = (uint16_t)bin[j];
             }
         }
+        __builtin_amdgcn_sched_barrier(0);  // keep the next tile's loads below the placement
+        KH_P2_LOAD(t + G * PART_TILE);  // next tile in flight while this one is written
         lds_barrier();
+#pragma unroll 4
         for (uint32_t x = threadIdx.x; x < total; x += PB) {
             const uint32_t q = sbin[x];
             const uint32_t w = gpos[q] + (x - start[q]);
@@ -665,6 +769,7 @@ __global__ __launch_bounds__(PB) void k_part2_res(KParams p, const uint64_t* buf
         lds_barrier();
     }
 }
+#undef KH_P2_LOAD
 
 // pass-2 offsets stored [bucket][block-in-bucket][bin]
 struct Off2Idx {
