@@ -156,15 +156,18 @@ def main():
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic.get("k_walk") if traffic else None,
             "alg_bytes_per_unit": b_alg, "units_per_launch": nl, "avg_launch_ms": walk_ms,
+            "traffic_GBs": (traffic["k_walk"] / (walk_ms / 1e3) / 1e9) if traffic and "k_walk" in traffic else None,
             "random_access_ceiling": {
                 "lookups_per_s": nl / (walk_ms / 1e3),
-                "measured_peak_dependent_16B_loads_per_s": 50.8e9,
-                "note": "tools/membench chase16 at a 6.4 GB table (profiles/r01/membench.jsonl); "
-                        "one walk step = one dependent 16-B slot probe + ~0.5 extra probes"},
+                "measured_peak_random_64B_requests_per_s": 50.8e9,
+                "note": "tools/membench chase16/chase64q at a 6.4 GB table (profiles/r01/membench.jsonl): "
+                        "one random 16-64 B load = one 64-B HBM read request (TCC_EA0_RDREQ, calibrated in "
+                        "profiles/pmc_traffic.json 'membench'); the walk issues ~1.06 requests per lookup "
+                        "(4-lane block probes)"},
             "note": "achieved = algorithmic bytes (2*sizeof(kmer_pair) per lookup) / HIP-event "
                     "duration of k_walk" + (f"; traffic from {tsrc}" if tsrc else "")}
-    insert_pipe = {"kernels": "k_part1_convert, scan, k_part1_scatter, k_part2_hist, scan, "
-                              "k_part2_scatter, k_part_build, k_insert_overflow",
+    insert_pipe = {"kernels": "k_part1_convert, scan, k_part1_scatter, k_part2_res, k_part_build, "
+                              "k_insert_overflow",
                    "ms": ins_ms, "achieved_alg_GBs": n * b_alg / (ins_ms / 1e3) / 1e9,
                    "inserts_per_s": n / (ins_ms / 1e3),
                    "traffic": traffic.get("insert_pipeline") if traffic else None}

@@ -99,7 +99,12 @@ __global__ void k_chaseg(const uint64_t* t, uint64_t nblocks, int iters, uint64_
 }
 
 int main(int argc, char** argv) {
-    const double gib[] = {0.25, 1, 2, 4, 6.4, 16};
+    // "calib": one pass over a 6.4 GB table per case, for PMC calibration of random access widths
+    const bool calib = argc > 1 && !strcmp(argv[1], "calib");
+    const double gib_all[] = {0.25, 1, 2, 4, 6.4, 16};
+    const double gib_cal[] = {6.4};
+    const double* gib_p = calib ? gib_cal : gib_all;
+    const int ngib = calib ? 1 : 6;
     const uint64_t maxw = (uint64_t)(16.0 * (1ull << 30) / 8);
     uint64_t *t, *sink;
     CK(hipMalloc(&t, maxw * 8));
@@ -110,7 +115,8 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const int threads = 256;
-    for (double g : gib) {
+    for (int gi = 0; gi < ngib; ++gi) {
+        const double g = gib_p[gi];
         const uint64_t nslots = (uint64_t)(g * (1ull << 30) / 16);
         struct Case { const char* name; int grid; int iters; } cases[] = {
             {"gather16", 16384, 64}, {"chase16", 2048, 256}, {"cas8", 16384, 16},
@@ -119,7 +125,7 @@ int main(int argc, char** argv) {
             {"chase16w", 8192, 256}};
         for (auto& c : cases) {
             float best = 1e30f;
-            for (int rep = 0; rep < 3; ++rep) {
+            for (int rep = 0; rep < (calib ? 1 : 3); ++rep) {
                 CK(hipEventRecord(a));
                 if (c.name[0] == 'g') k_gather16<<<c.grid, threads>>>(t, nslots, c.iters, sink);
                 else if (!strcmp(c.name, "chase32p")) k_chaseg<2><<<c.grid, threads>>>(t, nslots / 2, c.iters, sink);

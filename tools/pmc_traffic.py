@@ -15,12 +15,20 @@ import json
 import os
 import sys
 
-KERNELS = {"k_insert": "k_insert<", "k_walk": "k_walk<", "k_part1_convert": "k_part1_convert<",
-           "k_part1_scatter": "k_part1_scatter<", "k_part2_hist": "k_part2_hist<",
-           "k_part2_scatter": "k_part2_scatter<", "k_part_build": "k_part_build<",
-           "k_insert_overflow": "k_insert_overflow<"}
-PIPELINE = ["k_part1_convert", "k_part1_scatter", "k_part2_hist", "k_part2_scatter", "k_part_build",
-            "k_insert_overflow"]
+KERNELS = {"k_insert": ("k_insert<",), "k_walk": ("k_walk<", "k_walk_g<"),
+           "k_part1_convert": ("k_part1_convert<",), "k_part1_fused": ("k_part1_fused<",),
+           "k_part1_scatter": ("k_part1_scatter<",), "k_part2_hist": ("k_part2_hist<",),
+           "k_part2_scatter": ("k_part2_scatter<",), "k_part2_res": ("k_part2_res<",),
+           "k_part_build": ("k_part_build<",), "k_insert_overflow": ("k_insert_overflow<",),
+           "membench_gather16": ("k_gather16",), "membench_chase16": ("k_chase16",),
+           "membench_chase64q": ("k_chasegILi4",), "membench_chase128o": ("k_chasegILi8",)}
+# kernels of the insert pipeline (whichever of them ran)
+PIPELINE = ["k_part1_convert", "k_part1_fused", "k_part1_scatter", "k_part2_hist", "k_part2_scatter",
+            "k_part2_res", "k_part_build", "k_insert_overflow"]
+# random-access kernels: FETCH_SIZE is NOT doubled (the 1/2 correction is for wide coalesced
+# streaming reads); their requests are calibrated against tools/membench (random 16-B loads)
+RANDOM = {"k_walk", "k_insert", "k_insert_overflow", "membench_gather16", "membench_chase16",
+          "membench_chase64q", "membench_chase128o"}
 
 
 def per_kernel(counter, prefix):
@@ -29,10 +37,13 @@ def per_kernel(counter, prefix):
         return {}
     vals = {}
     for r in csv.DictReader(open(files[0])):
-        for short, pat in KERNELS.items():
-            if pat in r["Kernel_Name"]:
-                vals.setdefault(short, []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}
+        for short, pats in KERNELS.items():
+            if any(pat in r["Kernel_Name"] for pat in pats):
+                vals.setdefault((short, r.get("Counter_Name", counter)), []).append(float(r["Counter_Value"]))
+    out = {}
+    for (k, c), v in vals.items():
+        out.setdefault(c, {})[k] = sum(v) / len(v)
+    return out[counter] if counter in out else out
 
 
 def main():
@@ -42,18 +53,24 @@ def main():
     fetch = per_kernel("FETCH_SIZE", prefix)
     write = per_kernel("WRITE_SIZE", prefix)
     atom = per_kernel("TCC_EA0_ATOMIC_sum", prefix)
+    req = per_kernel("RDREQ", prefix)  # pass with TCC_EA0_RDREQ_sum, _32B_sum, TCC_BUBBLE_sum
     try:
         doc = json.load(open(out))
     except (OSError, ValueError):
         doc = {}
     e = {"n": n, "unit": "bytes per launch",
-         "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH half-count correction)",
-         "raw_kib": {"FETCH_SIZE": fetch, "WRITE_SIZE": write}, "atomics": atom}
+         "formula": "streaming kernels: 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH half-count correction, "
+                    "MI355X_MICROARCH.md HBM); random-access kernels: FETCH_SIZE + WRITE_SIZE (64-B "
+                    "read requests, calibrated with tools/membench, see 'requests')",
+         "raw_kib": {"FETCH_SIZE": fetch, "WRITE_SIZE": write}, "atomics": atom, "requests": req}
     for k in KERNELS:
         if k in fetch and k in write:
-            e[k] = 2 * fetch[k] * 1024 + write[k] * 1024
-    if all(k in e for k in PIPELINE):
-        e["insert_pipeline"] = sum(e[k] for k in PIPELINE)
+            f = 1 if k in RANDOM else 2
+            e[k] = f * fetch[k] * 1024 + write[k] * 1024
+    ran = [k for k in PIPELINE if k in e]
+    if ran:
+        e["insert_pipeline"] = sum(e[k] for k in ran)
+        e["insert_pipeline_kernels"] = ran
     doc[workload] = e
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
