@@ -365,19 +365,35 @@ __global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __res
 // probe ~1 + P(the run crosses the block end).
 // Walker state is replicated in the G lanes of a group; the group's lane 0 (the leader) performs
 // every side effect (chunk allocation, base words, contig length, segment records).
-template <int W, int G>
-__global__ __launch_bounds__(BLOCK) void k_walk_g(KParams p, const uint64_t* __restrict__ slots,
+// ---------------------------------------------------------------------------------------------
+// Quad-transposed walker (KH_WALK_G=-4, the default): one walker per lane as in k_walk (no
+// redundant per-walker ALU), but every probe reads the walker's whole 4-slot block (64 B at 16-B
+// slots): lane q of a quad loads slot q of the block of each of the quad's 4 walkers, so a lookup
+// costs ~1.06 random requests instead of ~1.3 (linear-probing displacement crossing a slot). All
+// intra-quad exchange is DPP quad_perm (ALU, no LDS): each walker's probe position and key are
+// broadcast to its quad, and the hit slot's extension comes back by a quad OR-reduction.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int J>
+__device__ __forceinline__ uint64_t qbcast64(uint64_t v) {  // value of quad lane J
+    constexpr int C = J * 0x55;  // quad_perm [J,J,J,J]
+    return ((uint64_t)qperm32<C>((uint32_t)(v >> 32)) << 32) | qperm32<C>((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t qor32(uint32_t v) {
+    v |= qperm32<0xB1>(v);  // [1,0,3,2]
+    v |= qperm32<0x4E>(v);  // [2,3,0,1]
+    return v;
+}
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __restrict__ slots,
                                                   uint64_t cap, WalkBuffers wb,
                                                   unsigned long long* ctr,
                                                   unsigned long long* stats) {
-    static_assert(G >= 2 && G <= 16 && (G & (G - 1)) == 0, "group size");
     const uint32_t lane = lane_id();
-    const uint32_t q = lane & (G - 1), gl = lane & ~(uint32_t)(G - 1);
-    const bool lead = q == 0;
-    constexpr uint64_t GM = (1ull << G) - 1;
-    uint64_t LM = 0;  // one bit per group leader
-#pragma unroll
-    for (int i = 0; i < 64; i += G) LM |= 1ull << i;
+    const uint32_t q = lane & 3, ql = lane & ~3u;
     const uint64_t n = wb.n_starts + walk_splits(wb);
     const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
     uint64_t bbase = 0;
@@ -391,11 +407,11 @@ __global__ __launch_bounds__(BLOCK) void k_walk_g(KParams p, const uint64_t* __r
     uint32_t fwd = 0, steps = 0, chunk = 0;
     while (true) {
         while (true) {
-            const bool need = !active && !done;  // uniform within a group
-            const uint64_t m = __ballot(need) & LM;
+            const bool need = !active && !done;
+            const uint64_t m = __ballot(need);
             if (m) {
                 const uint32_t cnt = (uint32_t)__popcll(m);
-                const uint32_t rank = (uint32_t)__popcll(m & ((1ull << gl) - 1));
+                const uint32_t rank = mbcnt64(m);
                 const uint32_t avail = WALK_GRAB - bused;
                 const uint32_t src_old = min(bused + rank, (uint32_t)WALK_GRAB - 1);
                 const uint64_t o0 = __shfl(bw0, (int)src_old, 64);
@@ -450,87 +466,308 @@ __global__ __launch_bounds__(BLOCK) void k_walk_g(KParams p, const uint64_t* __r
             }
             const bool fin = active && resolved && fwd > 3;
             if (fin) {
-                if (lead) {
-                    if (fwd != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
-                    finish_contig(o, c, steps, chunk, buf);
-                }
+                if (fwd != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+                finish_contig(o, c, steps, chunk, buf);
                 active = false;
             }
             if (!__any(fin)) break;
         }
         if (!__any(active)) break;
         if (active && resolved) {
-            if (lead) {
-                append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
-            } else {
-                ++steps;
-            }
+            append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
             k = key_next(k, fwd, p);
             const uint64_t h = key_hash(k);
             if (is_splitter(h, p)) {
-                if (lead) {
-                    finish_contig(o, c, steps, chunk, buf);
-                    wb.seg_next[c] = SEG_AT_SPLIT;
-                    wb.seg_key[2 * c] = k.hi;
-                    wb.seg_key[2 * c + 1] = k.lo;
-                }
+                finish_contig(o, c, steps, chunk, buf);
+                wb.seg_next[c] = SEG_AT_SPLIT;
+                wb.seg_key[2 * c] = k.hi;
+                wb.seg_key[2 * c + 1] = k.lo;
                 active = false;
             } else {
                 s = home_slot(h, cap);
                 resolved = false;
             }
         }
-        // -- one block load per active group: lane q reads slot (s & ~(G-1)) + q ------------------
-        const uint64_t lb = s & ~(uint64_t)(G - 1);
-        const uint64_t my = lb + q;
-        const bool valid = active && my >= s && my < cap;
-        uint64_t w0 = EMPTY, w1 = 0;
-        if (active && my < cap) load_slot<W>(slots, my, w0, w1);
-        const bool empty = w0 == EMPTY;
-        const bool hit = !empty & ((w0 >> 6) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
-        const uint64_t bh = (__ballot(valid && hit) >> gl) & GM;
-        const uint64_t be = (__ballot(valid && empty) >> gl) & GM;
-        const uint32_t fh = bh ? (uint32_t)__builtin_ctzll(bh) : (uint32_t)G;
-        const uint32_t fe = be ? (uint32_t)__builtin_ctzll(be) : (uint32_t)G;
-        const uint64_t hw0 = __shfl(w0, (int)(gl + (fh & (G - 1))), 64);
+        // -- quad block probes: 4 loads per lane, one per quad member's block ------------------
+        const uint64_t sp = active ? s : ~0ull;  // ~0: inactive walker, no load
+        uint64_t sj[4], w0[4], w1[4];
+        sj[0] = qbcast64<0>(sp);
+        sj[1] = qbcast64<1>(sp);
+        sj[2] = qbcast64<2>(sp);
+        sj[3] = qbcast64<3>(sp);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t my = (sj[j] & ~3ull) + q;
+            w0[j] = EMPTY;
+            w1[j] = 0;
+            if (sj[j] != ~0ull && my < cap) load_slot<W>(slots, my, w0[j], w1[j]);
+        }
+        uint64_t kh_[4], kl_[4];
+        kh_[0] = qbcast64<0>(k.hi);
+        kh_[1] = qbcast64<1>(k.hi);
+        kh_[2] = qbcast64<2>(k.hi);
+        kh_[3] = qbcast64<3>(k.hi);
+        kl_[0] = qbcast64<0>(k.lo);
+        kl_[1] = qbcast64<1>(k.lo);
+        kl_[2] = qbcast64<2>(k.lo);
+        kl_[3] = qbcast64<3>(k.lo);
+        uint32_t myfh = 4, myfe = 4, myext = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t my = (sj[j] & ~3ull) + q;
+            const bool valid = sj[j] != ~0ull && my >= sj[j] && my < cap;
+            const bool empty = w0[j] == EMPTY;
+            const bool hit = !empty & ((w0[j] >> 6) == ((W == 1) ? kl_[j] : kh_[j])) &
+                             ((W == 1) | (w1[j] == kl_[j]));
+            const uint32_t bh = (uint32_t)(__ballot(valid && hit) >> ql) & 0xFu;
+            const uint32_t be = (uint32_t)(__ballot(valid && empty) >> ql) & 0xFu;
+            const uint32_t fh = bh ? (uint32_t)__builtin_ctz(bh) : 4u;
+            const uint32_t fe = be ? (uint32_t)__builtin_ctz(be) : 4u;
+            const uint32_t ext = qor32(q == fh ? slot_ext(w0[j]) | 0x40u : 0u);
+            if (q == (uint32_t)j) {
+                myfh = fh;
+                myfe = fe;
+                myext = ext;
+            }
+        }
         if (active) {
-            if (fh < fe) {
-                fwd = ext_fwd(slot_ext(hw0));
+            if (myfh < myfe) {
+                fwd = ext_fwd(myext & 63u);
                 resolved = true;
                 if (steps > wb.max_steps) {
-                    if (lead) {
-                        atomicAdd(&stats[ST_CYCLE], 1ull);
-                        finish_contig(o, c, steps, chunk, buf);
-                    }
+                    atomicAdd(&stats[ST_CYCLE], 1ull);
+                    finish_contig(o, c, steps, chunk, buf);
                     active = false;
                 }
-            } else if (fe < (uint32_t)G) {
-                if (lead) {
-                    atomicAdd(&stats[ST_MISSING], 1ull);
-                    finish_contig(o, c, steps, chunk, buf);
-                }
+            } else if (myfe < 4u) {
+                atomicAdd(&stats[ST_MISSING], 1ull);
+                finish_contig(o, c, steps, chunk, buf);
                 active = false;
             } else {
-                s = (lb + G >= cap) ? 0 : lb + G;
+                const uint64_t nx = (s & ~3ull) + 4;
+                s = nx >= cap ? 0 : nx;
             }
         }
     }
 }
 
-// Walker lanes per contig: KH_WALK_G = 1 (per-lane walker) or a block size in slots. Default 4
-// (C3: 5.36-5.9 ms vs 5.47 for per-lane walkers, 7.6 ms at 8: too few walkers resident to
-// cover the latency; C2: 0.68 vs 0.75 ms).
+// NS walkers per group (KH_WALK_NS): the group's NS block loads are issued back to back, so
+// each group keeps NS requests in flight (at G=4 one walker per group leaves the walk latency-
+// bound: 8 waves/SIMD hold only 131K walkers).
+template <int W, int G, int NS>
+__global__ __launch_bounds__(BLOCK, NS == 2 ? 8 : 1) void k_walk_g(KParams p, const uint64_t* __restrict__ slots,
+                                                  uint64_t cap, WalkBuffers wb,
+                                                  unsigned long long* ctr,
+                                                  unsigned long long* stats) {
+    static_assert(G >= 2 && G <= 16 && (G & (G - 1)) == 0, "group size");
+    const uint32_t lane = lane_id();
+    const uint32_t q = lane & (G - 1), gl = lane & ~(uint32_t)(G - 1);
+    const bool lead = q == 0;
+    constexpr uint64_t GM = (1ull << G) - 1;
+    uint64_t LM = 0;  // one bit per group leader
+#pragma unroll
+    for (int i = 0; i < 64; i += G) LM |= 1ull << i;
+    const uint64_t below = (1ull << gl) - 1;
+    const uint64_t n = wb.n_starts + walk_splits(wb);
+    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
+    uint64_t bbase = 0;
+    uint32_t bused = WALK_GRAB;
+    bool bdry = false;
+    uint64_t bw0 = 0, bw1 = 0;
+
+    bool active[NS], done[NS], resolved[NS];
+    uint64_t c[NS], s[NS], buf[NS];
+    Key k[NS];
+    uint32_t fwd[NS], steps[NS], chunk[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        active[i] = done[i] = resolved[i] = false;
+        c[i] = s[i] = buf[i] = 0;
+        k[i] = Key{0, 0};
+        fwd[i] = steps[i] = chunk[i] = 0;
+    }
+    while (true) {
+        while (true) {
+            bool need[NS];
+            uint32_t rank[NS];
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                need[i] = !active[i] && !done[i];  // uniform within a group
+                const uint64_t m = __ballot(need[i]) & LM;
+                rank[i] = cnt + (uint32_t)__popcll(m & below);
+                cnt += (uint32_t)__popcll(m);
+            }
+            if (cnt) {
+                const uint32_t avail = WALK_GRAB - bused;
+                uint64_t x0[NS], x1[NS], xc[NS];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    const uint32_t src_old = min(bused + rank[i], (uint32_t)WALK_GRAB - 1);
+                    x0[i] = __shfl(bw0, (int)src_old, 64);
+                    x1[i] = __shfl(bw1, (int)src_old, 64);
+                    xc[i] = rank[i] < avail ? bbase + src_old : ~0ull;
+                }
+                if (cnt > avail) {
+                    if (!bdry) {
+                        unsigned long long g = 0;
+                        if (lane == 0) g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB);
+                        bbase = __shfl(g, 0, 64);
+                        if (bbase >= n) bdry = true;
+                        const uint64_t mi = bbase + lane;
+                        if (mi < n) {
+                            const uint64_t* src = mi < wb.n_starts ? wb.starts + mi * W
+                                                                   : wb.splits + (mi - wb.n_starts) * W;
+                            bw0 = src[0];
+                            bw1 = (W == 2) ? src[1] : 0;
+                        }
+#pragma unroll
+                        for (int i = 0; i < NS; ++i) {
+                            const uint32_t src_new = min(rank[i] - min(rank[i], avail), (uint32_t)WALK_GRAB - 1);
+                            const uint64_t n0 = __shfl(bw0, (int)src_new, 64);
+                            const uint64_t n1 = __shfl(bw1, (int)src_new, 64);
+                            if (rank[i] >= avail) {
+                                x0[i] = n0;
+                                x1[i] = n1;
+                                xc[i] = bbase + src_new;
+                            }
+                        }
+                    }
+                    bused = cnt - avail;
+                } else {
+                    bused += cnt;
+                }
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    if (need[i]) {
+                        if (xc[i] < n) {
+                            c[i] = xc[i];
+                            k[i] = slot_key(x0[i], x1[i], p);
+                            fwd[i] = ext_fwd(slot_ext(x0[i]));
+                            steps[i] = 0;
+                            buf[i] = 0;
+                            active[i] = true;
+                            resolved[i] = true;
+                        } else {
+                            done[i] = true;
+                        }
+                    }
+                }
+            }
+            bool anyfin = false;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                const bool fin = active[i] && resolved[i] && fwd[i] > 3;
+                if (fin) {
+                    if (lead) {
+                        if (fwd[i] != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
+                        finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
+                    }
+                    active[i] = false;
+                }
+                anyfin |= fin;
+            }
+            if (!__any(anyfin)) break;
+        }
+        bool anyact = false;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) anyact |= active[i];
+        if (!__any(anyact)) break;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (active[i] && resolved[i]) {
+                if (lead) {
+                    append_base(o, c[i], fwd[i], steps[i], chunk[i], buf[i], ctr, stats);
+                } else {
+                    ++steps[i];
+                }
+                k[i] = key_next(k[i], fwd[i], p);
+                const uint64_t h = key_hash(k[i]);
+                if (is_splitter(h, p)) {
+                    if (lead) {
+                        finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
+                        wb.seg_next[c[i]] = SEG_AT_SPLIT;
+                        wb.seg_key[2 * c[i]] = k[i].hi;
+                        wb.seg_key[2 * c[i] + 1] = k[i].lo;
+                    }
+                    active[i] = false;
+                } else {
+                    s[i] = home_slot(h, cap);
+                    resolved[i] = false;
+                }
+            }
+        }
+        // -- NS block loads per active group, all in flight together ------------------------------
+        uint64_t w0[NS], w1[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const uint64_t my = (s[i] & ~(uint64_t)(G - 1)) + q;
+            w0[i] = EMPTY;
+            w1[i] = 0;
+            if (active[i] && my < cap) load_slot<W>(slots, my, w0[i], w1[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const uint64_t lb = s[i] & ~(uint64_t)(G - 1);
+            const uint64_t my = lb + q;
+            const bool valid = active[i] && my >= s[i] && my < cap;
+            const bool empty = w0[i] == EMPTY;
+            const bool hit = !empty & ((w0[i] >> 6) == ((W == 1) ? k[i].lo : k[i].hi)) &
+                             ((W == 1) | (w1[i] == k[i].lo));
+            const uint64_t bh = (__ballot(valid && hit) >> gl) & GM;
+            const uint64_t be = (__ballot(valid && empty) >> gl) & GM;
+            const uint32_t fh = bh ? (uint32_t)__builtin_ctzll(bh) : (uint32_t)G;
+            const uint32_t fe = be ? (uint32_t)__builtin_ctzll(be) : (uint32_t)G;
+            const uint64_t hw0 = __shfl(w0[i], (int)(gl + (fh & (G - 1))), 64);
+            if (active[i]) {
+                if (fh < fe) {
+                    fwd[i] = ext_fwd(slot_ext(hw0));
+                    resolved[i] = true;
+                    if (steps[i] > wb.max_steps) {
+                        if (lead) {
+                            atomicAdd(&stats[ST_CYCLE], 1ull);
+                            finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
+                        }
+                        active[i] = false;
+                    }
+                } else if (fe < (uint32_t)G) {
+                    if (lead) {
+                        atomicAdd(&stats[ST_MISSING], 1ull);
+                        finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
+                    }
+                    active[i] = false;
+                } else {
+                    s[i] = (lb + G >= cap) ? 0 : lb + G;
+                }
+            }
+        }
+    }
+}
+
+// Walker shape (KH_WALK_G): -4 = quad-transposed block probes (k_walk_q, default), 1 = per-lane
+// walker (k_walk), G = 2..16 lanes per contig (k_walk_g). C3 k_walk on one box: -4: 5.38 ms,
+// 4: 5.50, 1: 5.59; 8: 7.6 (too few walkers resident). C2: 4 beat 1 by 9 %.
 static int walk_group(const KParams& p) {
     const char* e = getenv("KH_WALK_G");
     if (e && *e) return atoi(e);
     (void)p;
-    return 4;
+    return -4;
+}
+
+static int walk_states() {
+    const char* e = getenv("KH_WALK_NS");
+    return (e && *e) ? atoi(e) : 1;
 }
 
 template <int W, int G>
 static void launch_walk_g(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                           unsigned long long* stats, unsigned grid, hipStream_t s) {
-    k_walk_g<W, G><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+    switch (walk_states()) {
+        case 2: k_walk_g<W, G, 2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); break;
+        case 3: k_walk_g<W, G, 3><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); break;
+        case 4: k_walk_g<W, G, 4><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); break;
+        default: k_walk_g<W, G, 1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+    }
 }
 
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
@@ -538,7 +775,16 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     const uint64_t nw = wb.n_starts + wb.n_splits;
     if (nw == 0) return hipSuccess;
     const int G = walk_group(p);
-    const uint64_t lanes = nw * (uint64_t)(G > 1 ? G : 1);
+    if (G == -4) {  // quad-transposed: one walker per lane
+        const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
+                                             (uint64_t)(grid_blocks > 0 ? grid_blocks : 2048));
+        if (p.W == 1)
+            k_walk_q<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+        else
+            k_walk_q<2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+        return hipGetLastError();
+    }
+    const uint64_t lanes = nw * (uint64_t)(G > 1 ? G : 1) / (uint64_t)(G > 1 ? walk_states() : 1) + 1;
     uint64_t want = (lanes + BLOCK - 1) / BLOCK;
     unsigned grid = (unsigned)hmin(want, (uint64_t)(grid_blocks > 0 ? grid_blocks : 2048));
     if (p.W == 1) {

@@ -313,7 +313,7 @@ def test_gpu_splitters_off_equals_on(monkeypatch):
 
 
 # ---- walker shapes: per-lane (G=1) and cooperative block probes (G lanes per contig) ----------
-@pytest.mark.parametrize("G", ["1", "2", "4", "8", "16"])
+@pytest.mark.parametrize("G", ["-4", "1", "2", "4", "8", "16"])
 @pytest.mark.parametrize("k,n,lmin,lmax,load", [
     (51, 2_000_000, 8, 200, 0.5),
     (19, 1_000_000, 1, 2000, 0.9),     # W=1 slots, long runs at high load (block-crossing probes)
@@ -324,7 +324,7 @@ def test_gpu_walk_group_sizes(monkeypatch, G, k, n, lmin, lmax, load):
     if (W == 2 and G == "16") or (W == 1 and G == "2"):
         pytest.skip("block larger than one 128-B line / not dispatched")
     monkeypatch.setenv("KH_WALK_G", G)
-    g = kh.SyntheticKmers(k, n, lmin, lmax, 5, seed=k + int(G))
+    g = kh.SyntheticKmers(k, n, lmin, lmax, 5, seed=k + abs(int(G)))
     with kh.KmerHashTable(k, n, load) as t:
         t.insert_all(g.records())
         nc, _ = t.assemble()
@@ -332,7 +332,26 @@ def test_gpu_walk_group_sizes(monkeypatch, G, k, n, lmin, lmax, load):
         assert t.contigs_text() == g.truth()
 
 
-@pytest.mark.parametrize("G", ["1", "8"])
+@pytest.mark.parametrize("G,NS", [("2", "2"), ("4", "2"), ("4", "3"), ("8", "4")])
+@pytest.mark.parametrize("k,n,lmin,lmax,load", [
+    (51, 2_000_000, 8, 200, 0.5),
+    (19, 1_000_000, 1, 2000, 0.9),
+])
+def test_gpu_walk_multi_walker_groups(monkeypatch, G, NS, k, n, lmin, lmax, load):
+    """NS walkers per lane group (their loads in flight together) == ground truth."""
+    if k <= 29 and G == "2":
+        pytest.skip("not dispatched for 8-B slots")
+    monkeypatch.setenv("KH_WALK_G", G)
+    monkeypatch.setenv("KH_WALK_NS", NS)
+    g = kh.SyntheticKmers(k, n, lmin, lmax, 5, seed=k + int(G) * 10 + int(NS))
+    with kh.KmerHashTable(k, n, load) as t:
+        t.insert_all(g.records())
+        nc, _ = t.assemble()
+        assert nc == g.num_contigs
+        assert t.contigs_text() == g.truth()
+
+
+@pytest.mark.parametrize("G", ["-4", "1", "8"])
 def test_gpu_walk_group_missing_kmer(monkeypatch, G):
     monkeypatch.setenv("KH_WALK_G", G)
     g = kh.SyntheticKmers(51, 200_000, 20, 40, 0, seed=5)
