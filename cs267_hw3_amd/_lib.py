@@ -71,6 +71,8 @@ _SIGS = {
     "kh_collect_starts_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_route_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.c_int, c_vp, c_vp]),
     "kh_insert_words_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
+    "kh_insert_words_stage_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_u64]),
+    "kh_insert_words_finish": (ctypes.c_int, [c_vp]),
     "kh_walk_begin": (ctypes.c_int, [c_vp, c_u64, ctypes.POINTER(c_u64)]),
     "kh_walk_emit_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp]),
     "kh_find_ext_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp]),

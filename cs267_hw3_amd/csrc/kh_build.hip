@@ -87,6 +87,7 @@ static int p1_mode(bool rec) {
     const char* e = getenv("KH_P1");
     if (!e || !*e) return rec ? 1 : 0;
     if (!strcmp(e, "fused")) return 0;
+    if (!strcmp(e, "direct")) return 3;
     return !strcmp(e, "rec") ? 2 : 1;
 }
 static bool p2_res() {
@@ -529,6 +530,138 @@ __global__ __launch_bounds__(PB) void k_part1_fused(KParams p, const uint8_t* __
     }
 }
 
+// Record parse straight from global memory, no LDS staging (records of R <= 16 bytes, K <= 56):
+// lane i loads the aligned 16-B chunk holding record i's first byte and, when the record runs
+// past it, the next one; the 15-B record is funnel-shifted out of the 32-B window in registers.
+// Consecutive lanes read overlapping chunks, so a wave's loads coalesce into ~R*64/16 requests.
+__device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t sh) {  // sh in [0,64)
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+__device__ __forceinline__ void load_record_regs(const uint8_t* __restrict__ recs, uint64_t i, uint32_t R,
+                                                 uint64_t& x0, uint64_t& x1) {
+    const uint64_t a = i * R;
+    const uint32_t o = (uint32_t)(a & 15u);
+    const ulonglong2 c0 = *reinterpret_cast<const ulonglong2*>(recs + (a - o));
+    ulonglong2 c1 = make_ulonglong2(0, 0);
+    if (o + R > 16u) c1 = *reinterpret_cast<const ulonglong2*>(recs + (a - o) + 16);
+    uint64_t w0 = c0.x, w1 = c0.y, w2 = c1.x;
+    if (o >= 8u) {
+        w0 = w1;
+        w1 = w2;
+        w2 = c1.y;
+    }
+    const uint32_t sh = (o & 7u) * 8u;
+    x0 = funnel64(w0, w1, sh);
+    x1 = funnel64(w1, w2, sh);
+}
+
+// bytes 0..15 of a record (little-endian in x0, x1) -> key and extension codes (parse_record)
+__device__ __forceinline__ void parse_record_regs(uint64_t x0, uint64_t x1, const KParams& p, Key& k,
+                                                  uint32_t& ext) {
+    const unsigned __int128 be = ((unsigned __int128)__builtin_bswap64(x0) << 64) | __builtin_bswap64(x1);
+    const unsigned __int128 B = (be >> (8 * (16 - p.P))) >> (2 * p.pad);
+    k.lo = (uint64_t)B & LO_MASK;
+    k.hi = (uint64_t)(B >> 62);
+    const unsigned __int128 xx = ((unsigned __int128)x1 << 64) | x0;
+    const uint32_t e = (uint32_t)(xx >> (8 * p.P)) & 0xFFFFu;
+    ext = base_code((uint8_t)e) | (base_code((uint8_t)(e >> 8)) << 3);
+}
+
+template <int W>
+__global__ __launch_bounds__(PB) void k_part1_direct(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
+                                                     uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1,
+                                                     uint64_t* start_mask, uint64_t* split_mask,
+                                                     uint64_t* ovf, uint64_t ovf_cap,
+                                                     unsigned long long* ctr, unsigned long long* stats) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* items = smem;                                              // PART_TILE * 2 words
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + PART_TILE * 2);  // PART_TILE
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);      // NB1
+    uint32_t* start = hist + NB1;                                        // NB1
+    uint32_t* gpos = start + NB1;                                        // NB1
+    const uint32_t sub = blockIdx.x % S1;
+    const uint32_t R = (uint32_t)p.R;
+    for (int tt = 0; tt < T1; ++tt) {
+        const uint64_t base = ((uint64_t)blockIdx.x * T1 + tt) * PART_TILE;
+        if (base >= n) break;  // uniform
+        uint64_t a[PITEMS], b[PITEMS];
+        uint32_t bin[PITEMS];
+        uint64_t x0[PITEMS], x1[PITEMS];
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j) {
+            const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
+            x0[j] = x1[j] = 0;
+            if (i < n) load_record_regs(recs, i, R, x0[j], x1[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j) {
+            const uint64_t s0 = base + (uint64_t)j * PB;
+            const uint64_t i = s0 + threadIdx.x;
+            const bool valid = i < n;
+            Key k{0, 0};
+            uint32_t ext = 0;
+            if (valid) parse_record_regs(x0[j], x1[j], p, k, ext);
+            const uint64_t hk = key_hash(k);
+            if (s0 < n) {  // uniform
+                const bool is_start = valid && ext_bwd(ext) == EXT_F;
+                const uint64_t bal = __ballot(is_start);
+                const uint64_t sb = __ballot(valid && !is_start && is_splitter(hk, p));
+                const uint64_t wb = s0 + (threadIdx.x & ~63u);
+                if ((threadIdx.x & 63) == 0 && wb < n) {
+                    if (start_mask) start_mask[wb >> 6] = bal;
+                    if (split_mask) split_mask[wb >> 6] = sb;
+                }
+            }
+            a[j] = valid ? slot_w0(k, ext, p) : EMPTY;
+            b[j] = (valid && W == 2) ? k.lo : 0;
+            bin[j] = (uint32_t)(hk >> (64 - B1));
+        }
+        for (int i = threadIdx.x; i < NB1; i += PB) hist[i] = 0;
+        lds_barrier();
+        uint32_t rank[PITEMS];
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
+        lds_barrier();
+        const uint32_t total = scan_bins<NB1>(hist, start);
+        for (int i = threadIdx.x; i < NB1; i += PB)
+            gpos[i] = hist[i] ? atomicAdd(&wcnt[i * S1 + sub], hist[i]) : 0u;
+#pragma unroll
+        for (int j = 0; j < PITEMS; ++j) {
+            if (a[j] != EMPTY) {
+                const uint32_t pos = start[bin[j]] + rank[j];
+                items[pos * W] = a[j];
+                if (W == 2) items[pos * W + 1] = b[j];
+                sbin[pos] = (uint16_t)bin[j];
+            }
+        }
+        lds_barrier();
+#pragma unroll 4
+        for (uint32_t x = threadIdx.x; x < total; x += PB) {
+            const uint32_t q = sbin[x];
+            const uint32_t w = gpos[q] + (x - start[q]);
+            const uint64_t v0 = items[W * x], v1 = (W == 2) ? items[W * x + 1] : 0;
+            if (w < CAP1) {
+                const uint64_t g = (uint64_t)(q * S1 + sub) * CAP1 + w;
+                if (W == 2) {
+                    *reinterpret_cast<ulonglong2*>(buf1 + g * 2) = make_ulonglong2(v0, v1);
+                } else {
+                    buf1[g] = v0;
+                }
+            } else {
+                const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
+                if (idx < ovf_cap) {
+                    ovf[idx * W] = v0;
+                    if (W == 2) ovf[idx * W + 1] = v1;
+                } else {
+                    atomicAdd(&stats[ST_FULL], 1ull);
+                }
+            }
+        }
+        lds_barrier();
+    }
+}
+
 template <int W, bool REC>
 __global__ __launch_bounds__(PB) void k_part1_hist(KParams p, const uint8_t* recs, const uint64_t* words,
                                                    uint64_t n, uint64_t* hist1, uint64_t* start_mask,
@@ -924,13 +1057,16 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         if ((e = allow_lds(k_part2_res<W, false>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_part1_fused<W, true>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_part1_fused<W, false>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_part1_direct<W>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_part_build<W>, LDS_BYTES)) != hipSuccess) return e;
         attrs = true;
     }
     const PartPlan pl = part_plan(n);
     const unsigned nb1 = (unsigned)pl.nb1;
-    const int mode1 = p1_mode(REC);
-    const bool fused1 = mode1 == 0, rec1 = REC && mode1 == 2;
+    int mode1 = p1_mode(REC);
+    if (mode1 == 3 && (!REC || p.R > 16)) mode1 = REC ? 1 : 0;  // direct parse: records of <= 16 B
+    const bool direct1 = mode1 == 3;
+    const bool fused1 = mode1 == 0 || direct1, rec1 = REC && mode1 == 2;
     const bool res2 = fused1 || p2_res();
     if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
     uint32_t CAP1 = 0;
@@ -938,9 +1074,13 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (fused1) {
         CAP1 = part_win1_cap(n);
         if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
-        k_part1_fused<W, REC><<<nb1, PB, SORT_LDS, s>>>(p, recs, words, n, CAP1, wcnt, B.buf1, start_mask,
-                                                         split_mask, B.overflow, part_overflow_cap(n), ctr,
-                                                         stats);
+        if (direct1)
+            k_part1_direct<W><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask,
+                                                       B.overflow, part_overflow_cap(n), ctr, stats);
+        else
+            k_part1_fused<W, REC><<<nb1, PB, SORT_LDS, s>>>(p, recs, words, n, CAP1, wcnt, B.buf1, start_mask,
+                                                             split_mask, B.overflow, part_overflow_cap(n), ctr,
+                                                             stats);
     } else if (REC && !rec1) {
         // records -> words (input order) in buf2, which pass 2 only writes after pass 1 is done
         k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, B.hist1, start_mask, split_mask);
@@ -990,6 +1130,64 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     k_insert_overflow<W><<<1024, PB, 0, s>>>(p, B.overflow, part_overflow_cap(n), ctr, t.slots, t.cap,
                                              stats);
     return hipGetLastError();
+}
+
+// Staged build (sharded insert): words arrive in chunks (one per all-to-all chunk). Each chunk is
+// partitioned at once (pass 1 into its own windows, pass 2 appending to the region windows of a
+// build sized for `total` words) while the next chunk is still on the wire; one build at the end.
+template <int W>
+static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
+                             const PartBuffers& B, unsigned long long* ctr, unsigned long long* stats,
+                             hipStream_t s) {
+    hipError_t e;
+    if ((e = allow_lds(k_part1_fused<W, false>, SORT_LDS)) != hipSuccess) return e;
+    if ((e = allow_lds(k_part2_res<W, true>, SORT_LDS)) != hipSuccess) return e;
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(B.hist1);
+    uint32_t* rcnt = reinterpret_cast<uint32_t*>(B.hist2);
+    if (first) {
+        if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(rcnt, 0, (size_t)NREG * 4, s)) != hipSuccess) return e;
+    }
+    if (m == 0) return hipSuccess;
+    const PartPlan pl = part_plan(m);
+    const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(total);
+    if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
+    k_part1_fused<W, false><<<(unsigned)pl.nb1, PB, SORT_LDS, s>>>(p, nullptr, words, m, CAP1, wcnt, B.buf1,
+                                                                  nullptr, nullptr, B.overflow,
+                                                                  part_overflow_cap(total), ctr, stats);
+    k_part2_res<W, true><<<(unsigned)(NB1 * pl.G), PB, SORT_LDS, s>>>(p, B.buf1, m, B.off1, pl.G, RC, rcnt, B.buf2,
+                                                                      B.overflow, part_overflow_cap(total), ctr,
+                                                                      stats, CAP1, wcnt);
+    return hipGetLastError();
+}
+
+template <int W>
+static hipError_t part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty, const PartBuffers& B,
+                              unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+    hipError_t e;
+    if ((e = allow_lds(k_part_build<W>, LDS_BYTES)) != hipSuccess) return e;
+    const uint32_t RC = part_region_cap(total);
+    const uint32_t* rcnt = reinterpret_cast<const uint32_t*>(B.hist2);
+    const size_t lds = (size_t)region_max_slots(t.cap) * W * 8;
+    k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, total, B.off2, 1, t.slots, t.cap,
+                                                     table_empty ? 1 : 0, B.overflow, part_overflow_cap(total),
+                                                     ctr, stats, RC, rcnt);
+    k_insert_overflow<W><<<1024, PB, 0, s>>>(p, B.overflow, part_overflow_cap(total), ctr, t.slots, t.cap, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
+                             const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
+                             hipStream_t s) {
+    return p.W == 1 ? part_stage<1>(p, words, m, total, first, b, ctr, stats, s)
+                    : part_stage<2>(p, words, m, total, first, b, ctr, stats, s);
+}
+
+hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
+                              const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
+                              hipStream_t s) {
+    return p.W == 1 ? part_finish<1>(p, total, t, table_empty, b, ctr, stats, s)
+                    : part_finish<2>(p, total, t, table_empty, b, ctr, stats, s);
 }
 
 hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,

@@ -89,6 +89,8 @@ struct kh_table {
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_hist1, pb_off1, pb_hist2, pb_off2, pb_scratch, pb_ovf;  // part build
     bool last_insert_part = false;
+    bool staging = false, stage_part = false, stage_fresh = false;  // kh_insert_words_stage_dev build
+    uint64_t stage_total = 0, stage_n = 0;
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
     DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm, rw_pos, rw_ctl;  // round walker
     DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
@@ -315,6 +317,8 @@ int kh_clear(kh_table* t) {
     t->n_inserted = 0;
     t->assembled = false;
     t->split_ok = true;
+    t->staging = false;
+    t->stage_n = 0;
     return KH_OK;
 }
 
@@ -769,6 +773,76 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
     t->ins_timed = true;
     t->n_inserted += m;
+    t->assembled = false;
+    return KH_OK;
+}
+
+int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64_t total_hint) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (m && !words) return fail(KH_ERR_ARG, "null words");
+    if (int rc = set_device(t)) return rc;
+    if (!t->staging) {
+        if (total_hint < m) total_hint = m;
+        if (t->n_inserted + total_hint > t->n_kmers)
+            return fail(KH_ERR_FULL, "staging %llu k-mers into a shard created for %llu (%llu in)",
+                        (unsigned long long)total_hint, (unsigned long long)t->n_kmers,
+                        (unsigned long long)t->n_inserted);
+        t->split_ok = false;  // routed words carry no splitter marks
+        t->stage_total = total_hint;
+        t->stage_n = 0;
+        t->stage_part = use_part_build(t, total_hint);
+        kh::PartBuffers pb{};
+        if (t->stage_part)
+            if (int rc = ensure_part(t, total_hint, pb)) return rc;
+        // a partitioned build into a fresh table rewrites every slot: no clear needed
+        t->stage_fresh = t->stage_part && t->n_inserted == 0 && t->slots_stale;
+        if (!t->stage_fresh)
+            if (int rc = clean_slots(t)) return rc;
+        KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
+        t->staging = true;
+        t->last_insert_part = t->stage_part;
+        if (t->stage_part) {
+            kh::PartBuffers b{};
+            if (int rc = ensure_part(t, total_hint, b)) return rc;
+            KH_HIP(kh::launch_part_stage(t->kp, nullptr, 0, total_hint, true, b, t->ctr.as<unsigned long long>(),
+                                         t->stats.as<unsigned long long>(), t->stream));
+        }
+    }
+    if (t->stage_n + m > t->stage_total)
+        return fail(KH_ERR_FULL, "staged %llu + %llu words exceed the build's %llu",
+                    (unsigned long long)t->stage_n, (unsigned long long)m, (unsigned long long)t->stage_total);
+    if (m == 0) return KH_OK;
+    if (t->stage_part) {
+        kh::PartBuffers b{};
+        if (int rc = ensure_part(t, t->stage_total, b)) return rc;
+        KH_HIP(kh::launch_part_stage(t->kp, (const uint64_t*)words, m, t->stage_total, false, b,
+                                     t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(),
+                                     t->stream));
+    } else {
+        KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
+                                       t->stats.as<unsigned long long>(), t->stream));
+    }
+    t->stage_n += m;
+    return KH_OK;
+}
+
+int kh_insert_words_finish(kh_table* t) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (!t->staging) return fail(KH_ERR_STATE, "no staged insert open");
+    if (int rc = set_device(t)) return rc;
+    if (t->stage_part) {
+        kh::PartBuffers b{};
+        if (int rc = ensure_part(t, t->stage_total, b)) return rc;
+        KH_HIP(kh::launch_part_finish(t->kp, t->stage_total, view(t), t->stage_fresh, b, t->ctr.as<unsigned long long>(),
+                                      t->stats.as<unsigned long long>(), t->stream));
+        t->slots_stale = false;
+    }
+    KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
+    KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
+    t->ins_timed = true;
+    t->n_inserted += t->stage_n;
+    t->staging = false;
+    t->stage_n = 0;
     t->assembled = false;
     return KH_OK;
 }

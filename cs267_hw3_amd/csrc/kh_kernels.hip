@@ -555,7 +555,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __r
 // each group keeps NS requests in flight (at G=4 one walker per group leaves the walk latency-
 // bound: 8 waves/SIMD hold only 131K walkers).
 template <int W, int G, int NS>
-__global__ __launch_bounds__(BLOCK, NS == 2 ? 8 : 1) void k_walk_g(KParams p, const uint64_t* __restrict__ slots,
+__global__ __launch_bounds__(BLOCK) void k_walk_g(KParams p, const uint64_t* __restrict__ slots,
                                                   uint64_t cap, WalkBuffers wb,
                                                   unsigned long long* ctr,
                                                   unsigned long long* stats) {

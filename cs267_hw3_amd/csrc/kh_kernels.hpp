@@ -282,4 +282,14 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
                               unsigned long long* stats, hipStream_t s);
 
+// Staged build of routed words (sharded insert): launch_part_stage per received chunk (first = the
+// first chunk of a build sized for `total` words), then launch_part_finish once. Requires
+// region_slots_fit and buffers from ensure_part(total).
+hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
+                             const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
+                             hipStream_t s);
+hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
+                              const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
+                              hipStream_t s);
+
 }  // namespace kh

@@ -179,6 +179,13 @@ class GpuShard:
     def insert_words(self, words, m):
         check(self.L.kh_insert_words_dev(self.h, self._p(words), m))
 
+    def stage_words(self, words, m, total):
+        """Partition m received words toward one build of <= total (kh_insert_words_stage_dev)."""
+        check(self.L.kh_insert_words_stage_dev(self.h, self._p(words), m, total))
+
+    def finish_words(self):
+        check(self.L.kh_insert_words_finish(self.h))
+
     def walk_begin(self, total_kmers):
         nw = ctypes.c_uint64(0)
         check(self.L.kh_walk_begin(self.h, total_kmers, ctypes.byref(nw)))
@@ -388,7 +395,9 @@ class DistributedKmerHashMap:
     def _insert_pipelined(self, recs):
         """Route and exchange the records in chunks: the route kernels of chunk c+1 run while
         RCCL moves chunk c (counts go over the gloo ctrl group so they do not queue behind
-        the transfers). Words land back to back in one receive buffer sized by the shard."""
+        the transfers), and chunk c-1, already received, is partitioned toward the build
+        (stage_words) meanwhile; one build at the end (finish_words). Words land back to back
+        in one receive buffer sized by the shard."""
         sh, P, W = self.shard, self.P, self.shard.W
         n = recs.shape[0]
         nch = self.INSERT_CHUNKS
@@ -396,7 +405,7 @@ class DistributedKmerHashMap:
         words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
         recv = self._grow("_ins_recv", max(sh.n_kmers, 1) * W, torch.int64, recs.device)
         rank = self.comm.rank
-        works, pos = [], 0
+        works, spans, pos = [], [], 0
         for c in range(nch):
             c0, c1 = bounds[c], bounds[c + 1]
             w = words[c0 * W:max(c1, c0 + 1) * W]
@@ -411,17 +420,23 @@ class DistributedKmerHashMap:
             works.append(self.comm.all_to_all_async(recv[pos * W:(pos + m) * W], w[:(c1 - c0) * W],
                                                     [x * W for x in recv_splits],
                                                     [x * W for x in send_splits]))
+            spans.append((pos, m))
             pos += m
-        for wk in works:
-            wk.wait()
-        sh.insert_words(recv, pos)
+            if c > 0:  # previous chunk: received -> partition it while this one is on the wire
+                works[c - 1].wait()
+                p0, pm = spans[c - 1]
+                sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, sh.n_kmers)
+        works[-1].wait()
+        p0, pm = spans[-1]
+        sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, sh.n_kmers)
+        sh.finish_words()
         return pos
 
     def insert_all(self, recs):
         sh, P = self.shard, self.P
         sh.collect_starts(recs)
-        if (P > 1 and getattr(self.comm, "ctrl", None) is not None and self.INSERT_CHUNKS > 1
-                and recs.shape[0] >= self.PIPELINE_MIN):
+        if ((P > 1 or self.SELF_EXCHANGE) and getattr(self.comm, "ctrl", None) is not None
+                and self.INSERT_CHUNKS > 1 and recs.shape[0] >= self.PIPELINE_MIN):
             return self._insert_pipelined(recs)
         words, counts = sh.route(recs, P)
         send_splits, recv_splits, _, gmax = self._exchange_counts(counts)

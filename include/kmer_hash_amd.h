@@ -122,6 +122,14 @@ int kh_pack_text_dev(kh_table* t, const void* dev_text, uint64_t len, void* dev_
 int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
                  void* dev_counts_out);
 int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);
+/* Staged insert of routed words (one call per received all-to-all chunk, hash_map.hpp:55-80's
+ * insert_all split so that partitioning overlaps the exchange): stage partitions m words toward
+ * one build of at most total_hint words (the first stage after a clear/finish starts it; keep
+ * total_hint the same for every stage of one build); finish builds the table from them. Small
+ * builds insert each stage directly. dev_words may be reused once the next stage/finish call
+ * has been issued on the table's stream. */
+int kh_insert_words_stage_dev(kh_table* t, const void* dev_words, uint64_t m, uint64_t total_hint);
+int kh_insert_words_finish(kh_table* t);
 /* Round walk: begin (sync; sizes buffers; total_kmers = k-mers over all ranks, bounds contig
  * length), then per round emit -> exchange keys -> find_ext (owner) -> exchange replies -> apply,
  * until no rank emits; end materialises this rank's contig text (kh_contigs_text*). */

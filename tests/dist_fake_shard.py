@@ -13,8 +13,9 @@ import oracle_bind as ob
 class FakeShard:
     W = 2  # 16 bytes per routed record / query key
 
-    def __init__(self, k):
+    def __init__(self, k, n_kmers=1 << 24):
         self.k = k
+        self.n_kmers = n_kmers
         self.P = (k + 3) // 4
         self.R = self.P + 2
         assert self.R <= 16
@@ -54,15 +55,30 @@ class FakeShard:
             if r[self.P] == ord("F"):
                 self.starts.append(bytes(r))
 
-    def route(self, recs, nranks):
+    def route(self, recs, nranks, words=None):
         rows = [bytes(r) for r in recs.numpy()]
         payloads, _, counts = self._group([(self._owner(r[:self.P], nranks), r) for r in rows], nranks)
-        return self._enc(payloads), counts
+        enc = self._enc(payloads)
+        if words is not None:  # caller's buffer (the pipelined insert routes into slices of one)
+            words[:min(words.numel(), enc.numel())].copy_(enc[:words.numel()])
+            return words, counts
+        return enc, counts
 
     def insert_words(self, words, m):
         for rec in self._dec(words, m, self.R):
             assert rec[:self.P] not in self.table, "duplicate k-mer"
             self.table[rec[:self.P]] = rec
+
+    # staged insert (kh_insert_words_stage_dev / _finish): chunks are kept until finish
+    def stage_words(self, words, m, total):
+        self.staged = getattr(self, "staged", [])
+        self.staged.append(words[:m * 2].clone())
+        assert sum(t.numel() // 2 for t in self.staged) <= total
+
+    def finish_words(self):
+        for t in getattr(self, "staged", []):
+            self.insert_words(t, t.numel() // 2)
+        self.staged = []
 
     def walk_begin(self, total_kmers):
         # walker = [key bytes, fwd char (None = query in flight), contig string, done, reply pos]

@@ -21,7 +21,8 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="migrate", cap=None):
+def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="migrate", cap=None,
+               insert_chunks=None):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -34,7 +35,11 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="migr
                             world_size=world)
     k = MANIFEST[name]["k"]
     recs = kh.read_kmers(os.path.join(GOLDEN, f"{name}.txt"), k, world, rank)
-    dm = DistributedKmerHashMap(TorchComm(), FakeShard(k), protocol=protocol)
+    ctrl = dist.new_group(backend="gloo") if insert_chunks else None
+    dm = DistributedKmerHashMap(TorchComm(ctrl=ctrl), FakeShard(k), protocol=protocol)
+    if insert_chunks:                      # pipelined insert: chunked route/exchange + staged build
+        dm.INSERT_CHUNKS = insert_chunks
+        dm.PIPELINE_MIN = 0
     if cap:
         dm.CAP_LIMIT = cap                 # force segment overflow -> retry rounds
         dm.CHECK_EVERY = 3
@@ -76,3 +81,18 @@ def test_sharded_driver_gloo(tmp_path, name, world, chunk, protocol, cap):
     assert sorted(b"".join(parts).splitlines()) == sorted(want.splitlines())
     rounds = {open(tmp_path / f"rounds_{r}").read() for r in range(world)}
     assert len(rounds) == 1                    # every rank ran the same number of rounds
+
+
+@pytest.mark.parametrize("name,world,chunks", [("small51", 2, 3), ("mixed19", 3, 4), ("singles51", 2, 2)])
+def test_sharded_pipelined_insert_gloo(tmp_path, name, world, chunks):
+    """Pipelined insert over gloo: chunk counts over the ctrl group, async all-to-alls, each
+    received chunk staged while the next is in flight, one build at the end."""
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), None, "migrate", None,
+                                         chunks), nprocs=world, join=True, start_method="spawn")
+    import cs267_hw3_amd as kh
+    m = MANIFEST[name]
+    g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"],
+                          seed=m["seed"])
+    for r in range(world):
+        b, e = g.block(world, r)
+        assert open(tmp_path / f"test_{r}.dat", "rb").read() == g.truth(b, e)

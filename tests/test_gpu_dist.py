@@ -109,3 +109,39 @@ def test_sharded_pipelined_insert(chunks):
     from cs267_hw3_amd.dist import run_threaded
     g = kh.SyntheticKmers(51, 6_000_000, 8, 200, 10, seed=321)
     check_ranks(g, run_threaded(51, g.records(), 4, insert_chunks=chunks), 4)
+
+
+@pytest.mark.parametrize("mode", ["auto", "cas"])
+@pytest.mark.parametrize("k,n,chunks", [(51, 3_000_000, 4), (19, 2_000_000, 3), (51, 200_000, 2)])
+def test_staged_insert_words(monkeypatch, mode, k, n, chunks):
+    """kh_insert_words_stage_dev per chunk (an empty one included) + kh_insert_words_finish ==
+    one insert: the walk reproduces the ground truth; staging past the build's size fails."""
+    import torch
+    from cs267_hw3_amd import _lib
+    from cs267_hw3_amd.dist import GpuShard
+    if mode != "auto":
+        monkeypatch.setenv("KH_INSERT", mode)
+    g = kh.SyntheticKmers(k, n, 8, 300, 10, seed=k + chunks)
+    sh = GpuShard(k, n + 5)
+    with torch.cuda.stream(sh.stream):
+        recs = torch.from_numpy(g.records()).cuda()
+        sh.collect_starts(recs)
+        words, _ = sh.route(recs, 1)
+        W = sh.W
+        bounds = [n * c // chunks for c in range(chunks + 1)]
+        for c in range(chunks):
+            a, b = bounds[c], bounds[c + 1]
+            sh.stage_words(words[a * W:b * W], b - a, n + 5)
+            if c == 0:
+                sh.stage_words(words[:0], 0, n + 5)
+        sh.finish_words()
+        sh.table.assemble()
+        assert sh.table.contigs_text() == g.truth()
+        s = sh.stats()
+        assert s["n_dup"] == 0 and s["n_inserted"] == n
+        sh.clear()
+        sh.stage_words(words[:W * 10], 10, 10)
+        with pytest.raises(kh.KmerHashError) as e:
+            sh.stage_words(words[:W * 10], 10, 10)
+        assert e.value.code == _lib.KH_ERR_FULL
+        sh.finish_words()
