@@ -70,6 +70,7 @@ _SIGS = {
     "kh_word_count": (ctypes.c_int, [ctypes.c_int]),
     "kh_collect_starts_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_route_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.c_int, c_vp, c_vp]),
+    "kh_route_starts_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.c_int, c_vp, c_vp]),
     "kh_insert_words_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_insert_words_stage_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_u64]),
     "kh_insert_words_finish": (ctypes.c_int, [c_vp]),

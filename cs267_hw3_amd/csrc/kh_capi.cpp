@@ -91,6 +91,7 @@ struct kh_table {
     bool last_insert_part = false;
     bool staging = false, stage_part = false, stage_fresh = false;  // kh_insert_words_stage_dev build
     uint64_t stage_total = 0, stage_n = 0;
+    uint64_t collected_n = 0;  // records passed to kh_route_starts_dev since the last clear
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
     DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm, rw_pos, rw_ctl;  // round walker
     DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
@@ -319,6 +320,7 @@ int kh_clear(kh_table* t) {
     t->split_ok = true;
     t->staging = false;
     t->stage_n = 0;
+    t->collected_n = 0;
     return KH_OK;
 }
 
@@ -739,6 +741,36 @@ int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void
                             t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
                             t->route_scratch.as<uint64_t>(), t->route_own.as<uint8_t>(), (uint64_t*)words_out,
                             (uint64_t*)counts_out, t->stream));
+    return KH_OK;
+}
+
+int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* words_out,
+                        void* counts_out) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
+    if (!counts_out || (n && (!dev_recs || !words_out))) return fail(KH_ERR_ARG, "null buffer");
+    if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, n, nranks)) return rc;
+    if (int rc = t->route_own.ensure(n + 16)) return rc;
+    const uint64_t nw = (n + 63) / 64;
+    int rc;
+    if ((rc = t->mask.ensure(nw * 8 + 8))) return rc;
+    if ((rc = t->mask_off.ensure(nw * 8 + 8))) return rc;
+    if ((rc = t->scratch.ensure(kh::scan_scratch_words(nw) * 8 + 64))) return rc;
+    // capacity bound from host-side counts: no device read (and no host sync) per call
+    if ((rc = ensure_starts(t, t->collected_n + n))) return rc;
+    KH_HIP(kh::launch_route(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks,
+                            t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
+                            t->route_scratch.as<uint64_t>(), t->route_own.as<uint8_t>(), (uint64_t*)words_out,
+                            (uint64_t*)counts_out, t->stream, n ? t->mask.as<uint64_t>() : nullptr));
+    if (n)
+        KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
+                                         t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                         t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(),
+                                         t->stream));
+    t->collected_n += n;
+    t->assembled = false;
     return KH_OK;
 }
 

@@ -1157,7 +1157,8 @@ __device__ __forceinline__ void stage_records(const uint8_t* recs, uint64_t sub,
 }
 
 __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
-                                                     uint32_t P, uint8_t* own, uint64_t* hist) {
+                                                     uint32_t P, uint8_t* own, uint64_t* hist,
+                                                     uint64_t* start_mask) {
     __shared__ uint32_t h[MAX_RANKS];
     __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
     for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
@@ -1174,6 +1175,11 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* _
             const uint32_t q = owner_key(k, p, P);
             own[sub + threadIdx.x] = (uint8_t)q;
             atomicAdd(&h[q], 1u);
+        }
+        if (start_mask) {  // kmer_hash.cpp:27-31 start bits, same pass (ROUTE_TILE is 64-aligned)
+            const uint64_t bal = __ballot(threadIdx.x < cnt && st[threadIdx.x * p.R + p.P] == 'F');
+            const uint64_t wb = sub + (threadIdx.x & ~63u);
+            if ((threadIdx.x & 63) == 0 && wb < n) start_mask[wb >> 6] = bal;
         }
     }
     __syncthreads();
@@ -1211,11 +1217,11 @@ __global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p, const uint8_
 
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
                         uint64_t* hist, uint64_t* off, uint64_t* scratch, uint8_t* own, uint64_t* out_words,
-                        uint64_t* counts, hipStream_t s) {
+                        uint64_t* counts, hipStream_t s, uint64_t* start_mask) {
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
     const uint64_t nb = route_blocks(n);
     if (nb == 0) return hipMemsetAsync(counts, 0, (nranks + 1) * 8, s);
-    k_route_own<<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist);
+    k_route_own<<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask);
     hipError_t e = scan_exclusive(HistF{hist, nb, nranks}, nb * nranks, off, scratch + 1,
                                   (unsigned long long*)nullptr, total, s);
     if (e != hipSuccess) return e;

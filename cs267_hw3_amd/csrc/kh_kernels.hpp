@@ -177,7 +177,7 @@ hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, 
 // hist/off: route_blocks(n) * nranks words each; counts: nranks + 1 words (last = n).
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
                         uint64_t* hist, uint64_t* off, uint64_t* scratch, uint8_t* own, uint64_t* out_words,
-                        uint64_t* counts, hipStream_t s);
+                        uint64_t* counts, hipStream_t s, uint64_t* start_mask = nullptr);
 
 // Insert routed internal words.
 hipError_t launch_insert_words(const KParams& p, const uint64_t* words, uint64_t m, TableView t,

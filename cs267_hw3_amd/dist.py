@@ -168,12 +168,15 @@ class GpuShard:
     def collect_starts(self, recs):
         check(self.L.kh_collect_starts_dev(self.h, self._p(recs), recs.shape[0]))
 
-    def route(self, recs, nranks, words=None):
+    def route(self, recs, nranks, words=None, starts=False):
+        """Records -> owner-grouped words (+ counts); starts=True also collects this block's
+        start k-mers in the same pass (kh_route_starts_dev)."""
         n = recs.shape[0]
         if words is None:
             words = self.zeros(n * self.W, torch.int64)
         counts = self.zeros(nranks + 1, torch.int64)
-        check(self.L.kh_route_dev(self.h, self._p(recs), n, nranks, self._p(words), self._p(counts)))
+        f = self.L.kh_route_starts_dev if starts else self.L.kh_route_dev
+        check(f(self.h, self._p(recs), n, nranks, self._p(words), self._p(counts)))
         return words, counts
 
     def insert_words(self, words, m):
@@ -409,7 +412,7 @@ class DistributedKmerHashMap:
         for c in range(nch):
             c0, c1 = bounds[c], bounds[c + 1]
             w = words[c0 * W:max(c1, c0 + 1) * W]
-            _, counts = sh.route(recs[c0:c1], P, w)
+            _, counts = sh.route(recs[c0:c1], P, w, starts=True)
             send = counts[:P].cpu()                       # waits for this chunk's route only
             mat = self.comm.all_gather_host(send)         # [src][dst]
             recv_splits = mat[:, rank].tolist()
@@ -434,11 +437,10 @@ class DistributedKmerHashMap:
 
     def insert_all(self, recs):
         sh, P = self.shard, self.P
-        sh.collect_starts(recs)
         if ((P > 1 or self.SELF_EXCHANGE) and getattr(self.comm, "ctrl", None) is not None
                 and self.INSERT_CHUNKS > 1 and recs.shape[0] >= self.PIPELINE_MIN):
             return self._insert_pipelined(recs)
-        words, counts = sh.route(recs, P)
+        words, counts = sh.route(recs, P, starts=True)  # + this block's starts, same pass
         send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
         W = sh.W
         m = sum(recv_splits)
@@ -681,11 +683,22 @@ def bench_main(args, w, world, rank):
     dm = DistributedKmerHashMap(comm, shard, protocol=protocol)
     R = record_size(k)
 
+    phase_log = os.environ.get("KH_BENCH_PHASES") == "1"
+
     def step():
         with torch.cuda.stream(shard.stream):
             shard.clear()
+            t0 = time.perf_counter()
             dm.insert_all(recs)
+            if phase_log:
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
             dm.assemble(n_total)
+            if phase_log:
+                torch.cuda.synchronize()
+                print(f"[rank {rank}] insert {1e3 * (t1 - t0):.2f} ms, assemble "
+                      f"{1e3 * (time.perf_counter() - t1):.2f} ms, rounds {dm.rounds}", file=sys.stderr,
+                      flush=True)
 
     for _ in range(args.warmup):
         step()
@@ -698,6 +711,7 @@ def bench_main(args, w, world, rank):
         torch.cuda.synchronize()
         dist.barrier()
         times.append(time.perf_counter() - t0)
+    print(f"[rank {rank}] step ms: " + " ".join(f"{1e3 * x:.2f}" for x in times), file=sys.stderr, flush=True)
     mine = sum(times) / len(times)
     tmax = comm.all_reduce_max(mine)
     st = shard.stats()

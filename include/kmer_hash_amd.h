@@ -121,6 +121,10 @@ int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n); /* loc
 int kh_pack_text_dev(kh_table* t, const void* dev_text, uint64_t len, void* dev_recs, uint64_t* n_out);
 int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
                  void* dev_counts_out);
+/* kh_collect_starts_dev + kh_route_dev in one streaming pass over the records (the start bits
+ * come from the route's owner pass); successive calls append starts in call order. */
+int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
+                        void* dev_counts_out);
 int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);
 /* Staged insert of routed words (one call per received all-to-all chunk, hash_map.hpp:55-80's
  * insert_all split so that partitioning overlaps the exchange): stage partitions m words toward

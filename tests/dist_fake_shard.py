@@ -55,7 +55,9 @@ class FakeShard:
             if r[self.P] == ord("F"):
                 self.starts.append(bytes(r))
 
-    def route(self, recs, nranks, words=None):
+    def route(self, recs, nranks, words=None, starts=False):
+        if starts:
+            self.collect_starts(recs)
         rows = [bytes(r) for r in recs.numpy()]
         payloads, _, counts = self._group([(self._owner(r[:self.P], nranks), r) for r in rows], nranks)
         enc = self._enc(payloads)
