@@ -80,14 +80,17 @@ uint64_t part_buf2_words(const KParams& p, uint64_t n) {
 // Pass-1 / pass-2 variants (KH_P1 = convert | rec, KH_P2 = scan | res); defaults below.
 // Pass-1 variant (KH_P1): 0 fused = k_part1_fused (windows + atomics, no histogram pass),
 // 1 convert = records -> words + histogram, then the exact scatter (words input: histogram +
-// scatter), 2 rec = histogram and scatter both parse the records. Defaults (C3, MI355X):
-// records -> convert (1.5 + 1.9 ms; fused parse 5.7 ms: the record stage in LDS leaves it
-// latency-bound at 2 blocks/CU); words -> fused.
+// scatter), 2 rec = histogram and scatter both parse the records, 3 direct = record parse from
+// registers inside the windowed pass, 4 convfused = records -> words (k_part1_convert without
+// its histogram) then the windowed pass on the words. Defaults (C3, MI355X): records ->
+// convfused (1.45 + 1.91 ms; convert 1.45 + scans 0.42 + scatter 2.09; fused/direct parse in
+// the sort kernel 5.5-5.7); words -> fused.
 static int p1_mode(bool rec) {
     const char* e = getenv("KH_P1");
-    if (!e || !*e) return rec ? 1 : 0;
+    if (!e || !*e) return rec ? 4 : 0;
     if (!strcmp(e, "fused")) return 0;
     if (!strcmp(e, "direct")) return 3;
+    if (!strcmp(e, "convfused")) return 4;
     return !strcmp(e, "rec") ? 2 : 1;
 }
 static bool p2_res() {
@@ -391,9 +394,10 @@ __global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* 
             } else {
                 words_out[i] = w0;
             }
-            atomicAdd(&h[hk >> (64 - B1)], 1u);
+            if (hist1) atomicAdd(&h[hk >> (64 - B1)], 1u);
         }
     }
+    if (!hist1) return;  // words only (the windowed pass 1 needs no histogram)
     __syncthreads();
     for (int i = threadIdx.x; i < NB1; i += PB) hist1[(uint64_t)blockIdx.x * NB1 + i] = h[i];
 }
@@ -568,7 +572,19 @@ __device__ __forceinline__ void parse_record_regs(uint64_t x0, uint64_t x1, cons
     ext = base_code((uint8_t)e) | (base_code((uint8_t)(e >> 8)) << 3);
 }
 
-template <int W>
+// same with the packed size PK known at compile time: constant shifts, no SALU per record
+template <int PK>
+__device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, int pad, Key& k, uint32_t& ext) {
+    const unsigned __int128 be = ((unsigned __int128)__builtin_bswap64(x0) << 64) | __builtin_bswap64(x1);
+    const unsigned __int128 B = (be >> (8 * (16 - PK))) >> (2 * pad);
+    k.lo = (uint64_t)B & LO_MASK;
+    k.hi = (uint64_t)(B >> 62);
+    const unsigned __int128 xx = ((unsigned __int128)x1 << 64) | x0;
+    const uint32_t e = (uint32_t)(xx >> (8 * PK)) & 0xFFFFu;
+    ext = base_code((uint8_t)e) | (base_code((uint8_t)(e >> 8)) << 3);
+}
+
+template <int W, int PK = 0>
 __global__ __launch_bounds__(PB) void k_part1_direct(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
                                                      uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1,
                                                      uint64_t* start_mask, uint64_t* split_mask,
@@ -592,7 +608,7 @@ __global__ __launch_bounds__(PB) void k_part1_direct(KParams p, const uint8_t* _
         for (int j = 0; j < PITEMS; ++j) {
             const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
             x0[j] = x1[j] = 0;
-            if (i < n) load_record_regs(recs, i, R, x0[j], x1[j]);
+            if (i < n) load_record_regs(recs, i, PK ? (uint32_t)(PK + 2) : R, x0[j], x1[j]);
         }
 #pragma unroll
         for (int j = 0; j < PITEMS; ++j) {
@@ -601,7 +617,12 @@ __global__ __launch_bounds__(PB) void k_part1_direct(KParams p, const uint8_t* _
             const bool valid = i < n;
             Key k{0, 0};
             uint32_t ext = 0;
-            if (valid) parse_record_regs(x0[j], x1[j], p, k, ext);
+            if (valid) {
+                if (PK)
+                    parse_record_regs_t<PK>(x0[j], x1[j], p.pad, k, ext);
+                else
+                    parse_record_regs(x0[j], x1[j], p, k, ext);
+            }
             const uint64_t hk = key_hash(k);
             if (s0 < n) {  // uniform
                 const bool is_start = valid && ext_bwd(ext) == EXT_F;
@@ -1026,6 +1047,111 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
     }
 }
 
+// Build from fixed region windows with the next region's words prefetched: each thread holds up
+// to IPT words of the region it inserts and issues the loads of its words of the next region
+// before the LDS inserts and the slice write-out, and region hand-offs use LDS-only barriers,
+// so a block's window loads, LDS work and slice stores overlap.
+template <int W, int IPT>
+__global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p, const uint64_t* __restrict__ buf2,
+                                                                 uint64_t* slots, uint64_t cap, int table_empty,
+                                                                 uint64_t* ovf, uint64_t ovf_cap,
+                                                                 unsigned long long* ctr,
+                                                                 unsigned long long* stats, uint32_t RC,
+                                                                 const uint32_t* __restrict__ rcnt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
+    uint64_t a[IPT], b[IPT];
+    auto load = [&](uint32_t r, uint64_t (&x)[IPT], uint64_t (&y)[IPT]) {
+        const uint32_t m = r < NREG ? min(rcnt[r], RC) : 0u;
+        const uint64_t base = (uint64_t)(r < NREG ? r : 0) * RC;
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint32_t i = threadIdx.x + (uint32_t)j * BUILD_THREADS;
+            const uint64_t g = base + (i < m ? i : 0);
+            uint64_t v0, v1 = 0;
+            if (W == 2) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(buf2 + g * 2);
+                v0 = v.x;
+                v1 = v.y;
+            } else {
+                v0 = buf2[g];
+            }
+            x[j] = i < m ? v0 : EMPTY;
+            y[j] = v1;
+        }
+    };
+    uint32_t r = blockIdx.x;
+    load(r, a, b);
+    for (; r < NREG; r += gridDim.x) {
+        const uint64_t lo = mulhi64((uint64_t)r << (64 - RBITS), cap);
+        const uint64_t hi = (r + 1 < NREG) ? mulhi64((uint64_t)(r + 1) << (64 - RBITS), cap) : cap;
+        const uint32_t S = (uint32_t)(hi - lo);
+        if (W == 2) {
+            ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
+            const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
+                l2[i] = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
+                lt[i] = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
+        }
+        if (table_empty)
+            lds_barrier();
+        else
+            __syncthreads();
+        uint64_t na[IPT], nb[IPT];
+        load(r + gridDim.x, na, nb);  // next region's words in flight during this one
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            if (a[j] == EMPTY) continue;
+            const uint64_t home = home_slot(words_hash<W>(a[j], b[j], p), cap);
+            if (!lds_insert<W>(lt, S, home - lo, a[j], b[j], stats)) {
+                const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
+                if (idx < ovf_cap) {
+                    ovf[idx * W] = a[j];
+                    if (W == 2) ovf[idx * W + 1] = b[j];
+                } else {
+                    atomicAdd(&stats[ST_FULL], 1ull);
+                }
+            }
+        }
+        lds_barrier();
+        if (W == 2) {
+            ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
+            const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) dst[i] = l2[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) slots[lo + i] = lt[i];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            a[j] = na[j];
+            b[j] = nb[j];
+        }
+    }
+}
+
+// Region-window build: the prefetching kernel when a window fits IPT words per thread.
+template <int W>
+static void launch_build_windows(const KParams& p, const PartBuffers& B, uint64_t n, uint64_t G, TableView t,
+                                 bool table_empty, uint64_t ovf_cap, unsigned long long* ctr,
+                                 unsigned long long* stats, uint32_t RC, const uint32_t* rcnt, size_t lds,
+                                 hipStream_t s) {
+    const char* e = getenv("KH_BUILD");
+    const bool pf = !(e && !strcmp(e, "plain"));
+    if (pf && RC <= 4u * BUILD_THREADS) {
+        k_part_build_pf<W, 4><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, table_empty ? 1 : 0,
+                                                               B.overflow, ovf_cap, ctr, stats, RC, rcnt);
+    } else if (pf && RC <= 12u * BUILD_THREADS) {
+        k_part_build_pf<W, 12><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, table_empty ? 1 : 0,
+                                                                B.overflow, ovf_cap, ctr, stats, RC, rcnt);
+    } else {
+        k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, n, B.off2, G, t.slots, t.cap,
+                                                         table_empty ? 1 : 0, B.overflow, ovf_cap, ctr, stats, RC,
+                                                         rcnt);
+    }
+}
+
 template <int W>
 __global__ __launch_bounds__(PB) void k_insert_overflow(KParams p, const uint64_t* ovf, uint64_t ovf_cap,
                                                         const unsigned long long* ctr, uint64_t* slots,
@@ -1058,15 +1184,24 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         if ((e = allow_lds(k_part1_fused<W, true>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_part1_fused<W, false>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_part1_direct<W>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_part1_direct<W, 13>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_part1_direct<W, 5>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_part_build<W>, LDS_BYTES)) != hipSuccess) return e;
+        if ((e = allow_lds(k_part_build_pf<W, 4>, LDS_BYTES)) != hipSuccess) return e;
+        if ((e = allow_lds(k_part_build_pf<W, 12>, LDS_BYTES)) != hipSuccess) return e;
         attrs = true;
     }
     const PartPlan pl = part_plan(n);
     const unsigned nb1 = (unsigned)pl.nb1;
     int mode1 = p1_mode(REC);
     if (mode1 == 3 && (!REC || p.R > 16)) mode1 = REC ? 1 : 0;  // direct parse: records of <= 16 B
+    if (mode1 == 4 && !REC) mode1 = 0;
     const bool direct1 = mode1 == 3;
-    const bool fused1 = mode1 == 0 || direct1, rec1 = REC && mode1 == 2;
+    if (mode1 == 4) {  // records -> words (input order) in buf2, then the windowed pass 1 on them
+        k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, nullptr, start_mask, split_mask);
+        words = B.buf2;
+    }
+    const bool fused1 = mode1 == 0 || direct1 || mode1 == 4, rec1 = REC && mode1 == 2;
     const bool res2 = fused1 || p2_res();
     if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
     uint32_t CAP1 = 0;
@@ -1074,9 +1209,22 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (fused1) {
         CAP1 = part_win1_cap(n);
         if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
-        if (direct1)
+        if (direct1 && p.P == 13 && W == 2 && !getenv("KH_NOMASK"))
+            k_part1_direct<W, 13><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask,
+                                                           B.overflow, part_overflow_cap(n), ctr, stats);
+        else if (direct1 && p.P == 5 && W == 1)
+            k_part1_direct<W, 5><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask,
+                                                          B.overflow, part_overflow_cap(n), ctr, stats);
+        else if (direct1 && getenv("KH_NOMASK"))
+            k_part1_direct<W, 13><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, nullptr, nullptr,
+                                                           B.overflow, part_overflow_cap(n), ctr, stats);
+        else if (direct1)
             k_part1_direct<W><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask,
                                                        B.overflow, part_overflow_cap(n), ctr, stats);
+        else if (mode1 == 4)
+            k_part1_fused<W, false><<<nb1, PB, SORT_LDS, s>>>(p, nullptr, words, n, CAP1, wcnt, B.buf1, nullptr,
+                                                               nullptr, B.overflow, part_overflow_cap(n), ctr,
+                                                               stats);
         else
             k_part1_fused<W, REC><<<nb1, PB, SORT_LDS, s>>>(p, recs, words, n, CAP1, wcnt, B.buf1, start_mask,
                                                              split_mask, B.overflow, part_overflow_cap(n), ctr,
@@ -1124,9 +1272,12 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         k_part2_scatter<W><<<nb2, PB, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.nb1, pl.G, B.off2, B.buf2);
     }
     const size_t lds = (size_t)region_max_slots(t.cap) * W * 8;
-    k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, n, B.off2, pl.G, t.slots, t.cap,
-                                                     table_empty ? 1 : 0, B.overflow,
-                                                     part_overflow_cap(n), ctr, stats, RC, rcnt);
+    if (RC)
+        launch_build_windows<W>(p, B, n, pl.G, t, table_empty, part_overflow_cap(n), ctr, stats, RC, rcnt, lds, s);
+    else
+        k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, n, B.off2, pl.G, t.slots, t.cap,
+                                                         table_empty ? 1 : 0, B.overflow,
+                                                         part_overflow_cap(n), ctr, stats, RC, rcnt);
     k_insert_overflow<W><<<1024, PB, 0, s>>>(p, B.overflow, part_overflow_cap(n), ctr, t.slots, t.cap,
                                              stats);
     return hipGetLastError();
@@ -1166,12 +1317,12 @@ static hipError_t part_finish(const KParams& p, uint64_t total, TableView t, boo
                               unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
     hipError_t e;
     if ((e = allow_lds(k_part_build<W>, LDS_BYTES)) != hipSuccess) return e;
+    if ((e = allow_lds(k_part_build_pf<W, 4>, LDS_BYTES)) != hipSuccess) return e;
+    if ((e = allow_lds(k_part_build_pf<W, 12>, LDS_BYTES)) != hipSuccess) return e;
     const uint32_t RC = part_region_cap(total);
     const uint32_t* rcnt = reinterpret_cast<const uint32_t*>(B.hist2);
     const size_t lds = (size_t)region_max_slots(t.cap) * W * 8;
-    k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, total, B.off2, 1, t.slots, t.cap,
-                                                     table_empty ? 1 : 0, B.overflow, part_overflow_cap(total),
-                                                     ctr, stats, RC, rcnt);
+    launch_build_windows<W>(p, B, total, 1, t, table_empty, part_overflow_cap(total), ctr, stats, RC, rcnt, lds, s);
     k_insert_overflow<W><<<1024, PB, 0, s>>>(p, B.overflow, part_overflow_cap(total), ctr, t.slots, t.cap, stats);
     return hipGetLastError();
 }

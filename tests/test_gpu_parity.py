@@ -368,8 +368,8 @@ def test_gpu_walk_group_missing_kmer(monkeypatch, G):
 
 # ---- partitioned-build pass variants (KH_P1: record re-parse / word copy; KH_P2: region windows
 # with atomic reservations / histogram + scan) ----------------------------------------------------
-@pytest.mark.parametrize("p1,p2", [("direct", "res"), ("fused", "res"), ("rec", "res"), ("convert", "res"),
-                                   ("rec", "scan"), ("convert", "scan")])
+@pytest.mark.parametrize("p1,p2", [("convfused", "res"), ("direct", "res"), ("fused", "res"), ("rec", "res"),
+                                   ("convert", "res"), ("rec", "scan"), ("convert", "scan")])
 @pytest.mark.parametrize("k,n,batches", [(51, 3_000_000, 1), (60, 2_000_000, 2), (19, 2_000_000, 1),
                                          (29, 1_500_000, 1)])
 def test_gpu_part_pass_variants(monkeypatch, p1, p2, k, n, batches):
@@ -396,3 +396,17 @@ def test_gpu_part_pass_variants_duplicates(monkeypatch, p1, p2):
         t.insert_all(dup)
     assert e.value.code == _lib.KH_ERR_DUPLICATE
     assert t.stats()["n_dup"] == 1000
+
+
+@pytest.mark.parametrize("build", ["plain", "pf"])
+@pytest.mark.parametrize("k,n,load", [(51, 3_000_000, 0.5), (19, 2_000_000, 0.5), (31, 1_500_000, 0.9),
+                                      (51, 12_000_000, 0.3)])
+def test_gpu_build_kernels(monkeypatch, build, k, n, load):
+    """Region-window build, plain and prefetching (4 and 12 words per thread), == ground truth."""
+    monkeypatch.setenv("KH_INSERT", "part")
+    monkeypatch.setenv("KH_BUILD", build)
+    g = kh.SyntheticKmers(k, n, 8, 300, 10, seed=k * 5 + n % 7)
+    t, got, nc = run(k, g.records(), load=load)
+    assert got == g.truth() and nc == g.num_contigs
+    s = t.stats()
+    assert s["n_dup"] == 0 and s["n_full"] == 0

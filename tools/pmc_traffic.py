@@ -19,7 +19,7 @@ KERNELS = {"k_insert": ("k_insert<",), "k_walk": ("k_walk<", "k_walk_g<"),
            "k_part1_convert": ("k_part1_convert<",), "k_part1_fused": ("k_part1_fused<",),
            "k_part1_scatter": ("k_part1_scatter<",), "k_part2_hist": ("k_part2_hist<",),
            "k_part2_scatter": ("k_part2_scatter<",), "k_part2_res": ("k_part2_res<",),
-           "k_part_build": ("k_part_build<",), "k_insert_overflow": ("k_insert_overflow<",),
+           "k_part_build": ("k_part_build<", "k_part_build_pf<"), "k_insert_overflow": ("k_insert_overflow<",),
            "membench_gather16": ("k_gather16",), "membench_chase16": ("k_chase16",),
            "membench_chase64q": ("k_chasegILi4",), "membench_chase128o": ("k_chasegILi8",)}
 # kernels of the insert pipeline (whichever of them ran)
