@@ -1163,6 +1163,232 @@ __global__ __launch_bounds__(PB) void k_insert_overflow(KParams p, const uint64_
     }
 }
 
+// ---- windowed passes with a template block size --------------------------------------------
+// The two LDS-sorted passes hold a 4096-word tile (64 KB + 8 KB of bin ids) per block, so LDS caps
+// them at 2 blocks per CU; with TB = 512 threads per block that is 16 waves per CU instead of 8
+// (half the items per thread), for the same tile and run lengths.
+template <int TB>
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t& total, uint32_t* wsum) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    lds_barrier();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < TB / 64; ++i) {
+        const uint32_t s = wsum[i];
+        pre += i < w ? s : 0u;
+        tot += s;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
+template <int W, int TB>
+__device__ __forceinline__ void load_words_tb(const uint64_t* __restrict__ words, uint64_t base, uint64_t end,
+                                              uint64_t last, uint64_t* a, uint64_t* b) {
+    constexpr int IPT = PART_TILE / TB;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * TB + threadIdx.x;
+        const uint64_t ii = i < end ? i : last;
+        uint64_t x0, x1 = 0;
+        if (W == 2) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(words + 2 * ii);
+            x0 = v.x;
+            x1 = v.y;
+        } else {
+            x0 = words[ii];
+        }
+        a[j] = i < end ? x0 : EMPTY;
+        b[j] = i < end ? x1 : 0;
+    }
+}
+
+template <int W, int TB>
+__device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ buf1, uint32_t bk, uint32_t CAP1,
+                                                  const uint32_t* pre, uint64_t base, uint64_t end, uint64_t* a,
+                                                  uint64_t* b) {
+    constexpr int IPT = PART_TILE / TB;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint32_t v = (uint32_t)(base + (uint64_t)j * TB + threadIdx.x);
+        const bool ok = v < (uint32_t)end;
+        uint32_t w = 0, pw = 0;
+#pragma unroll
+        for (uint32_t q = 1; q < S1; ++q)
+            if (v >= pre[q]) {
+                w = q;
+                pw = pre[q];
+            }
+        const uint64_t i = ok ? (uint64_t)(bk * S1 + w) * CAP1 + (v - pw) : (uint64_t)bk * S1 * CAP1;
+        uint64_t x0, x1 = 0;
+        if (W == 2) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(buf1 + 2 * i);
+            x0 = x.x;
+            x1 = x.y;
+        } else {
+            x0 = buf1[i];
+        }
+        a[j] = ok ? x0 : EMPTY;
+        b[j] = ok ? x1 : 0;
+    }
+}
+
+// Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
+// with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
+// out[window(bin) + reserved + rank] (positions past cap -> overflow list).
+template <int W, int TB, int NB, class CtrF, class WinF, class NextF>
+__device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, const uint32_t* bin, uint64_t* items,
+                                                   uint16_t* sbin, uint32_t* hist, uint32_t* start, uint32_t* gpos,
+                                                   uint32_t* wsum, CtrF counter, WinF window, uint32_t cap,
+                                                   uint64_t* out, uint64_t* ovf, uint64_t ovf_cap,
+                                                   unsigned long long* ctr, unsigned long long* stats, NextF next) {
+    constexpr int IPT = PART_TILE / TB;
+    static_assert(NB <= TB, "one bin per thread");
+    if (threadIdx.x < NB) hist[threadIdx.x] = 0;
+    lds_barrier();
+    uint32_t rank[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
+    lds_barrier();
+    const uint32_t hv = threadIdx.x < NB ? hist[threadIdx.x] : 0u;
+    uint32_t total;
+    const uint32_t st = block_scan_u32<TB>(hv, total, wsum);
+    if (threadIdx.x < NB) {
+        start[threadIdx.x] = st;
+        gpos[threadIdx.x] = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (a[j] != EMPTY) {
+            const uint32_t pos = start[bin[j]] + rank[j];
+            items[pos * W] = a[j];
+            if (W == 2) items[pos * W + 1] = b[j];
+            sbin[pos] = (uint16_t)bin[j];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    next();  // the next tile's loads are in flight while this one is written
+    lds_barrier();
+#pragma unroll 4
+    for (uint32_t x = threadIdx.x; x < total; x += TB) {
+        const uint32_t q = sbin[x];
+        const uint32_t w = gpos[q] + (x - start[q]);
+        const uint64_t v0 = items[W * x], v1 = (W == 2) ? items[W * x + 1] : 0;
+        if (w < cap) {
+            const uint64_t g = window(q) + w;
+            if (W == 2) {
+                *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(v0, v1);
+            } else {
+                out[g] = v0;
+            }
+        } else {
+            const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
+            if (idx < ovf_cap) {
+                ovf[idx * W] = v0;
+                if (W == 2) ovf[idx * W + 1] = v1;
+            } else {
+                atomicAdd(&stats[ST_FULL], 1ull);
+            }
+        }
+    }
+    lds_barrier();
+}
+
+// pass 1 on words: bucket = top 9 hash bits, S1 windows per bucket (window blockIdx % S1)
+template <int W, int TB>
+__global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restrict__ words, uint64_t n,
+                                             uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1, uint64_t* ovf,
+                                             uint64_t ovf_cap, unsigned long long* ctr,
+                                             unsigned long long* stats) {
+    constexpr int IPT = PART_TILE / TB;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* items = smem;
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + PART_TILE * 2);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);
+    uint32_t* start = hist + NB1;
+    uint32_t* gpos = start + NB1;
+    __shared__ uint32_t wsum[TB / 64];
+    const uint32_t sub = blockIdx.x % S1;
+    const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
+    uint64_t a[IPT], b[IPT];
+    load_words_tb<W, TB>(words, b0, min(b0 + PART_TILE, n), b0 < n ? b0 : 0, a, b);
+    for (int tt = 0; tt < T1; ++tt) {
+        const uint64_t base = b0 + (uint64_t)tt * PART_TILE;
+        if (base >= n) break;  // uniform
+        uint32_t bin[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - B1));
+        const uint64_t nbase = base + PART_TILE;
+        sort_reserve_write<W, TB, NB1>(
+            a, b, bin, items, sbin, hist, start, gpos, wsum,
+            [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
+            [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
+            [&]() { load_words_tb<W, TB>(words, nbase, (tt + 1 < T1) ? min(nbase + PART_TILE, n) : nbase, base, a, b); });
+    }
+}
+
+// pass 2: next 8 hash bits within bucket bk, into the region windows (RC words each)
+template <int W, int TB, bool WIN>
+__global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restrict__ buf1, uint64_t n,
+                                             const uint64_t* off1, uint64_t G, uint32_t RC, uint32_t* rcnt,
+                                             uint64_t* buf2, uint64_t* ovf, uint64_t ovf_cap,
+                                             unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
+                                             const uint32_t* wcnt) {
+    constexpr int IPT = PART_TILE / TB;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* items = smem;
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + PART_TILE * 2);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);
+    uint32_t* start = hist + NB1;
+    uint32_t* gpos = start + NB1;
+    __shared__ uint32_t wsum[TB / 64];
+    const uint32_t bk = blockIdx.x / (uint32_t)G, g = blockIdx.x % (uint32_t)G;
+    uint64_t s, e;
+    uint32_t pre[S1 + 1];
+    if (WIN) {
+        pre[0] = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < S1; ++j) pre[j + 1] = pre[j] + min(wcnt[bk * S1 + j], CAP1);
+        s = 0;
+        e = pre[S1];
+    } else {
+        bucket_range(off1, 0, n, bk, s, e);
+    }
+    uint64_t a[IPT], b[IPT];
+    auto load = [&](uint64_t t) {
+        const uint64_t e_ = t < e ? min(t + PART_TILE, e) : t;
+        if (WIN)
+            load_words_win_tb<W, TB>(buf1, bk, CAP1, pre, t, e_, a, b);
+        else
+            load_words_tb<W, TB>(buf1, t, e_, s, a, b);
+    };
+    load(s + (uint64_t)g * PART_TILE);
+    for (uint64_t t = s + (uint64_t)g * PART_TILE; t < e; t += G * PART_TILE) {
+        uint32_t bin[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - RBITS)) & (NB2 - 1);
+        sort_reserve_write<W, TB, NB2>(
+            a, b, bin, items, sbin, hist, start, gpos, wsum,
+            [&](uint32_t q) { return &rcnt[(bk << B2) | q]; },
+            [&](uint32_t q) { return (uint64_t)((bk << B2) | q) * RC; }, RC, buf2, ovf, ovf_cap, ctr, stats,
+            [&]() { load(t + G * PART_TILE); });
+    }
+}
+
+static int win_tb() {
+    const char* e = getenv("KH_TB");
+    return (e && *e) ? atoi(e) : 512;
+}
+
 template <class K>
 static hipError_t allow_lds(K kernel, size_t bytes) {
     return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -1189,6 +1415,9 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         if ((e = allow_lds(k_part_build<W>, LDS_BYTES)) != hipSuccess) return e;
         if ((e = allow_lds(k_part_build_pf<W, 4>, LDS_BYTES)) != hipSuccess) return e;
         if ((e = allow_lds(k_part_build_pf<W, 12>, LDS_BYTES)) != hipSuccess) return e;
+        if ((e = allow_lds(k_win1<W, 512>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_win2<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_win2<W, 512, false>, SORT_LDS)) != hipSuccess) return e;
         attrs = true;
     }
     const PartPlan pl = part_plan(n);
@@ -1221,6 +1450,9 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         else if (direct1)
             k_part1_direct<W><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask,
                                                        B.overflow, part_overflow_cap(n), ctr, stats);
+        else if ((mode1 == 4 || (mode1 == 0 && !REC)) && win_tb() == 512)
+            k_win1<W, 512><<<nb1, 512, SORT_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
+                                                      part_overflow_cap(n), ctr, stats);
         else if (mode1 == 4)
             k_part1_fused<W, false><<<nb1, PB, SORT_LDS, s>>>(p, nullptr, words, n, CAP1, wcnt, B.buf1, nullptr,
                                                                nullptr, B.overflow, part_overflow_cap(n), ctr,
@@ -1255,7 +1487,15 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (res2) {
         RC = part_region_cap(n);
         if ((e = hipMemsetAsync(rcnt, 0, (size_t)NREG * 4, s)) != hipSuccess) return e;
-        if (CAP1)
+        if (win_tb() == 512 && CAP1)
+            k_win2<W, 512, true><<<nb2, 512, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.G, RC, rcnt, B.buf2,
+                                                           B.overflow, part_overflow_cap(n), ctr, stats, CAP1,
+                                                           wcnt);
+        else if (win_tb() == 512)
+            k_win2<W, 512, false><<<nb2, 512, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.G, RC, rcnt, B.buf2,
+                                                            B.overflow, part_overflow_cap(n), ctr, stats, 0,
+                                                            nullptr);
+        else if (CAP1)
             k_part2_res<W, true><<<nb2, PB, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.G, RC, rcnt, B.buf2,
                                                           B.overflow, part_overflow_cap(n), ctr, stats, CAP1,
                                                           wcnt);
@@ -1283,6 +1523,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     return hipGetLastError();
 }
 
+
 // Staged build (sharded insert): words arrive in chunks (one per all-to-all chunk). Each chunk is
 // partitioned at once (pass 1 into its own windows, pass 2 appending to the region windows of a
 // build sized for `total` words) while the next chunk is still on the wire; one build at the end.
@@ -1293,6 +1534,8 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     hipError_t e;
     if ((e = allow_lds(k_part1_fused<W, false>, SORT_LDS)) != hipSuccess) return e;
     if ((e = allow_lds(k_part2_res<W, true>, SORT_LDS)) != hipSuccess) return e;
+    if ((e = allow_lds(k_win1<W, 512>, SORT_LDS)) != hipSuccess) return e;
+    if ((e = allow_lds(k_win2<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(B.hist1);
     uint32_t* rcnt = reinterpret_cast<uint32_t*>(B.hist2);
     if (first) {
@@ -1303,6 +1546,15 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     const PartPlan pl = part_plan(m);
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(total);
     if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
+    if (win_tb() == 512) {
+        k_win1<W, 512><<<(unsigned)pl.nb1, 512, SORT_LDS, s>>>(p, words, m, CAP1, wcnt, B.buf1, B.overflow,
+                                                               part_overflow_cap(total), ctr, stats);
+        k_win2<W, 512, true><<<(unsigned)(NB1 * pl.G), 512, SORT_LDS, s>>>(p, B.buf1, m, B.off1, pl.G, RC, rcnt,
+                                                                           B.buf2, B.overflow,
+                                                                           part_overflow_cap(total), ctr, stats,
+                                                                           CAP1, wcnt);
+        return hipGetLastError();
+    }
     k_part1_fused<W, false><<<(unsigned)pl.nb1, PB, SORT_LDS, s>>>(p, nullptr, words, m, CAP1, wcnt, B.buf1,
                                                                   nullptr, nullptr, B.overflow,
                                                                   part_overflow_cap(total), ctr, stats);

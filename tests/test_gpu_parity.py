@@ -410,3 +410,16 @@ def test_gpu_build_kernels(monkeypatch, build, k, n, load):
     assert got == g.truth() and nc == g.num_contigs
     s = t.stats()
     assert s["n_dup"] == 0 and s["n_full"] == 0
+
+
+@pytest.mark.parametrize("tb", ["256", "512"])
+@pytest.mark.parametrize("k,n,batches", [(51, 3_000_000, 1), (19, 2_000_000, 2), (60, 1_500_000, 1)])
+def test_gpu_windowed_pass_block_sizes(monkeypatch, tb, k, n, batches):
+    """Windowed passes at 256 (k_part1_fused / k_part2_res) and 512 threads (k_win1 / k_win2)."""
+    monkeypatch.setenv("KH_INSERT", "part")
+    monkeypatch.setenv("KH_TB", tb)
+    g = kh.SyntheticKmers(k, n, 8, 300, 10, seed=k * 11 + batches)
+    t, got, nc = run(k, g.records(), batches=batches)
+    assert got == g.truth() and nc == g.num_contigs
+    s = t.stats()
+    assert s["n_dup"] == 0 and s["n_full"] == 0 and s["n_inserted"] == n
