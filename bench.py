@@ -171,6 +171,10 @@ def main():
                    "ms": ins_ms, "achieved_alg_GBs": n * b_alg / (ins_ms / 1e3) / 1e9,
                    "inserts_per_s": n / (ins_ms / 1e3),
                    "traffic": traffic.get("insert_pipeline") if traffic else None}
+    if insert_pipe["traffic"]:
+        # PMC-measured HBM bytes of the pipeline's kernels / their HIP-event time, against peak
+        insert_pipe["traffic_GBs"] = insert_pipe["traffic"] / (ins_ms / 1e3) / 1e9
+        insert_pipe["traffic_frac"] = insert_pipe["traffic_GBs"] / HBM_PEAK_GBS
     cpu = None
     if args.cpu_sample:
         t = time.time()
