@@ -28,6 +28,13 @@ WORKLOADS = {
     "c2": dict(k=19, n=10_000_000, len_min=200, len_max=1374, single=0, seed=19,
                desc="C2: k=19, 10M synthetic k-mers per GPU, contigs U[200,1374] k-mers "
                     "(test.txt-like mean 787), table load 0.5"),
+    # BASELINE.json configs[4]: skewed set, 8 chains of 10^6 k-mers among
+    # short contigs U[2,16], every start k-mer first in record order (the block split hands all
+    # walkers to the first rank)
+    "c5": dict(k=51, n=200_000_000, len_min=2, len_max=16, single=0, seed=5199,
+               gen=dict(n_long=8, long_len=1_000_000, front_starts=True),
+               desc="C5: k=51, 200M synthetic k-mers per GPU, 8 chains of 10^6 k-mers + contigs "
+                    "U[2,16], start k-mers first in record order, table load 0.5"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 BEST_PUBLISHED_OPS = 72.6e6    # k=51, 4 nodes x 128 ranks (512 CPU ranks)
@@ -44,7 +51,7 @@ def cpu_baseline(w, sample_n):
     import oracle_bind as ob
     import cs267_hw3_amd as kh
     g = kh.SyntheticKmers(w["k"], sample_n, w["len_min"], w["len_max"], w["single"],
-                          seed=w["seed"])
+                          seed=w["seed"], **w.get("gen", {}))
     recs = g.records()
     rc, text, nc, nl, ti, tw = ob.assemble(w["k"], recs)
     if rc != 0:
@@ -108,7 +115,7 @@ def main():
 
     k, n = w["k"], w["n"]
     t = time.time()
-    g = kh.SyntheticKmers(k, n, w["len_min"], w["len_max"], w["single"], seed=w["seed"])
+    g = kh.SyntheticKmers(k, n, w["len_min"], w["len_max"], w["single"], seed=w["seed"], **w.get("gen", {}))
     host = g.records()
     log(f"generated {n} records ({host.nbytes / 1e9:.2f} GB) in {time.time() - t:.1f}s")
     L = kh._lib.lib()

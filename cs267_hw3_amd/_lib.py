@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkmerhash_amd.so")
+LIB_PATH = os.environ.get("KH_LIB") or os.path.join(_HERE, "libkmerhash_amd.so")  # KH_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kmer_hash_amd.h")
 
 KH_OK = 0
@@ -101,6 +101,9 @@ _SIGS = {
     "kh_gen_create": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_int, c_u64, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_uint32, c_u64, ctypes.c_int,
                                      ctypes.c_int]),
+    "kh_gen_create_skewed": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_int, c_u64, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, c_u64, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]),
     "kh_gen_destroy": (ctypes.c_int, [c_vp]),
     "kh_gen_num_contigs": (c_u64, [c_vp]),
     "kh_gen_records": (ctypes.c_int, [c_vp, c_u64, c_u64, c_vp]),

@@ -470,11 +470,13 @@ int kh_assemble_dev(kh_table* t) {
     else
         kp.split_bits = 0;
     // Walk density: enough segments for ~1M walkers in all (few, long contigs: C2, C5) but at
-    // least 1 splitter per 4096 k-mers so that no single chain dominates the critical path.
+    // least 1 splitter per 256 k-mers, so that no single chain dominates the critical path (the
+    // longest segment bounds the walk: C5 with 10^6-k-mer chains took 64 ms at 1 per 4096, with
+    // geometric segment lengths up to ~10x their mean; C3 pays +0.2 ms for the extra segments).
     const uint64_t* splits = t->splits.as<uint64_t>();
     if (kp.split_bits && !getenv("KH_SPLIT_BITS")) {
         const uint64_t want = ns < (1ull << 20) ? (1ull << 20) - ns : 0;
-        const uint64_t floor_cnt = t->n_inserted >> 12;
+        const uint64_t floor_cnt = t->n_inserted >> 8;
         const uint64_t d = want > floor_cnt ? want : floor_cnt;
         int bw = kp.split_bits;
         while (bw < 12 && d && (t->n_inserted >> (bw + 1)) >= d) ++bw;

@@ -148,7 +148,12 @@ KH_HD uint64_t fmix64(uint64_t h) {
 // every key of a high-bit shard split on one GPU; SURVEY §7 hard part 1). Placement never changes
 // the output, only where a key lives.
 KH_HD uint64_t key_hash(Key k) {
+#ifdef KH_CHEAP_HASH  // experiment only
+    uint64_t h = (k.lo ^ (k.hi << 17)) * 0xff51afd7ed558ccdull;
+    return h ^ (h >> 31);
+#else
     return fmix64(k.lo ^ fmix64(k.hi ^ 0x9e3779b97f4a7c15ull));
+#endif
 }
 
 KH_HD uint64_t mulhi64(uint64_t a, uint64_t b) {

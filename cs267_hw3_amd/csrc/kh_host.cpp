@@ -205,8 +205,27 @@ struct kh_gen {
         const uint32_t fwd = (t + 1 == len[i]) ? kh::EXT_F : base(i, t + K);
         ext = bwd | (fwd << 3);
     }
-    uint64_t pos_of(uint64_t g) const { return shuffle ? perm.fwd(g) : g; }
-    uint64_t g_of(uint64_t p) const { return shuffle ? perm.inv(p) : p; }
+    // C5 record order (front_starts): every start k-mer (t = 0) before every other k-mer, each
+    // group in its own seeded shuffle; nb[i] = off[i] - i = non-start k-mers before contig i.
+    bool front_starts = false;
+    Perm perm_s, perm_n;
+    std::vector<uint64_t> nb;
+    uint64_t pos_of(uint64_t g) const {
+        if (!front_starts) return shuffle ? perm.fwd(g) : g;
+        const uint64_t i = (uint64_t)(std::upper_bound(off.begin(), off.end(), g) - off.begin()) - 1;
+        const uint64_t C = len.size();
+        if (g == off[i]) return shuffle ? perm_s.fwd(i) : i;
+        const uint64_t q = g - i - 1;
+        return C + (shuffle ? perm_n.fwd(q) : q);
+    }
+    uint64_t g_of(uint64_t p) const {
+        if (!front_starts) return shuffle ? perm.inv(p) : p;
+        const uint64_t C = len.size();
+        if (p < C) return off[shuffle ? perm_s.inv(p) : p];
+        const uint64_t q = shuffle ? perm_n.inv(p - C) : p - C;
+        const uint64_t i = (uint64_t)(std::upper_bound(nb.begin(), nb.end(), q) - nb.begin()) - 1;
+        return off[i] + 1 + (q - nb[i]);
+    }
 };
 
 namespace {
@@ -249,6 +268,12 @@ extern "C" {
 
 int kh_gen_create(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
                   uint32_t single_permille, uint64_t seed, int shuffle, int threads) {
+    return kh_gen_create_skewed(out, k, n, len_min, len_max, single_permille, seed, shuffle, threads, 0, 0, 0);
+}
+
+int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
+                         uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
+                         uint32_t long_len, int front_starts) {
     if (!out) return hfail(KH_ERR_ARG, "out is NULL");
     *out = nullptr;
     if (k < 1 || k > KH_K_MAX || len_min < 1 || len_max < len_min || single_permille > 1000)
@@ -261,12 +286,14 @@ int kh_gen_create(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t le
     g->seed = seed;
     g->shuffle = shuffle != 0;
     g->threads = pick_threads(threads);
-    // 1) contig lengths until n k-mers (last one truncated)
+    // 1) contig lengths until n k-mers (last one truncated); the first n_long contigs have
+    //    long_len k-mers (C5: a handful of 10^6-k-mer chains among short contigs)
     uint64_t sum = 0;
     const uint64_t span = (uint64_t)len_max - len_min + 1;
     for (uint64_t i = 0; sum < n; ++i) {
         const uint64_t u = splitmix(seed * 0x2545f4914f6cdd1dull + i + 1);
         uint64_t L = ((u % 1000) < single_permille) ? 1 : len_min + (u >> 10) % span;
+        if (i < n_long && long_len) L = long_len;
         if (L > n - sum) L = n - sum;
         g->len.push_back((uint32_t)L);
         g->off.push_back(sum);
@@ -275,6 +302,14 @@ int kh_gen_create(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t le
     g->off.push_back(sum);
     g->salt.assign(g->len.size(), 0);
     g->perm.init(n, splitmix(seed ^ 0x3c6ef372fe94f82bull));
+    if (front_starts) {
+        const uint64_t C = g->len.size();
+        g->front_starts = true;
+        g->nb.resize(C);
+        for (uint64_t i = 0; i < C; ++i) g->nb[i] = g->off[i] - i;
+        g->perm_s.init(C, splitmix(seed ^ 0x510e527fade682d1ull));
+        g->perm_n.init(n - C, splitmix(seed ^ 0x9b05688c2b3e6c1full));
+    }
     // 2) uniqueness: re-draw every contig holding a k-mer that occurs more than once, until none.
     //    Skipped when the expected number of repeats n^2 / (2 * 4^k) is below 1e-9 (k=51 and
     //    anything below 10^12 k-mers); the table's duplicate counter still checks it on insert.
@@ -349,7 +384,7 @@ int kh_gen_truth(const kh_gen* g, uint64_t pb, uint64_t pe, char* out, uint64_t 
     const uint64_t C = g->len.size();
     std::vector<std::pair<uint64_t, uint32_t>> sel;  // (start position, contig)
     for (uint64_t i = 0; i < C; ++i) {
-        const uint64_t p = g->pos_of(g->off[i]);
+        const uint64_t p = g->front_starts ? (g->shuffle ? g->perm_s.fwd(i) : i) : g->pos_of(g->off[i]);
         if (p >= pb && p < pe) sel.emplace_back(p, (uint32_t)i);
     }
     std::sort(sel.begin(), sel.end());

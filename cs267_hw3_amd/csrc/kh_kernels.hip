@@ -76,21 +76,40 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_starts(KParams p, const uint8
                                                           const uint64_t* mask,
                                                           const uint64_t* mask_off,
                                                           uint64_t* starts) {
+    // 64 mask words per wave (one per lane). Sparse (C3: ~1 start per 100 records): each lane
+    // parses the set bits of its own word. Dense (C5: every start k-mer at the front of the
+    // records): the wave takes the words one at a time, lane j = record 64w + j, so the record
+    // reads coalesce instead of 64 serial byte-wise parses per lane.
     const uint64_t nw = (n + 63) >> 6;
-    for (uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; w < nw;
-         w += (uint64_t)gridDim.x * BLOCK) {
-        uint64_t m = mask[w];
-        uint64_t o = mask_off[w];
-        while (m) {
-            const int b = __ffsll((unsigned long long)m) - 1;
-            m &= m - 1;
-            const uint64_t i = (w << 6) + (uint64_t)b;
-            Key k;
-            uint32_t ext;
-            parse_record(recs + i * (uint64_t)p.R, p, k, ext);
-            starts[o * W] = slot_w0(k, ext, p);
-            if (W == 2) starts[o * W + 1] = k.lo;
-            ++o;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
+    auto put = [&](uint64_t i, uint64_t o) {
+        Key k;
+        uint32_t ext;
+        parse_record(recs + i * (uint64_t)p.R, p, k, ext);
+        starts[o * W] = slot_w0(k, ext, p);
+        if (W == 2) starts[o * W + 1] = k.lo;
+    };
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * 64; w0 < nw; w0 += waves * 64) {
+        const uint64_t w = w0 + lane;
+        const uint64_t m = w < nw ? mask[w] : 0;
+        const uint64_t o = w < nw ? mask_off[w] : 0;
+        uint32_t c = (uint32_t)__popcll(m);
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) c += __shfl_xor(c, d, 64);
+        if (c <= 128) {
+            uint64_t mm = m, oo = o;
+            while (mm) {
+                const int b = __ffsll((unsigned long long)mm) - 1;
+                mm &= mm - 1;
+                put((w << 6) + (uint64_t)b, oo++);
+            }
+        } else {
+            for (int j = 0; j < 64; ++j) {
+                const uint64_t mj = __shfl(m, j, 64);
+                const uint64_t oj = __shfl(o, j, 64);
+                if ((mj >> lane) & 1) put(((w0 + j) << 6) + lane, oj + (uint64_t)__popcll(mj & ((1ull << lane) - 1)));
+            }
         }
     }
 }

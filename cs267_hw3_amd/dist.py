@@ -670,7 +670,7 @@ def bench_main(args, w, world, rank):
     k, n_per = w["k"], w["n"]
     n_total = n_per * world  # weak scaling: n k-mers per GPU
     t = time.time()
-    g = SyntheticKmers(k, n_total, w["len_min"], w["len_max"], w["single"], seed=w["seed"])
+    g = SyntheticKmers(k, n_total, w["len_min"], w["len_max"], w["single"], seed=w["seed"], **w.get("gen", {}))
     b, e = g.block(world, rank)
     host = g.records(b, e)
     recs = torch.from_numpy(host).to(torch.device("cuda", local))

@@ -210,13 +210,15 @@ class SyntheticKmers:
     """Seeded synthetic dataset (kh_gen_*): records at any position range + ground truth."""
 
     def __init__(self, k, n, len_min=8, len_max=200, single_permille=0, seed=1, shuffle=True,
-                 threads=0):
+                 threads=0, n_long=0, long_len=0, front_starts=False):
+        """n_long / long_len / front_starts: the C5 skew (kh_gen_create_skewed)."""
         self.k, self.n = k, int(n)
         self.R = record_size(k)
         self._L = _lib.lib()
         h = ctypes.c_void_p()
-        check(self._L.kh_gen_create(ctypes.byref(h), k, self.n, len_min, len_max,
-                                    single_permille, seed, 1 if shuffle else 0, threads))
+        check(self._L.kh_gen_create_skewed(ctypes.byref(h), k, self.n, len_min, len_max,
+                                           single_permille, seed, 1 if shuffle else 0, threads,
+                                           n_long, long_len, 1 if front_starts else 0))
         self._h = h
 
     def close(self):

@@ -209,6 +209,12 @@ int kh_next_kmer(int k, const uint8_t* rec, uint8_t* packed_out);
 typedef struct kh_gen kh_gen;
 int kh_gen_create(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
                   uint32_t single_permille, uint64_t seed, int shuffle, int threads);
+/* C5-style skewed set (BASELINE configs[4]): the first n_long contigs have long_len
+ * k-mers, the rest U[len_min, len_max]; front_starts != 0 puts every start k-mer ahead of every
+ * other record (so the block split hands all walkers to the first ranks). */
+int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
+                         uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
+                         uint32_t long_len, int front_starts);
 int kh_gen_destroy(kh_gen* g);
 uint64_t kh_gen_num_contigs(const kh_gen* g);
 /* records at output positions [pos_begin, pos_end) in kmer_pair layout (block split of

@@ -145,3 +145,13 @@ def test_staged_insert_words(monkeypatch, mode, k, n, chunks):
             sh.stage_words(words[:W * 10], 10, 10)
         assert e.value.code == _lib.KH_ERR_FULL
         sh.finish_words()
+
+
+@pytest.mark.parametrize("P", [1, 4])
+def test_sharded_skewed_c5(P):
+    """C5 skew at small scale: long chains (hundreds of migrations each) among short contigs,
+    every start k-mer in the first records (rank 0 owns all walkers)."""
+    from cs267_hw3_amd.dist import run_threaded
+    g = kh.SyntheticKmers(51, 600_000, 2, 16, 0, seed=55, n_long=4, long_len=20_000, front_starts=True)
+    info = {}
+    check_ranks(g, run_threaded(51, g.records(), P, info=info), P)

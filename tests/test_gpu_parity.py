@@ -423,3 +423,11 @@ def test_gpu_windowed_pass_block_sizes(monkeypatch, tb, k, n, batches):
     assert got == g.truth() and nc == g.num_contigs
     s = t.stats()
     assert s["n_dup"] == 0 and s["n_full"] == 0 and s["n_inserted"] == n
+
+
+@pytest.mark.parametrize("k,n,n_long,long_len", [(51, 4_000_000, 4, 600_000), (19, 2_000_000, 3, 300_000)])
+def test_gpu_skewed_c5(k, n, n_long, long_len):
+    """C5 skew on one GPU: splitter segments walk the long chains; starts first in record order."""
+    g = kh.SyntheticKmers(k, n, 2, 16, 0, seed=k + n_long, n_long=n_long, long_len=long_len, front_starts=True)
+    t, got, nc = run(k, g.records())
+    assert nc == g.num_contigs and got == g.truth()

@@ -118,3 +118,18 @@ def test_generator_unshuffled_is_contig_major():
     r = g.records()
     assert all(r[i * 10, 5] == ord("F") for i in range(100))          # starts every 10 records
     assert all(r[i * 10 + 9, 6] == ord("F") for i in range(100))      # ends
+
+
+@pytest.mark.parametrize("k,front", [(19, True), (51, True), (31, False)])
+def test_skewed_generator_c5(k, front):
+    """C5 skew (BASELINE configs[4]): long chains among short contigs, start k-mers first in
+    record order; the oracle's assembly == the generator's truth, every block split included."""
+    g = kh.SyntheticKmers(k, 150_000, 2, 16, 0, seed=k + 5, n_long=3, long_len=20_000, front_starts=front)
+    recs = g.records()
+    rc, text, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0 and nc == g.num_contigs and text == g.truth()
+    P = (k + 3) // 4
+    starts = np.nonzero(recs[:, P] == ord("F"))[0]
+    if front:
+        assert starts.max() == g.num_contigs - 1      # all walkers in the first records
+    assert b"".join(g.truth(*g.block(4, r)) for r in range(4)) == g.truth()
