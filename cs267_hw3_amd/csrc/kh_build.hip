@@ -1398,7 +1398,8 @@ template <int W, bool REC>
 static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
                               TableView t, bool table_empty, const PartBuffers& B, uint64_t* start_mask,
                               uint64_t* split_mask,
-                              unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+                              unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
+                              hipEvent_t after_records = nullptr) {
     static bool attrs = false;  // per template instance
     hipError_t e;
     if (!attrs) {
@@ -1429,6 +1430,10 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (mode1 == 4) {  // records -> words (input order) in buf2, then the windowed pass 1 on them
         k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, nullptr, start_mask, split_mask);
         words = B.buf2;
+        if (after_records) {  // start / splitter bits are complete: the caller's compaction may start
+            if ((e = hipEventRecord(after_records, s)) != hipSuccess) return e;
+            after_records = nullptr;
+        }
     }
     const bool fused1 = mode1 == 0 || direct1 || mode1 == 4, rec1 = REC && mode1 == 2;
     const bool res2 = fused1 || p2_res();
@@ -1472,6 +1477,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     } else {
         k_part1_hist<W, false><<<nb1, PB, 0, s>>>(p, nullptr, words, n, B.hist1, nullptr, nullptr);
     }
+    if (after_records && (e = hipEventRecord(after_records, s)) != hipSuccess) return e;
     if (!fused1) {
         e = scan_exclusive(Hist1F{B.hist1, pl.nb1}, pl.nb1 * NB1, B.off1, B.scratch,
                            (unsigned long long*)nullptr, (unsigned long long*)nullptr, s, Off1Idx{pl.nb1});
@@ -1596,13 +1602,13 @@ hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, boo
 hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
                               TableView t, bool table_empty, const PartBuffers& b,
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
-                              unsigned long long* stats, hipStream_t s) {
+                              unsigned long long* stats, hipStream_t s, hipEvent_t after_records) {
     if (n == 0) return hipSuccess;
     if (recs) {
         return p.W == 1 ? part_insert<1, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
-                                               stats, s)
+                                               stats, s, after_records)
                         : part_insert<2, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
-                                               stats, s);
+                                               stats, s, after_records);
     }
     return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s)
                     : part_insert<2, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s);

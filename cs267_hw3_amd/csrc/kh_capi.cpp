@@ -112,6 +112,9 @@ struct kh_table {
 
     hipEvent_t ev_ins0 = nullptr, ev_ins1 = nullptr, ev_ins2 = nullptr;
     hipEvent_t ev_walk0 = nullptr, ev_walk1 = nullptr, ev_mat1 = nullptr;
+    // side stream: start / splitter compaction overlapped with the partition passes
+    hipStream_t side = nullptr;
+    hipEvent_t ev_conv = nullptr, ev_side = nullptr;
     bool ins_timed = false, walk_timed = false;
 };
 
@@ -274,9 +277,14 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     if (hipStreamCreateWithFlags(&t->own_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(KH_ERR_HIP, "hipStreamCreate failed"));
     t->stream = t->own_stream;
+    if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(KH_ERR_HIP, "hipStreamCreate failed"));
     hipEvent_t* evs[] = {&t->ev_ins0, &t->ev_ins1, &t->ev_ins2, &t->ev_walk0, &t->ev_walk1, &t->ev_mat1};
     for (auto* ev : evs)
         if (hipEventCreate(ev) != hipSuccess) return bail(fail(KH_ERR_HIP, "hipEventCreate failed"));
+    for (auto* ev : {&t->ev_conv, &t->ev_side})
+        if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
+            return bail(fail(KH_ERR_HIP, "hipEventCreate failed"));
     if ((rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8))) return bail(rc);
     if ((rc = t->ctr.ensure(kh::CT_NUM * 8))) return bail(rc);
     if ((rc = t->stats.ensure(kh::ST_NUM * 8))) return bail(rc);
@@ -301,9 +309,12 @@ int kh_destroy(kh_table* t) {
                       &t->pb_buf1, &t->pb_buf2, &t->pb_hist1, &t->pb_off1, &t->pb_hist2,
                       &t->pb_off2, &t->pb_scratch, &t->pb_ovf};
     for (auto* b : bufs) b->release();
-    hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1};
+    if (t->side) (void)hipStreamSynchronize(t->side);
+    hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_conv,
+                        t->ev_side};
     for (auto ev : evs)
         if (ev) (void)hipEventDestroy(ev);
+    if (t->side) (void)hipStreamDestroy(t->side);
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
     delete t;
     return KH_OK;
@@ -366,25 +377,34 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     if (!fresh && (rc = clean_slots(t))) return rc;
     t->slots_stale = false;
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
+    // partitioned build: the start / splitter bits exist once the record pass has run, so their
+    // compaction runs on the side stream, overlapped with the partition passes and the build
+    const bool overlap = part && !getenv("KH_NO_OVERLAP");
+    hipStream_t cs = overlap ? t->side : t->stream;
     if (part)
         KH_HIP(kh::launch_part_insert(t->kp, (const uint8_t*)dev_recs, nullptr, n, view(t),
                                       fresh, pb, t->mask.as<uint64_t>(), split_mask,
                                       t->ctr.as<unsigned long long>(),
-                                      t->stats.as<unsigned long long>(), t->stream));
+                                      t->stats.as<unsigned long long>(), t->stream,
+                                      overlap ? t->ev_conv : nullptr));
     else
         KH_HIP(kh::launch_insert(t->kp, (const uint8_t*)dev_recs, n, view(t), t->mask.as<uint64_t>(),
                                  split_mask, t->stats.as<unsigned long long>(), t->stream));
     t->last_insert_part = part;
-    KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
+    if (overlap) KH_HIP(hipStreamWaitEvent(t->side, t->ev_conv, 0));
     KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
                                      t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                     t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(),
-                                     t->stream));
+                                     t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(), cs));
     if (split)
         KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, split_mask,
                                          t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                         t->splits.as<uint64_t>(), t->ctr.as<unsigned long long>(),
-                                         t->stream, kh::CT_N_SPLIT));
+                                         t->splits.as<uint64_t>(), t->ctr.as<unsigned long long>(), cs,
+                                         kh::CT_N_SPLIT));
+    KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
+    if (overlap) {
+        KH_HIP(hipEventRecord(t->ev_side, t->side));
+        KH_HIP(hipStreamWaitEvent(t->stream, t->ev_side, 0));
+    }
     KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
     t->ins_timed = true;
     t->n_inserted += n;
