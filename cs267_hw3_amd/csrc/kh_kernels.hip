@@ -794,6 +794,7 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     const uint64_t nw = wb.n_starts + wb.n_splits;
     if (nw == 0) return hipSuccess;
     const int G = walk_group(p);
+    if (const char* e = getenv("KH_WALK_BLOCKS")) grid_blocks = atoi(e);  // experiments
     if (G == -4) {  // quad-transposed: one walker per lane
         const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
                                              (uint64_t)(grid_blocks > 0 ? grid_blocks : 2048));
