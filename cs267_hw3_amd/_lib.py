@@ -42,6 +42,9 @@ class KhStats(ctypes.Structure):
 SEG_SUBS = 8  # KH_SEG_SUBS: sub-segments per peer segment of the fixed walk rounds
 MSG_WORDS = 5  # KH_MSG_WORDS: migrating-walker message
 TEXT_REC_WORDS = 2  # KH_TEXT_REC_WORDS
+LINK_WORDS = 4  # KH_LINK_WORDS
+JUMP_REPLY_WORDS = 3  # KH_JUMP_REPLY_WORDS
+SEG_REC_WORDS = 3  # KH_SEG_REC_WORDS
 
 _SIGS = {
     "kh_abi_version": (ctypes.c_int, []),
@@ -89,6 +92,14 @@ _SIGS = {
     "kh_mwalk_text_count": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "kh_mwalk_text_dev": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "kh_mwalk_end_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
+    "kh_mwalk_segments": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
+    "kh_mwalk_link_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
+    "kh_mwalk_pred_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
+    "kh_mwalk_jump_emit_dev": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "kh_mwalk_jump_answer_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp]),
+    "kh_mwalk_jump_apply_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.POINTER(c_u64)]),
+    "kh_mwalk_retag_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
+    "kh_mwalk_end_seg_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_u64]),
     "kh_dev_malloc": (ctypes.c_int, [ctypes.POINTER(c_vp), c_u64, ctypes.c_int]),
     "kh_dev_free": (ctypes.c_int, [c_vp]),
     "kh_memcpy_htod": (ctypes.c_int, [c_vp, c_vp, c_u64]),
@@ -136,6 +147,8 @@ def lib():
             pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("KH_LIB") and not hasattr(L, name):
+                continue  # A/B experiments against an older build
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -34,6 +34,10 @@ static constexpr int BUILD_THREADS = 512;
 static constexpr int T1 = 2;                      // consecutive tiles per pass-1 block
 static constexpr uint32_t S1 = 8;                 // pass-1 windows (atomic counters) per bucket
 static constexpr uint32_t NW1 = NB1 * S1;
+// splitter buffer of k_win1 in the dynamic-LDS tail: (4 KB - 2 KB gpos - wsum - counter) / 16 B
+static constexpr uint32_t WIN_SPLIT_LCAP = 120;
+static_assert(PART_TILE * 18 + 3 * 512 * 4 + 8 + WIN_SPLIT_LCAP * 16 + 8 <= PART_TILE * 16 + PART_TILE * 2 + 512 * 16,
+              "k_win1 LDS tail");
 static constexpr uint64_t LDS_BYTES = 160 * 1024;
 // radix-pass LDS: sorted items (2 words) + bin ids + hist/start (u32) + per-bin bases (u64) = 80 KiB
 static constexpr size_t SORT_LDS = (size_t)PART_TILE * 16 + PART_TILE * 2 + 2 * NB1 * 4 + NB1 * 8;
@@ -1303,11 +1307,12 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
 }
 
 // pass 1 on words: bucket = top 9 hash bits, S1 windows per bucket (window blockIdx % S1)
-template <int W, int TB>
+template <int W, int TB, bool COLLECT = false>
 __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restrict__ words, uint64_t n,
                                              uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1, uint64_t* ovf,
                                              uint64_t ovf_cap, unsigned long long* ctr,
-                                             unsigned long long* stats) {
+                                             unsigned long long* stats, uint64_t* splits = nullptr,
+                                             uint64_t splits_cap = 0) {
     constexpr int IPT = PART_TILE / TB;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
@@ -1315,23 +1320,60 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
     uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);
     uint32_t* start = hist + NB1;
     uint32_t* gpos = start + NB1;
+    // block-scan partials in static LDS: 80 KB + a few bytes keeps these kernels at one block
+    // (8 waves) per CU, measured faster than two (C3: pass 1 1.79-1.89 vs 1.98 ms, pass 2
+    // 1.61-1.67 vs 1.69); the splitter buffer (COLLECT) uses the dynamic region's unused tail
     __shared__ uint32_t wsum[TB / 64];
+    uint32_t* scount = gpos + NB1;
+    uint64_t* sbuf = reinterpret_cast<uint64_t*>(scount + 2);
     const uint32_t sub = blockIdx.x % S1;
     const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
     uint64_t a[IPT], b[IPT];
+    if (COLLECT && threadIdx.x == 0) *scount = 0;
     load_words_tb<W, TB>(words, b0, min(b0 + PART_TILE, n), b0 < n ? b0 : 0, a, b);
     for (int tt = 0; tt < T1; ++tt) {
         const uint64_t base = b0 + (uint64_t)tt * PART_TILE;
         if (base >= n) break;  // uniform
         uint32_t bin[IPT];
 #pragma unroll
-        for (int j = 0; j < IPT; ++j) bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - B1));
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t h = words_hash<W>(a[j], b[j], p);
+            bin[j] = (uint32_t)(h >> (64 - B1));
+            // splitter k-mers this shard owns (they head migrating-walk segments, kh_mseg.hip)
+            if (COLLECT && a[j] != EMPTY && ext_bwd(slot_ext(a[j])) != EXT_F && is_splitter(h, p)) {
+                const uint32_t pos = atomicAdd(scount, 1u);
+                if (pos < WIN_SPLIT_LCAP) {
+                    sbuf[pos * W] = a[j];
+                    if (W == 2) sbuf[pos * W + 1] = b[j];
+                } else {
+                    const unsigned long long o = atomicAdd(&ctr[CT_N_SPLIT], 1ull);
+                    if (o < splits_cap) {
+                        splits[o * W] = a[j];
+                        if (W == 2) splits[o * W + 1] = b[j];
+                    }
+                }
+            }
+        }
         const uint64_t nbase = base + PART_TILE;
         sort_reserve_write<W, TB, NB1>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
             [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
             [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
             [&]() { load_words_tb<W, TB>(words, nbase, (tt + 1 < T1) ? min(nbase + PART_TILE, n) : nbase, base, a, b); });
+    }
+    if (COLLECT) {  // this block's splitters: one list reservation
+        __syncthreads();
+        const uint32_t k = min(*scount, WIN_SPLIT_LCAP);
+        unsigned long long* sbase = reinterpret_cast<unsigned long long*>(sbuf + WIN_SPLIT_LCAP * W);
+        if (threadIdx.x == 0) *sbase = k ? atomicAdd(&ctr[CT_N_SPLIT], (unsigned long long)k) : 0ull;
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < k; x += TB) {
+            const uint64_t o = *sbase + x;
+            if (o < splits_cap) {
+                splits[o * W] = sbuf[x * W];
+                if (W == 2) splits[o * W + 1] = sbuf[x * W + 1];
+            }
+        }
     }
 }
 
@@ -1349,7 +1391,7 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restri
     uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);
     uint32_t* start = hist + NB1;
     uint32_t* gpos = start + NB1;
-    __shared__ uint32_t wsum[TB / 64];
+    __shared__ uint32_t wsum[TB / 64];  // static: one block per CU (see k_win1)
     const uint32_t bk = blockIdx.x / (uint32_t)G, g = blockIdx.x % (uint32_t)G;
     uint64_t s, e;
     uint32_t pre[S1 + 1];
@@ -1399,7 +1441,8 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
                               TableView t, bool table_empty, const PartBuffers& B, uint64_t* start_mask,
                               uint64_t* split_mask,
                               unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
-                              hipEvent_t after_records = nullptr) {
+                              hipEvent_t after_records = nullptr, uint64_t* wsplits = nullptr,
+                              uint64_t wsplits_cap = 0) {
     static bool attrs = false;  // per template instance
     hipError_t e;
     if (!attrs) {
@@ -1417,6 +1460,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         if ((e = allow_lds(k_part_build_pf<W, 4>, LDS_BYTES)) != hipSuccess) return e;
         if ((e = allow_lds(k_part_build_pf<W, 12>, LDS_BYTES)) != hipSuccess) return e;
         if ((e = allow_lds(k_win1<W, 512>, SORT_LDS)) != hipSuccess) return e;
+        if ((e = allow_lds(k_win1<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_win2<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
         if ((e = allow_lds(k_win2<W, 512, false>, SORT_LDS)) != hipSuccess) return e;
         attrs = true;
@@ -1456,8 +1500,15 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
             k_part1_direct<W><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask,
                                                        B.overflow, part_overflow_cap(n), ctr, stats);
         else if ((mode1 == 4 || (mode1 == 0 && !REC)) && win_tb() == 512)
-            k_win1<W, 512><<<nb1, 512, SORT_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
-                                                      part_overflow_cap(n), ctr, stats);
+        {
+            if (wsplits)
+                k_win1<W, 512, true><<<nb1, 512, SORT_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
+                                                                part_overflow_cap(n), ctr, stats, wsplits,
+                                                                wsplits_cap);
+            else
+                k_win1<W, 512><<<nb1, 512, SORT_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
+                                                          part_overflow_cap(n), ctr, stats);
+        }
         else if (mode1 == 4)
             k_part1_fused<W, false><<<nb1, PB, SORT_LDS, s>>>(p, nullptr, words, n, CAP1, wcnt, B.buf1, nullptr,
                                                                nullptr, B.overflow, part_overflow_cap(n), ctr,
@@ -1536,11 +1587,12 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
 template <int W>
 static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
                              const PartBuffers& B, unsigned long long* ctr, unsigned long long* stats,
-                             hipStream_t s) {
+                             hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap) {
     hipError_t e;
     if ((e = allow_lds(k_part1_fused<W, false>, SORT_LDS)) != hipSuccess) return e;
     if ((e = allow_lds(k_part2_res<W, true>, SORT_LDS)) != hipSuccess) return e;
     if ((e = allow_lds(k_win1<W, 512>, SORT_LDS)) != hipSuccess) return e;
+    if ((e = allow_lds(k_win1<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
     if ((e = allow_lds(k_win2<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(B.hist1);
     uint32_t* rcnt = reinterpret_cast<uint32_t*>(B.hist2);
@@ -1553,8 +1605,13 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(total);
     if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if (win_tb() == 512) {
-        k_win1<W, 512><<<(unsigned)pl.nb1, 512, SORT_LDS, s>>>(p, words, m, CAP1, wcnt, B.buf1, B.overflow,
-                                                               part_overflow_cap(total), ctr, stats);
+        if (wsplits)
+            k_win1<W, 512, true><<<(unsigned)pl.nb1, 512, SORT_LDS, s>>>(p, words, m, CAP1, wcnt, B.buf1,
+                                                                         B.overflow, part_overflow_cap(total), ctr,
+                                                                         stats, wsplits, wsplits_cap);
+        else
+            k_win1<W, 512><<<(unsigned)pl.nb1, 512, SORT_LDS, s>>>(p, words, m, CAP1, wcnt, B.buf1, B.overflow,
+                                                                   part_overflow_cap(total), ctr, stats);
         k_win2<W, 512, true><<<(unsigned)(NB1 * pl.G), 512, SORT_LDS, s>>>(p, B.buf1, m, B.off1, pl.G, RC, rcnt,
                                                                            B.buf2, B.overflow,
                                                                            part_overflow_cap(total), ctr, stats,
@@ -1587,9 +1644,9 @@ static hipError_t part_finish(const KParams& p, uint64_t total, TableView t, boo
 
 hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
                              const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
-                             hipStream_t s) {
-    return p.W == 1 ? part_stage<1>(p, words, m, total, first, b, ctr, stats, s)
-                    : part_stage<2>(p, words, m, total, first, b, ctr, stats, s);
+                             hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap) {
+    return p.W == 1 ? part_stage<1>(p, words, m, total, first, b, ctr, stats, s, wsplits, wsplits_cap)
+                    : part_stage<2>(p, words, m, total, first, b, ctr, stats, s, wsplits, wsplits_cap);
 }
 
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
@@ -1599,10 +1656,13 @@ hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, boo
                     : part_finish<2>(p, total, t, table_empty, b, ctr, stats, s);
 }
 
+bool part_words_collect_splits() { return win_tb() == 512; }
+
 hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
                               TableView t, bool table_empty, const PartBuffers& b,
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
-                              unsigned long long* stats, hipStream_t s, hipEvent_t after_records) {
+                              unsigned long long* stats, hipStream_t s, hipEvent_t after_records,
+                              uint64_t* wsplits, uint64_t wsplits_cap) {
     if (n == 0) return hipSuccess;
     if (recs) {
         return p.W == 1 ? part_insert<1, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
@@ -1610,8 +1670,10 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
                         : part_insert<2, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
                                                stats, s, after_records);
     }
-    return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s)
-                    : part_insert<2, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s);
+    return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s,
+                                            nullptr, wsplits, wsplits_cap)
+                    : part_insert<2, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s,
+                                            nullptr, wsplits, wsplits_cap);
 }
 
 }  // namespace kh

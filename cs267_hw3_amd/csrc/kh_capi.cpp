@@ -95,6 +95,11 @@ struct kh_table {
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
     DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm, rw_pos, rw_ctl;  // round walker
     DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
+    // splitter segments of the migrating walk (kh_mseg.hip)
+    DevBuf ms_len, ms_hi, ms_lo, ms_has, ms_done, ms_jump, ms_acc, ms_stab, ms_stab_id, ms_qsrc, ms_misc;
+    bool words_split = true;   // every routed word since the last clear went through splitter collection
+    bool ms_on = false;        // the current migrating walk uses splitter segments
+    uint64_t ms_ns = 0, ms_nsp = 0, ms_cap2 = 0, ms_nq = 0;
     uint64_t mw_store_n = 0;   // text records in mw_store
     uint32_t mw_P = 0, mw_rank = 0;
     bool mw_live = false, mw_stepped = false;
@@ -305,7 +310,8 @@ int kh_destroy(kh_table* t) {
                       &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id, &t->rw_hi, &t->rw_lo,
                       &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm, &t->rw_pos, &t->rw_ctl,
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
-                      &t->mw_misc, &t->mw_store,
+                      &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
+                      &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
                       &t->pb_buf1, &t->pb_buf2, &t->pb_hist1, &t->pb_off1, &t->pb_hist2,
                       &t->pb_off2, &t->pb_scratch, &t->pb_ovf};
     for (auto* b : bufs) b->release();
@@ -332,6 +338,7 @@ int kh_clear(kh_table* t) {
     t->staging = false;
     t->stage_n = 0;
     t->collected_n = 0;
+    t->words_split = true;
     return KH_OK;
 }
 
@@ -766,6 +773,38 @@ int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void
     return KH_OK;
 }
 
+// Splitter segments for the migrating walk (KH_MW_SEGMENTS=0 turns them off).
+static bool mseg_enabled(const kh_table* t) {
+    const char* e = getenv("KH_MW_SEGMENTS");
+    return t->kp.split_bits > 0 && !(e && !strcmp(e, "0"));
+}
+
+// Splitter density of the migrating walk: the table's (1 per 256 k-mers at C3 sizes;
+// KH_MW_SPLIT_EXTRA adds bits). Measured at one rank (C3 / C5 ms per step): off 15.4 / 2159,
+// +0 17.8 / 36.5, +2 17.3 / 66.6 — the segment phase is mostly a fixed cost (link, jump, retag
+// rounds), while sparser splitters leave longer segments (more rounds) on long chains.
+static kh::KParams mseg_params(const kh_table* t) {
+    kh::KParams p = t->kp;
+    int extra = 0;
+    if (const char* e = getenv("KH_MW_SPLIT_EXTRA")) extra = atoi(e);
+    int b = p.split_bits + extra;
+    p.split_bits = b < 1 ? 1 : (b > 30 ? 30 : b);
+    return p;
+}
+
+// Routed words: collect the splitter k-mers this shard owns (they head migrating-walk segments).
+// in_insert: the partitioned insert that follows collects them itself (k_win1): only size the list.
+static int collect_word_splits(kh_table* t, const void* words, uint64_t m, bool in_insert = false) {
+    if (!mseg_enabled(t) || !t->words_split) return KH_OK;
+    const kh::KParams mp = mseg_params(t);
+    const uint64_t need = (t->n_kmers >> (mp.split_bits > 3 ? mp.split_bits - 3 : 0)) + 4096;
+    if (int rc = ensure_list(t, t->splits, t->splits_cap, need)) return rc;
+    if (in_insert) return KH_OK;
+    KH_HIP(kh::launch_split_collect(mp, (const uint64_t*)words, m, t->splits.as<uint64_t>(), t->splits_cap,
+                                    t->ctr.as<unsigned long long>(), t->stream));
+    return KH_OK;
+}
+
 int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* words_out,
                         void* counts_out) {
     if (!t) return fail(KH_ERR_ARG, "null table");
@@ -807,6 +846,8 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     if (int rc = set_device(t)) return rc;
     t->split_ok = false;  // routed words carry no splitter marks: walks on this table use none
     const bool part = use_part_build(t, m);
+    const bool coll = part && kh::part_words_collect_splits() && mseg_enabled(t) && t->words_split;
+    if (int rc = collect_word_splits(t, words, m, coll)) return rc;
     kh::PartBuffers pb{};
     if (part)
         if (int rc = ensure_part(t, m, pb)) return rc;
@@ -816,9 +857,10 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     t->slots_stale = false;
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
     if (part)
-        KH_HIP(kh::launch_part_insert(t->kp, nullptr, (const uint64_t*)words, m, view(t),
+        KH_HIP(kh::launch_part_insert(coll ? mseg_params(t) : t->kp, nullptr, (const uint64_t*)words, m, view(t),
                                       fresh, pb, nullptr, nullptr, t->ctr.as<unsigned long long>(),
-                                      t->stats.as<unsigned long long>(), t->stream));
+                                      t->stats.as<unsigned long long>(), t->stream, nullptr,
+                                      coll ? t->splits.as<uint64_t>() : nullptr, coll ? t->splits_cap : 0));
     else
         KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
                                        t->stats.as<unsigned long long>(), t->stream));
@@ -866,12 +908,15 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
         return fail(KH_ERR_FULL, "staged %llu + %llu words exceed the build's %llu",
                     (unsigned long long)t->stage_n, (unsigned long long)m, (unsigned long long)t->stage_total);
     if (m == 0) return KH_OK;
+    const bool coll = t->stage_part && kh::part_words_collect_splits() && mseg_enabled(t) && t->words_split;
+    if (int rc = collect_word_splits(t, words, m, coll)) return rc;
     if (t->stage_part) {
         kh::PartBuffers b{};
         if (int rc = ensure_part(t, t->stage_total, b)) return rc;
-        KH_HIP(kh::launch_part_stage(t->kp, (const uint64_t*)words, m, t->stage_total, false, b,
+        KH_HIP(kh::launch_part_stage(coll ? mseg_params(t) : t->kp, (const uint64_t*)words, m, t->stage_total, false, b,
                                      t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(),
-                                     t->stream));
+                                     t->stream, coll ? t->splits.as<uint64_t>() : nullptr,
+                                     coll ? t->splits_cap : 0));
     } else {
         KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
                                        t->stats.as<unsigned long long>(), t->stream));
@@ -1044,6 +1089,18 @@ int grow_keep(DevBuf& b, uint64_t want, uint64_t used, hipStream_t s) {
 }
 }  // namespace
 
+static kh::MSegState mseg_state(kh_table* t) {
+    kh::MSegState st;
+    st.len = t->ms_len.as<uint32_t>();
+    st.link_hi = t->ms_hi.as<uint64_t>();
+    st.link_lo = t->ms_lo.as<uint64_t>();
+    st.has_link = t->ms_has.as<uint8_t>();
+    st.done = t->ms_done.as<uint8_t>();
+    st.jump = t->ms_jump.as<uint64_t>();
+    st.acc = t->ms_acc.as<uint64_t>();
+    return st;
+}
+
 int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t* n_walkers) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (nranks < 1 || nranks > kh::MAX_RANKS || rank < 0 || rank >= nranks)
@@ -1054,9 +1111,36 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     uint64_t ns = 0;
     if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
     if (ns >= (1ull << 31)) return fail(KH_ERR_ARG, "%llu start k-mers on one rank (max 2^31)", (unsigned long long)ns);
-    if ((rc = t->mw_init.ensure((ns + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_misc.ensure(64)) ||
-        (rc = t->mw_store.ensure((ns + 1024) * 16)))
+    // splitter segments: every splitter this shard owns seeds a walker too (kh_mseg.hip)
+    // on or off the same way on every rank (walkers stop before splitters owned anywhere)
+    uint64_t nsp = 0;
+    t->ms_on = mseg_enabled(t) && t->words_split;
+    if (t->ms_on && t->splits.p) {
+        if ((rc = read_ctr(t, kh::CT_N_SPLIT, &nsp))) return rc;
+        if (nsp > t->splits_cap)
+            return fail(KH_ERR_FULL, "%llu splitter k-mers exceed the list (%llu)", (unsigned long long)nsp,
+                        (unsigned long long)t->splits_cap);
+        if (ns + nsp >= (1ull << 31))
+            return fail(KH_ERR_ARG, "%llu walk segments on one rank (max 2^31)", (unsigned long long)(ns + nsp));
+    }
+    const uint64_t nseg = ns + nsp;
+    if ((rc = t->mw_init.ensure((nseg + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_misc.ensure(64)) ||
+        (rc = t->mw_store.ensure((nseg + 1024) * 16)))
         return rc;
+    t->ms_ns = ns;
+    t->ms_nsp = nsp;
+    if (t->ms_on) {
+        uint64_t cap2 = 64;
+        while (cap2 < 2 * nsp + 64) cap2 <<= 1;
+        t->ms_cap2 = cap2;
+        if ((rc = t->ms_len.ensure((nseg + 1) * 4)) || (rc = t->ms_hi.ensure((nseg + 1) * 8)) ||
+            (rc = t->ms_lo.ensure((nseg + 1) * 8)) || (rc = t->ms_has.ensure(nseg + 1)) ||
+            (rc = t->ms_done.ensure(nseg + 1)) || (rc = t->ms_jump.ensure((nseg + 1) * 8)) ||
+            (rc = t->ms_acc.ensure((nseg + 1) * 8)) || (rc = t->ms_stab.ensure(cap2 * 16)) ||
+            (rc = t->ms_stab_id.ensure(cap2 * 4)) || (rc = t->ms_qsrc.ensure((nsp + 1) * 4)) ||
+            (rc = t->ms_misc.ensure(64)))
+            return rc;
+    }
     t->mw_P = (uint32_t)nranks;
     t->mw_rank = (uint32_t)rank;
     t->rw_n = ns;
@@ -1065,10 +1149,135 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
     KH_HIP(kh::launch_mw_init(t->kp, t->starts.as<uint64_t>(), ns, (uint32_t)rank, t->mw_init.as<uint64_t>(),
                               t->stream));
+    if (t->ms_on) {
+        KH_HIP(kh::launch_mw_init(t->kp, t->splits.as<uint64_t>(), nsp, (uint32_t)rank,
+                                  t->mw_init.as<uint64_t>() + ns * kh::MSG_WORDS, t->stream, ns));
+        KH_HIP(kh::launch_mseg_init(ns, nseg, (uint32_t)rank, mseg_state(t), t->stream));
+        KH_HIP(kh::launch_mseg_stab(t->kp, t->splits.as<uint64_t>(), nsp, t->ms_stab.as<uint64_t>(),
+                                    t->ms_stab_id.as<uint32_t>(), t->ms_cap2, t->stream));
+    }
+    t->rw_n = nseg;
     t->mw_live = true;
     t->mw_stepped = false;
     t->assembled = false;
-    if (n_walkers) *n_walkers = ns;
+    if (n_walkers) *n_walkers = nseg;
+    return KH_OK;
+}
+
+int kh_mwalk_segments(kh_table* t, uint64_t* n_splitter_segments) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (!n_splitter_segments) return fail(KH_ERR_ARG, "null output");
+    *n_splitter_segments = t->ms_on ? t->ms_nsp : 0;
+    return KH_OK;
+}
+
+int kh_mwalk_link_dev(kh_table* t, const void* recs, uint64_t n, void* out, void* counts) {
+    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
+    if (!counts || (n && !recs)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    const uint64_t nseg = t->ms_ns + t->ms_nsp;
+    if (nseg && !out) return fail(KH_ERR_ARG, "null output");
+    if (int rc = ensure_route(t, nseg, (int)t->mw_P)) return rc;
+    unsigned long long* fin = t->ms_misc.as<unsigned long long>();
+    KH_HIP(hipMemsetAsync(fin, 0, 8, t->stream));
+    const kh::MSegState st = mseg_state(t);
+    KH_HIP(kh::launch_mseg_scan((const uint64_t*)recs, n, nseg, st, fin, t->stream));
+    uint64_t f = 0;
+    KH_HIP(hipMemcpyAsync(&f, fin, 8, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    if (f != nseg)
+        return fail(KH_ERR_NOT_FOUND, "%llu of %llu walk segments did not finish (records lost in transit?)",
+                    (unsigned long long)(nseg - f), (unsigned long long)nseg);
+    KH_HIP(kh::launch_mseg_link(t->kp, st, nseg, t->mw_P, t->mw_rank, t->route_hist.as<uint64_t>(),
+                                t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(), (uint64_t*)out,
+                                (uint64_t*)counts, t->stream));
+    return KH_OK;
+}
+
+int kh_mwalk_pred_dev(kh_table* t, const void* links, uint64_t m) {
+    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
+    if (m && !links) return fail(KH_ERR_ARG, "null links");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_mseg_pred((const uint64_t*)links, m, t->ms_stab.as<uint64_t>(), t->ms_stab_id.as<uint32_t>(),
+                                t->ms_cap2, t->ms_ns, mseg_state(t), t->stats.as<unsigned long long>(), t->stream));
+    return KH_OK;
+}
+
+int kh_mwalk_jump_emit_dev(kh_table* t, void* out, void* counts) {
+    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
+    if (!counts || (t->ms_nsp && !out)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, t->ms_nsp, (int)t->mw_P)) return rc;
+    KH_HIP(kh::launch_mseg_jump_emit(mseg_state(t), t->ms_ns, t->ms_nsp, t->mw_P, t->route_hist.as<uint64_t>(),
+                                     t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(), (uint64_t*)out,
+                                     t->ms_qsrc.as<uint32_t>(), (uint64_t*)counts, t->stream));
+    return KH_OK;
+}
+
+int kh_mwalk_jump_answer_dev(kh_table* t, const void* queries, uint64_t m, void* replies) {
+    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
+    if (m && (!queries || !replies)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_mseg_jump_answer((const uint64_t*)queries, m, mseg_state(t), (uint64_t*)replies, t->stream));
+    return KH_OK;
+}
+
+int kh_mwalk_jump_apply_dev(kh_table* t, const void* replies, uint64_t m, uint64_t* pending) {
+    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
+    if (!pending || (m && !replies)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    unsigned long long* left = t->ms_misc.as<unsigned long long>() + 1;
+    KH_HIP(kh::launch_mseg_jump_apply((const uint64_t*)replies, m, t->ms_qsrc.as<uint32_t>(), t->ms_ns,
+                                      mseg_state(t), left, t->stream));
+    uint64_t l = 0;
+    KH_HIP(hipMemcpyAsync(&l, left, 8, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    *pending = l;
+    return KH_OK;
+}
+
+int kh_mwalk_retag_dev(kh_table* t, const void* recs, uint64_t n, void* out, void* counts) {
+    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
+    if (!counts || (n && !recs) || (n + t->ms_nsp && !out)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, n + t->ms_nsp, (int)t->mw_P)) return rc;
+    const kh::MSegState st = mseg_state(t);
+    KH_HIP(kh::launch_mseg_check(t->ms_ns, t->ms_ns + t->ms_nsp, st, t->stats.as<unsigned long long>(), t->stream));
+    KH_HIP(kh::launch_mseg_retag((const uint64_t*)recs, n, t->ms_ns, t->ms_nsp, st, t->mw_P,
+                                 t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
+                                 t->route_scratch.as<uint64_t>(), (uint64_t*)out, (uint64_t*)counts, t->stream));
+    return KH_OK;
+}
+
+int kh_mwalk_end_seg_dev(kh_table* t, const void* recs, uint64_t n, const void* seg_recs, uint64_t m) {
+    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
+    if ((n && !recs) || (m && !seg_recs)) return fail(KH_ERR_ARG, "null records");
+    if (int rc = set_device(t)) return rc;
+    const uint64_t nc = t->ms_ns;
+    int rc;
+    if ((rc = t->contig_len.ensure((nc + 1) * 4)) || (rc = t->contig_off.ensure((nc + 1) * 8)) ||
+        (rc = t->scratch.ensure(kh::scan_scratch_words(nc) * 8 + 64)))
+        return rc;
+    unsigned long long* ctr = t->ctr.as<unsigned long long>();
+    const kh::MSegState st = mseg_state(t);
+    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
+    KH_HIP(kh::launch_mseg_lens((const uint64_t*)seg_recs, m, nc, st, t->contig_len.as<uint32_t>(), t->stream));
+    KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
+                                     t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
+    if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
+    uint64_t bytes = 0;
+    KH_HIP(hipMemcpyAsync(&bytes, ctr + kh::CT_OUT_BYTES, 8, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    if ((rc = t->text.ensure(bytes + 64))) return rc;
+    KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
+                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+    KH_HIP(kh::launch_mseg_words(t->kp.K, (const uint64_t*)recs, n, (const uint64_t*)seg_recs, m, nc, st,
+                                 t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+    KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
+    t->walk_timed = true;
+    t->last_contigs = nc;
+    t->assembled = true;
+    t->mw_live = false;
     return KH_OK;
 }
 
@@ -1094,6 +1303,7 @@ int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, vo
     kh::MWalkRound mw;
     mw.P = t->mw_P;
     mw.rank = t->mw_rank;
+    mw.split_bits = t->ms_on ? (uint32_t)mseg_params(t).split_bits : 0u;
     mw.max_steps = t->rw_total;
     mw.in = src;
     mw.n_in = n;
@@ -1138,6 +1348,8 @@ int kh_mwalk_text_dev(kh_table* t, void* out, void* counts) {
 
 int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
     if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (t->ms_on && t->ms_nsp)
+        return fail(KH_ERR_STATE, "segmented walk: use kh_mwalk_link_dev .. kh_mwalk_end_seg_dev");
     if (n && !recs) return fail(KH_ERR_ARG, "null records");
     if (int rc = set_device(t)) return rc;
     const uint64_t nc = t->rw_n;

@@ -117,9 +117,10 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
 // word (or bases appended, fin)].
 static constexpr int MSG_WORDS = 5;
 static constexpr int MW_RUN_WORDS = 8;                  // words a walker may flush per round
-static constexpr int MW_REC_SLOTS = MW_RUN_WORDS + 2;   // + final partial word + finish record
+static constexpr int MW_REC_SLOTS = MW_RUN_WORDS + 4;   // + final partial word + finish + 2 link records
 struct MWalkRound {
     uint32_t P, rank;
+    uint32_t split_bits = 0;  // > 0: walkers stop before splitter k-mers (kh_mseg.hip)
     uint64_t max_steps;
     const uint64_t* in;   // n_in messages
     uint64_t n_in;
@@ -129,7 +130,45 @@ struct MWalkRound {
     uint8_t* nrec;        // n_in
 };
 hipError_t launch_mw_init(const KParams& p, const uint64_t* starts, uint64_t n, uint32_t rank, uint64_t* msgs,
-                          hipStream_t s);
+                          hipStream_t s, uint64_t idx0 = 0);
+
+// ---- splitter segments of the migrating walk (kh_mseg.hip) ----------------------------------
+struct MSegState {       // per local segment: starts [0, ns), splitter segments [ns, ns + nsp)
+    uint32_t* len;       // bases appended by the segment's walker
+    uint64_t* link_hi;   // key of the splitter it stopped before
+    uint64_t* link_lo;
+    uint8_t* has_link;
+    uint8_t* done;       // head known
+    uint64_t* jump;      // pointer-jumping target (gid = rank << 40 | index); when done: head
+    uint64_t* acc;       // bases from the start of `jump` to this segment; when done: offset
+};
+hipError_t launch_split_collect(const KParams& p, const uint64_t* words, uint64_t m, uint64_t* out, uint64_t cap,
+                                unsigned long long* ctr, hipStream_t s);
+hipError_t launch_mseg_stab(const KParams& p, const uint64_t* splits, uint64_t nsp, uint64_t* stab, uint32_t* id,
+                            uint64_t cap2, hipStream_t s);
+hipError_t launch_mseg_init(uint64_t ns, uint64_t nseg, uint32_t rank, const MSegState& st, hipStream_t s);
+hipError_t launch_mseg_scan(const uint64_t* recs, uint64_t n, uint64_t nseg, const MSegState& st,
+                            unsigned long long* fin, hipStream_t s);
+hipError_t launch_mseg_link(const KParams& p, const MSegState& st, uint64_t nseg, uint32_t P, uint32_t rank,
+                            uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out, uint64_t* counts,
+                            hipStream_t s);
+hipError_t launch_mseg_pred(const uint64_t* msgs, uint64_t m, const uint64_t* stab, const uint32_t* id, uint64_t cap2,
+                            uint64_t ns, const MSegState& st, unsigned long long* stats, hipStream_t s);
+hipError_t launch_mseg_jump_emit(const MSegState& st, uint64_t ns, uint64_t nsp, uint32_t P, uint64_t* hist,
+                                 uint64_t* off, uint64_t* scratch, uint64_t* out, uint32_t* qsrc, uint64_t* counts,
+                                 hipStream_t s);
+hipError_t launch_mseg_jump_answer(const uint64_t* q, uint64_t m, const MSegState& st, uint64_t* rep, hipStream_t s);
+hipError_t launch_mseg_jump_apply(const uint64_t* rep, uint64_t m, const uint32_t* qsrc, uint64_t ns,
+                                  const MSegState& st, unsigned long long* left, hipStream_t s);
+hipError_t launch_mseg_check(uint64_t ns, uint64_t nseg, const MSegState& st, unsigned long long* stats,
+                             hipStream_t s);
+hipError_t launch_mseg_retag(const uint64_t* recs, uint64_t n, uint64_t ns, uint64_t nsp, const MSegState& st,
+                             uint32_t P, uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out,
+                             uint64_t* counts, hipStream_t s);
+hipError_t launch_mseg_lens(const uint64_t* in3, uint64_t m, uint64_t ns, const MSegState& st, uint32_t* contig_len,
+                            hipStream_t s);
+hipError_t launch_mseg_words(int K, const uint64_t* recs, uint64_t n, const uint64_t* in3, uint64_t m, uint64_t ns,
+                             const MSegState& st, const uint64_t* off, char* out, hipStream_t s);
 hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
                          hipStream_t s);
 hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
@@ -280,14 +319,17 @@ struct PartBuffers {
 hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint64_t* words,
                               uint64_t n, TableView t, bool table_empty, const PartBuffers& b,
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
-                              unsigned long long* stats, hipStream_t s, hipEvent_t after_records = nullptr);
+                              unsigned long long* stats, hipStream_t s, hipEvent_t after_records = nullptr,
+                              uint64_t* word_splits = nullptr, uint64_t word_splits_cap = 0);
+// True when the partitioned insert of words collects splitter k-mers itself (k_win1).
+bool part_words_collect_splits();
 
 // Staged build of routed words (sharded insert): launch_part_stage per received chunk (first = the
 // first chunk of a build sized for `total` words), then launch_part_finish once. Requires
 // region_slots_fit and buffers from ensure_part(total).
 hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
                              const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
-                             hipStream_t s);
+                             hipStream_t s, uint64_t* word_splits = nullptr, uint64_t word_splits_cap = 0);
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
                               const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
                               hipStream_t s);

@@ -73,8 +73,20 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
                     buf = 0;
                 }
                 k = key_next(k, st, p);
-                const uint32_t q = owner_key(k, p, mw.P);
-                if (q != mw.rank || nwords >= MW_RUN_WORDS) {
+                if (mw.split_bits && (key_hash(k) & ((1ull << mw.split_bits) - 1)) == 0) {
+                    // the next k-mer heads a segment of its own: report it as this segment's link
+                    rec[2 * nrec] = rec_tag(origin, true, 1, idx);
+                    rec[2 * nrec + 1] = k.hi;
+                    ++nrec;
+                    rec[2 * nrec] = rec_tag(origin, true, 2, idx);
+                    rec[2 * nrec + 1] = k.lo;
+                    ++nrec;
+                    fin = true;
+                }
+                const uint32_t q = fin ? mw.rank : owner_key(k, p, mw.P);
+                if (fin) {
+                    // finished below (length record, no message)
+                } else if (q != mw.rank || nwords >= MW_RUN_WORDS) {
                     uint64_t* o = mw.tmp + j * MSG_WORDS;
                     o[0] = k.hi;
                     o[1] = k.lo;
@@ -136,7 +148,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
 
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p, const uint64_t* starts, uint64_t n, uint32_t rank,
-                                                   uint64_t* msgs) {
+                                                   uint64_t* msgs, uint64_t idx0) {
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t w0 = starts[i * W];
         const uint64_t w1 = (W == 2) ? starts[i * W + 1] : 0;
@@ -146,7 +158,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p, const uint64_t* st
         m[0] = k.hi;
         m[1] = k.lo;
         m[2] = 0;
-        m[3] = i << 32;
+        m[3] = (idx0 + i) << 32;
         m[4] = rank | ((uint64_t)(f > 4 ? EXT_BAD : f) << 8);
     }
 }
@@ -234,12 +246,12 @@ static unsigned grid_for(uint64_t n, uint64_t cap_blocks) {
 }
 
 hipError_t launch_mw_init(const KParams& p, const uint64_t* starts, uint64_t n, uint32_t rank, uint64_t* msgs,
-                          hipStream_t s) {
+                          hipStream_t s, uint64_t idx0) {
     if (n == 0) return hipSuccess;
     if (p.W == 1)
-        k_mw_init<1><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs);
+        k_mw_init<1><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs, idx0);
     else
-        k_mw_init<2><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs);
+        k_mw_init<2><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs, idx0);
     return hipGetLastError();
 }
 

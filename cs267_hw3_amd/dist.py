@@ -251,6 +251,45 @@ class GpuShard:
     def mw_end(self, recs, n):
         check(self.L.kh_mwalk_end_dev(self.h, self._p(recs), n))
 
+    # splitter segments of the migrating walk (kh_mseg.hip)
+    LINK_WORDS = _lib.LINK_WORDS
+    JUMP_REPLY_WORDS = _lib.JUMP_REPLY_WORDS
+    SEG_REC_WORDS = _lib.SEG_REC_WORDS
+
+    def mw_segments(self):
+        v = ctypes.c_uint64(0)
+        check(self.L.kh_mwalk_segments(self.h, ctypes.byref(v)))
+        return v.value
+
+    def mw_link(self, recs, n, out):
+        counts = self.zeros(self.nranks + 1, torch.int64)
+        check(self.L.kh_mwalk_link_dev(self.h, self._p(recs), n, self._p(out), self._p(counts)))
+        return counts
+
+    def mw_pred(self, links, m):
+        check(self.L.kh_mwalk_pred_dev(self.h, self._p(links), m))
+
+    def mw_jump_emit(self, out):
+        counts = self.zeros(self.nranks + 1, torch.int64)
+        check(self.L.kh_mwalk_jump_emit_dev(self.h, self._p(out), self._p(counts)))
+        return counts
+
+    def mw_jump_answer(self, queries, m, out):
+        check(self.L.kh_mwalk_jump_answer_dev(self.h, self._p(queries), m, self._p(out)))
+
+    def mw_jump_apply(self, replies, m):
+        v = ctypes.c_uint64(0)
+        check(self.L.kh_mwalk_jump_apply_dev(self.h, self._p(replies), m, ctypes.byref(v)))
+        return v.value
+
+    def mw_retag(self, recs, n, out):
+        counts = self.zeros(self.nranks + 1, torch.int64)
+        check(self.L.kh_mwalk_retag_dev(self.h, self._p(recs), n, self._p(out), self._p(counts)))
+        return counts
+
+    def mw_end_seg(self, recs, n, seg, m):
+        check(self.L.kh_mwalk_end_seg_dev(self.h, self._p(recs), n, self._p(seg), m))
+
     def signature(self):
         v = ctypes.c_uint64()
         check(self.L.kh_walk_signature(self.h, ctypes.byref(v)))
@@ -540,6 +579,7 @@ class DistributedKmerHashMap:
         sh, P = self.shard, self.P
         M, T = sh.MSG_WORDS, sh.TEXT_REC_WORDS
         n_in = sh.mw_begin(P, self.comm.rank, total_kmers)
+        n_in_total = n_in
         inp = None
         self.rounds = 0
         while True:
@@ -570,9 +610,78 @@ class DistributedKmerHashMap:
             trecv = sh.zeros(max(r, 1) * T, torch.int64)
             self._all_to_all(trecv[:r * T], tout[:nrec * T], [c * T for c in recv_splits],
                              [c * T for c in send_splits], gmax * T)
-        sh.mw_end(trecv, r)
+        nseg = sh.mw_segments() if hasattr(sh, "mw_segments") else 0
+        # every rank takes the same branch (a rank without splitters still links and answers)
+        seg_any = self._global_max(nseg) if P > 1 else nseg
+        if seg_any:
+            self._segments_end(trecv, r, n_in_total)
+        else:
+            sh.mw_end(trecv, r)
         sh.sync()
         return self.rounds
+
+    def _global_max(self, x):
+        """max of a host int over ranks (one small all-to-all)."""
+        P = self.P
+        send = torch.full((P,), int(x), dtype=torch.int64, device=self.shard.zeros(1, torch.int64).device)
+        recv = torch.empty_like(send)
+        self.comm.all_to_all(recv, send, [1] * P, [1] * P)
+        return int(recv.max().item())
+
+    def _segments_end(self, trecv, r, nseg):
+        """Splitter segments: link each segment to its successor's owner, pointer-jump to the
+        contig heads, send the segments' text to the contig origins, materialise."""
+        sh, P = self.shard, self.P
+        dev = trecv.device
+        L, J, S = sh.LINK_WORDS, sh.JUMP_REPLY_WORDS, sh.SEG_REC_WORDS
+        local = P == 1 and not self.SELF_EXCHANGE  # one rank: every exchange is the identity
+        lout = self._grow("_ms_links", max(nseg, 1) * L, torch.int64, dev)
+        counts = sh.mw_link(trecv, r, lout)
+        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
+        m = sum(recv_splits)
+        if local:
+            lin = lout
+        else:
+            lin = self._grow("_ms_links_in", max(m, 1) * L, torch.int64, dev)
+            self._all_to_all(lin[:m * L], lout[:sum(send_splits) * L], [c * L for c in recv_splits],
+                             [c * L for c in send_splits], gmax * L)
+        sh.mw_pred(lin, m)
+        self.jump_rounds = 0
+        qout = self._grow("_ms_q", max(nseg, 1), torch.int64, dev)
+        while True:
+            counts = sh.mw_jump_emit(qout)
+            send_splits, recv_splits, totals, gmax = self._exchange_counts(counts)
+            if sum(totals) == 0:
+                break
+            self.jump_rounds += 1
+            ms, mr = sum(send_splits), sum(recv_splits)
+            if local:
+                qin = qout
+            else:
+                qin = self._grow("_ms_qin", max(mr, 1), torch.int64, dev)
+                self._all_to_all(qin[:mr], qout[:ms], recv_splits, send_splits, gmax)
+            rep = self._grow("_ms_rep", max(mr, 1) * J, torch.int64, dev)
+            sh.mw_jump_answer(qin, mr, rep)
+            if local:
+                rin = rep
+            else:
+                rin = self._grow("_ms_rin", max(ms, 1) * J, torch.int64, dev)
+                # replies go back the way the queries came (per-peer counts swapped; the global
+                # max per-peer split is the queries' one)
+                self._all_to_all(rin[:ms * J], rep[:mr * J], [c * J for c in send_splits],
+                                 [c * J for c in recv_splits], gmax * J)
+            sh.mw_jump_apply(rin, ms)
+        tout = self._grow("_ms_t", max(r + nseg, 1) * S, torch.int64, dev)
+        counts = sh.mw_retag(trecv, r, tout)
+        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
+        m = sum(recv_splits)
+        if local:
+            tin = tout
+        else:
+            tin = self._grow("_ms_tin", max(m, 1) * S, torch.int64, dev)
+            self._all_to_all(tin[:m * S], tout[:sum(send_splits) * S], [c * S for c in recv_splits],
+                             [c * S for c in send_splits], gmax * S)
+        sh.mw_end_seg(trecv, r, tin, m)
 
     def _assemble_variable(self, total_kmers):
         """Variable-size rounds: exact per-peer counts exchanged (and read on the host) every

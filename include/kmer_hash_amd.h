@@ -183,6 +183,29 @@ int kh_mwalk_round_dev(kh_table* t, const void* dev_in, uint64_t n_in, void* dev
 int kh_mwalk_text_count(kh_table* t, uint64_t* n_records);
 int kh_mwalk_text_dev(kh_table* t, void* dev_out, void* dev_counts_out);
 int kh_mwalk_end_dev(kh_table* t, const void* dev_recs, uint64_t n);
+/* Splitter segments of the migrating walk (kh_mseg.hip; on when the shard collects splitters,
+ * KH_MW_SEGMENTS=0 turns them off). kh_mwalk_begin then also seeds a walker at every splitter
+ * k-mer this shard owns (n_walkers includes them) and walkers stop before splitters. When
+ * kh_mwalk_segments reports > 0 (on any rank: the count is per rank), after the text records have
+ * come home (kh_mwalk_text_dev + exchange) the end of the walk is, instead of kh_mwalk_end_dev:
+ *   kh_mwalk_link_dev(recs)  -> KH_LINK_WORDS-word links grouped by owner -> exchange -> kh_mwalk_pred_dev
+ *   repeat: kh_mwalk_jump_emit_dev -> 1-word queries, exchange -> kh_mwalk_jump_answer_dev ->
+ *           KH_JUMP_REPLY_WORDS-word replies, exchange back (counts reversed) ->
+ *           kh_mwalk_jump_apply_dev (pending = segments still without a head); until no rank emits
+ *   kh_mwalk_retag_dev(recs) -> KH_SEG_REC_WORDS-word records grouped by contig origin -> exchange
+ *   kh_mwalk_end_seg_dev(recs, received segment records)   (this rank's test_<rank>.dat in HBM)
+ * Buffers: links <= n_walkers records, queries <= segments, retag output <= n + segments. */
+#define KH_LINK_WORDS 4
+#define KH_JUMP_REPLY_WORDS 3
+#define KH_SEG_REC_WORDS 3
+int kh_mwalk_segments(kh_table* t, uint64_t* n_splitter_segments);
+int kh_mwalk_link_dev(kh_table* t, const void* dev_recs, uint64_t n, void* dev_links_out, void* dev_counts_out);
+int kh_mwalk_pred_dev(kh_table* t, const void* dev_links, uint64_t m);
+int kh_mwalk_jump_emit_dev(kh_table* t, void* dev_queries_out, void* dev_counts_out);
+int kh_mwalk_jump_answer_dev(kh_table* t, const void* dev_queries, uint64_t m, void* dev_replies_out);
+int kh_mwalk_jump_apply_dev(kh_table* t, const void* dev_replies, uint64_t m, uint64_t* pending);
+int kh_mwalk_retag_dev(kh_table* t, const void* dev_recs, uint64_t n, void* dev_seg_recs_out, void* dev_counts_out);
+int kh_mwalk_end_seg_dev(kh_table* t, const void* dev_recs, uint64_t n, const void* dev_seg_recs, uint64_t m);
 
 /* ---- device memory helpers (for hosts without an allocator of their own) --------------------*/
 int kh_dev_malloc(void** p, uint64_t bytes, int device);
