@@ -1224,15 +1224,17 @@ int kh_mwalk_jump_answer_dev(kh_table* t, const void* queries, uint64_t m, void*
 
 int kh_mwalk_jump_apply_dev(kh_table* t, const void* replies, uint64_t m, uint64_t* pending) {
     if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
-    if (!pending || (m && !replies)) return fail(KH_ERR_ARG, "null buffer");
+    if (m && !replies) return fail(KH_ERR_ARG, "null buffer");
     if (int rc = set_device(t)) return rc;
     unsigned long long* left = t->ms_misc.as<unsigned long long>() + 1;
     KH_HIP(kh::launch_mseg_jump_apply((const uint64_t*)replies, m, t->ms_qsrc.as<uint32_t>(), t->ms_ns,
                                       mseg_state(t), left, t->stream));
-    uint64_t l = 0;
-    KH_HIP(hipMemcpyAsync(&l, left, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
-    *pending = l;
+    if (pending) {  // optional: the next emit's counts already say whether any rank is pending
+        uint64_t l = 0;
+        KH_HIP(hipMemcpyAsync(&l, left, 8, hipMemcpyDeviceToHost, t->stream));
+        KH_HIP(hipStreamSynchronize(t->stream));
+        *pending = l;
+    }
     return KH_OK;
 }
 

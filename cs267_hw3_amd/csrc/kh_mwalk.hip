@@ -73,7 +73,8 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
                     buf = 0;
                 }
                 k = key_next(k, st, p);
-                if (mw.split_bits && (key_hash(k) & ((1ull << mw.split_bits) - 1)) == 0) {
+                const uint64_t hk = key_hash(k);
+                if (mw.split_bits && (hk & ((1ull << mw.split_bits) - 1)) == 0) {
                     // the next k-mer heads a segment of its own: report it as this segment's link
                     rec[2 * nrec] = rec_tag(origin, true, 1, idx);
                     rec[2 * nrec + 1] = k.hi;
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
                     ovf = true;
                 } else {
                     probing = true;
-                    s = home_slot(key_hash(k), cap);
+                    s = home_slot(hk, cap);
                 }
             }
             if (fin) {

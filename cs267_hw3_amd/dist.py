@@ -278,9 +278,8 @@ class GpuShard:
         check(self.L.kh_mwalk_jump_answer_dev(self.h, self._p(queries), m, self._p(out)))
 
     def mw_jump_apply(self, replies, m):
-        v = ctypes.c_uint64(0)
-        check(self.L.kh_mwalk_jump_apply_dev(self.h, self._p(replies), m, ctypes.byref(v)))
-        return v.value
+        # no pending count: the next emit's exchanged counts end the loop (no host sync here)
+        check(self.L.kh_mwalk_jump_apply_dev(self.h, self._p(replies), m, None))
 
     def mw_retag(self, recs, n, out):
         counts = self.zeros(self.nranks + 1, torch.int64)

@@ -191,7 +191,8 @@ int kh_mwalk_end_dev(kh_table* t, const void* dev_recs, uint64_t n);
  *   kh_mwalk_link_dev(recs)  -> KH_LINK_WORDS-word links grouped by owner -> exchange -> kh_mwalk_pred_dev
  *   repeat: kh_mwalk_jump_emit_dev -> 1-word queries, exchange -> kh_mwalk_jump_answer_dev ->
  *           KH_JUMP_REPLY_WORDS-word replies, exchange back (counts reversed) ->
- *           kh_mwalk_jump_apply_dev (pending = segments still without a head); until no rank emits
+ *           kh_mwalk_jump_apply_dev (pending, may be NULL = segments still without a head); until no
+ *           rank emits
  *   kh_mwalk_retag_dev(recs) -> KH_SEG_REC_WORDS-word records grouped by contig origin -> exchange
  *   kh_mwalk_end_seg_dev(recs, received segment records)   (this rank's test_<rank>.dat in HBM)
  * Buffers: links <= n_walkers records, queries <= segments, retag output <= n + segments. */
