@@ -348,12 +348,15 @@ __device__ __forceinline__ void sorted_write(const uint64_t (&a)[PITEMS], const 
 // Record input: parse the reference records once, one per thread per 256-record sub-tile (the next
 // sub-tile's 16-B loads are in flight while this one is parsed), emit internal words in input
 // order, count bins, and write the start bits. The pass-1 scatter then reads words only.
-template <int W>
+template <int PK>
+__device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, int pad, Key& k, uint32_t& ext);
+
+template <int W, int PK = 0>
 __global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* __restrict__ recs,
                                                       uint64_t n, uint64_t* words_out, uint64_t* hist1,
                                                       uint64_t* start_mask, uint64_t* split_mask) {
     __shared__ uint32_t h[NB1];
-    __shared__ __attribute__((aligned(16))) uint8_t stage[2][PB * 17];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[2][PB * 17 + 16];
     for (int i = threadIdx.x; i < NB1; i += PB) h[i] = 0;
     const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
     const uint64_t b1 = min(b0 + (uint64_t)T1 * PART_TILE, n);
@@ -377,11 +380,22 @@ __global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* 
         if (threadIdx.x + PB < nvec) reinterpret_cast<uint4*>(st)[threadIdx.x + PB] = r1;
         for (uint32_t x = (nvec << 4) + threadIdx.x; x < bytes; x += PB) st[x] = recs[sub * R + x];
         if (j + 1 < nsub) fetch(j + 1);
-        __syncthreads();
+        lds_barrier();  // LDS hand-off only: __syncthreads would also wait for the prefetch above
         const bool valid = threadIdx.x < cnt;
         Key k{0, 0};
         uint32_t ext = 0;
-        if (valid) parse_record(st + threadIdx.x * R, p, k, ext);
+        if (valid) {
+            if constexpr (PK != 0) {  // 3 aligned 8-B LDS reads + funnel shifts instead of 15 byte reads
+                const uint32_t a = threadIdx.x * (uint32_t)(PK + 2), a8 = a & ~7u, sh = (a & 7u) * 8u;
+                const uint64_t* q = reinterpret_cast<const uint64_t*>(st + a8);
+                const uint64_t u0 = q[0], u1 = q[1], u2 = q[2];
+                const uint64_t x0 = sh ? (u0 >> sh) | (u1 << (64 - sh)) : u0;
+                const uint64_t x1 = sh ? (u1 >> sh) | (u2 << (64 - sh)) : u1;
+                parse_record_regs_t<PK>(x0, x1, p.pad, k, ext);
+            } else {
+                parse_record(st + threadIdx.x * R, p, k, ext);
+            }
+        }
         const bool is_start = valid && ext_bwd(ext) == EXT_F;
         const uint64_t bal = __ballot(is_start);
         const uint64_t wb = sub + (threadIdx.x & ~63u);
@@ -622,7 +636,7 @@ __global__ __launch_bounds__(PB) void k_part1_direct(KParams p, const uint8_t* _
             Key k{0, 0};
             uint32_t ext = 0;
             if (valid) {
-                if (PK)
+                if constexpr (PK != 0)
                     parse_record_regs_t<PK>(x0[j], x1[j], p.pad, k, ext);
                 else
                     parse_record_regs(x0[j], x1[j], p, k, ext);
@@ -1472,7 +1486,12 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (mode1 == 4 && !REC) mode1 = 0;
     const bool direct1 = mode1 == 3;
     if (mode1 == 4) {  // records -> words (input order) in buf2, then the windowed pass 1 on them
-        k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, nullptr, start_mask, split_mask);
+        if (p.P == 13 && W == 2)
+            k_part1_convert<W, 13><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, nullptr, start_mask, split_mask);
+        else if (p.P == 5 && W == 1)
+            k_part1_convert<W, 5><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, nullptr, start_mask, split_mask);
+        else
+            k_part1_convert<W><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, nullptr, start_mask, split_mask);
         words = B.buf2;
         if (after_records) {  // start / splitter bits are complete: the caller's compaction may start
             if ((e = hipEventRecord(after_records, s)) != hipSuccess) return e;
