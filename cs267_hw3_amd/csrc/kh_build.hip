@@ -41,6 +41,20 @@ static_assert(PART_TILE * 18 + 3 * 512 * 4 + 8 + WIN_SPLIT_LCAP * 16 + 8 <= PART
 static constexpr uint64_t LDS_BYTES = 160 * 1024;
 // radix-pass LDS: sorted items (2 words) + bin ids + hist/start (u32) + per-bin bases (u64) = 80 KiB
 static constexpr size_t SORT_LDS = (size_t)PART_TILE * 16 + PART_TILE * 2 + 2 * NB1 * 4 + NB1 * 8;
+// the windowed passes (k_win1 / k_win2) sort tiles of WIN_TILE words: 8192 doubles the runs each
+// bin gets per tile (C3 pass 1: 16 words = 256 B instead of 128 B) in 152 KiB of LDS
+static constexpr int WIN_TILE = 8192;
+constexpr size_t sort_lds(int tile) { return (size_t)tile * 16 + tile * 2 + 2 * NB1 * 4 + NB1 * 8; }
+static_assert(sort_lds(WIN_TILE) + 64 <= 160 * 1024, "k_win LDS");
+static int win_tile() {
+    const char* e = getenv("KH_WTILE");
+    return (e && *e) ? atoi(e) : WIN_TILE;
+}
+static uint64_t win_blocks1(uint64_t n, int tile) { return (n + (uint64_t)T1 * tile - 1) / ((uint64_t)T1 * tile); }
+static uint64_t win_G(uint64_t n, int tile) {
+    const uint64_t tiles_per_bucket = (n / NB1 + tile - 1) / tile + 1;
+    return (tiles_per_bucket + 1) / 2;
+}
 
 PartPlan part_plan(uint64_t n) {
     PartPlan pl;
@@ -1207,10 +1221,10 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t& total, 
     return pre + x - v;
 }
 
-template <int W, int TB>
+template <int W, int TB, int TILE>
 __device__ __forceinline__ void load_words_tb(const uint64_t* __restrict__ words, uint64_t base, uint64_t end,
                                               uint64_t last, uint64_t* a, uint64_t* b) {
-    constexpr int IPT = PART_TILE / TB;
+    constexpr int IPT = TILE / TB;
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
         const uint64_t i = base + (uint64_t)j * TB + threadIdx.x;
@@ -1228,11 +1242,11 @@ __device__ __forceinline__ void load_words_tb(const uint64_t* __restrict__ words
     }
 }
 
-template <int W, int TB>
+template <int W, int TB, int TILE>
 __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ buf1, uint32_t bk, uint32_t CAP1,
                                                   const uint32_t* pre, uint64_t base, uint64_t end, uint64_t* a,
                                                   uint64_t* b) {
-    constexpr int IPT = PART_TILE / TB;
+    constexpr int IPT = TILE / TB;
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
         const uint32_t v = (uint32_t)(base + (uint64_t)j * TB + threadIdx.x);
@@ -1261,13 +1275,13 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
 // Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
 // with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
 // out[window(bin) + reserved + rank] (positions past cap -> overflow list).
-template <int W, int TB, int NB, class CtrF, class WinF, class NextF>
+template <int W, int TB, int NB, int TILE, class CtrF, class WinF, class NextF>
 __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, const uint32_t* bin, uint64_t* items,
                                                    uint16_t* sbin, uint32_t* hist, uint32_t* start, uint32_t* gpos,
                                                    uint32_t* wsum, CtrF counter, WinF window, uint32_t cap,
                                                    uint64_t* out, uint64_t* ovf, uint64_t ovf_cap,
                                                    unsigned long long* ctr, unsigned long long* stats, NextF next) {
-    constexpr int IPT = PART_TILE / TB;
+    constexpr int IPT = TILE / TB;
     static_assert(NB <= TB, "one bin per thread");
     if (threadIdx.x < NB) hist[threadIdx.x] = 0;
     lds_barrier();
@@ -1321,17 +1335,17 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
 }
 
 // pass 1 on words: bucket = top 9 hash bits, S1 windows per bucket (window blockIdx % S1)
-template <int W, int TB, bool COLLECT = false>
+template <int W, int TB, bool COLLECT, int TILE>
 __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restrict__ words, uint64_t n,
                                              uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1, uint64_t* ovf,
                                              uint64_t ovf_cap, unsigned long long* ctr,
                                              unsigned long long* stats, uint64_t* splits = nullptr,
                                              uint64_t splits_cap = 0) {
-    constexpr int IPT = PART_TILE / TB;
+    constexpr int IPT = TILE / TB;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
-    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + PART_TILE * 2);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + TILE * 2);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + TILE);
     uint32_t* start = hist + NB1;
     uint32_t* gpos = start + NB1;
     // block-scan partials in static LDS: 80 KB + a few bytes keeps these kernels at one block
@@ -1341,12 +1355,12 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
     uint32_t* scount = gpos + NB1;
     uint64_t* sbuf = reinterpret_cast<uint64_t*>(scount + 2);
     const uint32_t sub = blockIdx.x % S1;
-    const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
+    const uint64_t b0 = (uint64_t)blockIdx.x * T1 * TILE;
     uint64_t a[IPT], b[IPT];
     if (COLLECT && threadIdx.x == 0) *scount = 0;
-    load_words_tb<W, TB>(words, b0, min(b0 + PART_TILE, n), b0 < n ? b0 : 0, a, b);
+    load_words_tb<W, TB, TILE>(words, b0, min(b0 + TILE, n), b0 < n ? b0 : 0, a, b);
     for (int tt = 0; tt < T1; ++tt) {
-        const uint64_t base = b0 + (uint64_t)tt * PART_TILE;
+        const uint64_t base = b0 + (uint64_t)tt * TILE;
         if (base >= n) break;  // uniform
         uint32_t bin[IPT];
 #pragma unroll
@@ -1368,12 +1382,12 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
                 }
             }
         }
-        const uint64_t nbase = base + PART_TILE;
-        sort_reserve_write<W, TB, NB1>(
+        const uint64_t nbase = base + TILE;
+        sort_reserve_write<W, TB, NB1, TILE>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
             [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
             [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
-            [&]() { load_words_tb<W, TB>(words, nbase, (tt + 1 < T1) ? min(nbase + PART_TILE, n) : nbase, base, a, b); });
+            [&]() { load_words_tb<W, TB, TILE>(words, nbase, (tt + 1 < T1) ? min(nbase + TILE, n) : nbase, base, a, b); });
     }
     if (COLLECT) {  // this block's splitters: one list reservation
         __syncthreads();
@@ -1392,17 +1406,17 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
 }
 
 // pass 2: next 8 hash bits within bucket bk, into the region windows (RC words each)
-template <int W, int TB, bool WIN>
+template <int W, int TB, bool WIN, int TILE>
 __global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restrict__ buf1, uint64_t n,
                                              const uint64_t* off1, uint64_t G, uint32_t RC, uint32_t* rcnt,
                                              uint64_t* buf2, uint64_t* ovf, uint64_t ovf_cap,
                                              unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
                                              const uint32_t* wcnt) {
-    constexpr int IPT = PART_TILE / TB;
+    constexpr int IPT = TILE / TB;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
-    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + PART_TILE * 2);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + PART_TILE);
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + TILE * 2);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + TILE);
     uint32_t* start = hist + NB1;
     uint32_t* gpos = start + NB1;
     __shared__ uint32_t wsum[TB / 64];  // static: one block per CU (see k_win1)
@@ -1420,23 +1434,23 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restri
     }
     uint64_t a[IPT], b[IPT];
     auto load = [&](uint64_t t) {
-        const uint64_t e_ = t < e ? min(t + PART_TILE, e) : t;
+        const uint64_t e_ = t < e ? min(t + TILE, e) : t;
         if (WIN)
-            load_words_win_tb<W, TB>(buf1, bk, CAP1, pre, t, e_, a, b);
+            load_words_win_tb<W, TB, TILE>(buf1, bk, CAP1, pre, t, e_, a, b);
         else
-            load_words_tb<W, TB>(buf1, t, e_, s, a, b);
+            load_words_tb<W, TB, TILE>(buf1, t, e_, s, a, b);
     };
-    load(s + (uint64_t)g * PART_TILE);
-    for (uint64_t t = s + (uint64_t)g * PART_TILE; t < e; t += G * PART_TILE) {
+    load(s + (uint64_t)g * TILE);
+    for (uint64_t t = s + (uint64_t)g * TILE; t < e; t += G * TILE) {
         uint32_t bin[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
             bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - RBITS)) & (NB2 - 1);
-        sort_reserve_write<W, TB, NB2>(
+        sort_reserve_write<W, TB, NB2, TILE>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
             [&](uint32_t q) { return &rcnt[(bk << B2) | q]; },
             [&](uint32_t q) { return (uint64_t)((bk << B2) | q) * RC; }, RC, buf2, ovf, ovf_cap, ctr, stats,
-            [&]() { load(t + G * PART_TILE); });
+            [&]() { load(t + G * TILE); });
     }
 }
 
@@ -1448,6 +1462,54 @@ static int win_tb() {
 template <class K>
 static hipError_t allow_lds(K kernel, size_t bytes) {
     return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+// windowed pass 1 / pass 2 launches at tile size TILE (KH_WTILE = 4096 | 8192)
+template <int W, int TILE>
+static hipError_t win1_launch_t(const KParams& p, const uint64_t* words, uint64_t n, uint32_t CAP1, uint32_t* wcnt,
+                                const PartBuffers& B, uint64_t ovf_cap, unsigned long long* ctr,
+                                unsigned long long* stats, hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap) {
+    constexpr size_t L = sort_lds(TILE);
+    const unsigned nb = (unsigned)win_blocks1(n, TILE);
+    hipError_t e;
+    if (wsplits) {
+        if ((e = allow_lds(k_win1<W, 512, true, TILE>, L)) != hipSuccess) return e;
+        k_win1<W, 512, true, TILE><<<nb, 512, L, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow, ovf_cap, ctr,
+                                                      stats, wsplits, wsplits_cap);
+    } else {
+        if ((e = allow_lds(k_win1<W, 512, false, TILE>, L)) != hipSuccess) return e;
+        k_win1<W, 512, false, TILE><<<nb, 512, L, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow, ovf_cap, ctr,
+                                                       stats);
+    }
+    return hipSuccess;
+}
+template <int W>
+static hipError_t win1_launch(const KParams& p, const uint64_t* words, uint64_t n, uint32_t CAP1, uint32_t* wcnt,
+                              const PartBuffers& B, uint64_t ovf_cap, unsigned long long* ctr,
+                              unsigned long long* stats, hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap) {
+    return win_tile() == PART_TILE
+               ? win1_launch_t<W, PART_TILE>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, wsplits, wsplits_cap)
+               : win1_launch_t<W, WIN_TILE>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, wsplits, wsplits_cap);
+}
+template <int W, bool WIN, int TILE>
+static hipError_t win2_launch_t(const KParams& p, const PartBuffers& B, uint64_t n, uint32_t RC, uint32_t* rcnt,
+                                uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
+                                const uint32_t* wcnt, hipStream_t s) {
+    constexpr size_t L = sort_lds(TILE);
+    const uint64_t G = win_G(n, TILE);
+    hipError_t e;
+    if ((e = allow_lds(k_win2<W, 512, WIN, TILE>, L)) != hipSuccess) return e;
+    k_win2<W, 512, WIN, TILE><<<(unsigned)(NB1 * G), 512, L, s>>>(p, B.buf1, n, B.off1, G, RC, rcnt, B.buf2,
+                                                                  B.overflow, ovf_cap, ctr, stats, CAP1, wcnt);
+    return hipSuccess;
+}
+template <int W, bool WIN>
+static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n, uint32_t RC, uint32_t* rcnt,
+                              uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
+                              const uint32_t* wcnt, hipStream_t s) {
+    return win_tile() == PART_TILE
+               ? win2_launch_t<W, WIN, PART_TILE>(p, B, n, RC, rcnt, ovf_cap, ctr, stats, CAP1, wcnt, s)
+               : win2_launch_t<W, WIN, WIN_TILE>(p, B, n, RC, rcnt, ovf_cap, ctr, stats, CAP1, wcnt, s);
 }
 
 template <int W, bool REC>
@@ -1473,10 +1535,6 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         if ((e = allow_lds(k_part_build<W>, LDS_BYTES)) != hipSuccess) return e;
         if ((e = allow_lds(k_part_build_pf<W, 4>, LDS_BYTES)) != hipSuccess) return e;
         if ((e = allow_lds(k_part_build_pf<W, 12>, LDS_BYTES)) != hipSuccess) return e;
-        if ((e = allow_lds(k_win1<W, 512>, SORT_LDS)) != hipSuccess) return e;
-        if ((e = allow_lds(k_win1<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
-        if ((e = allow_lds(k_win2<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
-        if ((e = allow_lds(k_win2<W, 512, false>, SORT_LDS)) != hipSuccess) return e;
         attrs = true;
     }
     const PartPlan pl = part_plan(n);
@@ -1520,13 +1578,9 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
                                                        B.overflow, part_overflow_cap(n), ctr, stats);
         else if ((mode1 == 4 || (mode1 == 0 && !REC)) && win_tb() == 512)
         {
-            if (wsplits)
-                k_win1<W, 512, true><<<nb1, 512, SORT_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
-                                                                part_overflow_cap(n), ctr, stats, wsplits,
-                                                                wsplits_cap);
-            else
-                k_win1<W, 512><<<nb1, 512, SORT_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
-                                                          part_overflow_cap(n), ctr, stats);
+            if ((e = win1_launch<W>(p, words, n, CAP1, wcnt, B, part_overflow_cap(n), ctr, stats, s, wsplits,
+                                    wsplits_cap)) != hipSuccess)
+                return e;
         }
         else if (mode1 == 4)
             k_part1_fused<W, false><<<nb1, PB, SORT_LDS, s>>>(p, nullptr, words, n, CAP1, wcnt, B.buf1, nullptr,
@@ -1563,15 +1617,16 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (res2) {
         RC = part_region_cap(n);
         if ((e = hipMemsetAsync(rcnt, 0, (size_t)NREG * 4, s)) != hipSuccess) return e;
-        if (win_tb() == 512 && CAP1)
-            k_win2<W, 512, true><<<nb2, 512, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.G, RC, rcnt, B.buf2,
-                                                           B.overflow, part_overflow_cap(n), ctr, stats, CAP1,
-                                                           wcnt);
-        else if (win_tb() == 512)
-            k_win2<W, 512, false><<<nb2, 512, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.G, RC, rcnt, B.buf2,
-                                                            B.overflow, part_overflow_cap(n), ctr, stats, 0,
-                                                            nullptr);
-        else if (CAP1)
+        if (win_tb() == 512 && CAP1) {
+            if ((e = win2_launch<W, true>(p, B, n, RC, rcnt, part_overflow_cap(n), ctr, stats, CAP1, wcnt, s)) !=
+                hipSuccess)
+                return e;
+        } else if (win_tb() == 512) {  // pass-1 exact offsets: the grid of part_plan
+            if ((e = allow_lds(k_win2<W, 512, false, PART_TILE>, SORT_LDS)) != hipSuccess) return e;
+            k_win2<W, 512, false, PART_TILE><<<nb2, 512, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.G, RC, rcnt,
+                                                                        B.buf2, B.overflow, part_overflow_cap(n),
+                                                                        ctr, stats, 0, nullptr);
+        } else if (CAP1)
             k_part2_res<W, true><<<nb2, PB, SORT_LDS, s>>>(p, B.buf1, n, B.off1, pl.G, RC, rcnt, B.buf2,
                                                           B.overflow, part_overflow_cap(n), ctr, stats, CAP1,
                                                           wcnt);
@@ -1610,9 +1665,6 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     hipError_t e;
     if ((e = allow_lds(k_part1_fused<W, false>, SORT_LDS)) != hipSuccess) return e;
     if ((e = allow_lds(k_part2_res<W, true>, SORT_LDS)) != hipSuccess) return e;
-    if ((e = allow_lds(k_win1<W, 512>, SORT_LDS)) != hipSuccess) return e;
-    if ((e = allow_lds(k_win1<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
-    if ((e = allow_lds(k_win2<W, 512, true>, SORT_LDS)) != hipSuccess) return e;
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(B.hist1);
     uint32_t* rcnt = reinterpret_cast<uint32_t*>(B.hist2);
     if (first) {
@@ -1624,17 +1676,12 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(total);
     if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if (win_tb() == 512) {
-        if (wsplits)
-            k_win1<W, 512, true><<<(unsigned)pl.nb1, 512, SORT_LDS, s>>>(p, words, m, CAP1, wcnt, B.buf1,
-                                                                         B.overflow, part_overflow_cap(total), ctr,
-                                                                         stats, wsplits, wsplits_cap);
-        else
-            k_win1<W, 512><<<(unsigned)pl.nb1, 512, SORT_LDS, s>>>(p, words, m, CAP1, wcnt, B.buf1, B.overflow,
-                                                                   part_overflow_cap(total), ctr, stats);
-        k_win2<W, 512, true><<<(unsigned)(NB1 * pl.G), 512, SORT_LDS, s>>>(p, B.buf1, m, B.off1, pl.G, RC, rcnt,
-                                                                           B.buf2, B.overflow,
-                                                                           part_overflow_cap(total), ctr, stats,
-                                                                           CAP1, wcnt);
+        if ((e = win1_launch<W>(p, words, m, CAP1, wcnt, B, part_overflow_cap(total), ctr, stats, s, wsplits,
+                                wsplits_cap)) != hipSuccess)
+            return e;
+        if ((e = win2_launch<W, true>(p, B, m, RC, rcnt, part_overflow_cap(total), ctr, stats, CAP1, wcnt, s)) !=
+            hipSuccess)
+            return e;
         return hipGetLastError();
     }
     k_part1_fused<W, false><<<(unsigned)pl.nb1, PB, SORT_LDS, s>>>(p, nullptr, words, m, CAP1, wcnt, B.buf1,
