@@ -173,8 +173,7 @@ def main():
                         "(4-lane block probes)"},
             "note": "achieved = algorithmic bytes (2*sizeof(kmer_pair) per lookup) / HIP-event "
                     "duration of k_walk" + (f"; traffic from {tsrc}" if tsrc else "")}
-    insert_pipe = {"kernels": "k_part1_convert, k_part1_fused, k_part2_res, k_part_build_pf, "
-                              "k_insert_overflow",
+    insert_pipe = {"kernels": "k_win1_rec (records pass 1), k_win2, k_part_build_pf, k_insert_overflow",
                    "ms": ins_ms, "achieved_alg_GBs": n * b_alg / (ins_ms / 1e3) / 1e9,
                    "inserts_per_s": n / (ins_ms / 1e3),
                    "traffic": traffic.get("insert_pipeline") if traffic else None}

@@ -102,13 +102,16 @@ uint64_t part_buf2_words(const KParams& p, uint64_t n) {
 // registers inside the windowed pass, 4 convfused = records -> words (k_part1_convert without
 // its histogram) then the windowed pass on the words. Defaults (C3, MI355X): records ->
 // convfused (1.45 + 1.91 ms; convert 1.45 + scans 0.42 + scatter 2.09; fused/direct parse in
-// the sort kernel 5.5-5.7); words -> fused.
+// the sort kernel 5.5-5.7); 5 recwin = the windowed pass reading the records itself (coalesced
+// 16-B blocks, records gathered by cross-lane shuffles; k with 13 or 5 packed bytes, else 4):
+// 2.56 ms vs 1.21 + 1.65-1.82 at C3, the default for records; words -> fused.
 static int p1_mode(bool rec) {
     const char* e = getenv("KH_P1");
-    if (!e || !*e) return rec ? 4 : 0;
+    if (!e || !*e) return rec ? 5 : 0;
     if (!strcmp(e, "fused")) return 0;
     if (!strcmp(e, "direct")) return 3;
     if (!strcmp(e, "convfused")) return 4;
+    if (!strcmp(e, "recwin")) return 5;
     return !strcmp(e, "rec") ? 2 : 1;
 }
 static bool p2_res() {
@@ -1405,6 +1408,111 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
     }
 }
 
+// pass 1 on records (KH_P1=recwin, k with a compile-time packed size PK): the windowed pass 1
+// reading the reference records itself — one unaligned 16-B load per record (a record is PK + 2
+// <= 16 bytes), parsed in registers after the tile's loads land, with the start / splitter bits
+// of the record pass — instead of a record -> word copy and a second pass over the copy.
+template <int PK>
+__device__ __forceinline__ void load_record16(const uint8_t* __restrict__ recs, uint64_t i, uint64_t n,
+                                              uint64_t& x0, uint64_t& x1) {
+    if (i + 1 < n) {  // the 16 bytes stay inside the next record
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        u64x2 v;
+        __builtin_memcpy(&v, recs + i * (uint64_t)(PK + 2), 16);
+        x0 = v.x;
+        x1 = v.y;
+    } else {
+        load_record_regs(recs, i, (uint32_t)(PK + 2), x0, x1);
+    }
+}
+
+template <int W, int TB, int TILE, int PK>
+__global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
+                                                 uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1,
+                                                 uint64_t* start_mask, uint64_t* split_mask, uint64_t* ovf,
+                                                 uint64_t ovf_cap, unsigned long long* ctr,
+                                                 unsigned long long* stats) {
+    constexpr int IPT = TILE / TB;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* items = smem;
+    uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + TILE * 2);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + TILE);
+    uint32_t* start = hist + NB1;
+    uint32_t* gpos = start + NB1;
+    __shared__ uint32_t wsum[TB / 64];
+    const uint32_t sub = blockIdx.x % S1;
+    const uint64_t b0 = (uint64_t)blockIdx.x * T1 * TILE;
+    // a wave's 64 records are one contiguous run of 64 * R bytes: lane l loads the run's l-th
+    // aligned 16-B block (coalesced, no straddling), and each lane later gathers the two blocks
+    // holding its record by cross-lane shuffles
+    constexpr uint32_t R = PK + 2;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nbytes = n * (uint64_t)R;
+    uint64_t a[IPT], b[IPT];  // raw 16-B blocks until parsed, then the words
+    auto load = [&](uint64_t base, uint64_t end) {
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t r0 = base + (uint64_t)j * TB + (threadIdx.x & ~63u);  // the wave's first record
+            const uint64_t g = ((r0 * R) & ~15ull) + 16ull * lane;
+            a[j] = b[j] = 0;
+            if (r0 < end && lane < 62 && g < nbytes) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(recs + g);
+                a[j] = v.x;
+                b[j] = v.y;
+            }
+        }
+    };
+    load(b0, min(b0 + TILE, n));
+    for (int tt = 0; tt < T1; ++tt) {
+        const uint64_t base = b0 + (uint64_t)tt * TILE;
+        if (base >= n) break;  // uniform
+        uint32_t bin[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t s0 = base + (uint64_t)j * TB;
+            const bool valid = s0 + threadIdx.x < n;
+            Key k{0, 0};
+            uint32_t ext = 0;
+            {
+                const uint64_t r0 = s0 + (threadIdx.x & ~63u);
+                const uint32_t off = (uint32_t)((r0 * R) & 15u) + lane * R;  // from the first block
+                const int blk = (int)(off >> 4);
+                const uint32_t o = off & 15u;
+                const uint64_t p0 = __shfl(a[j], blk, 64), p1 = __shfl(b[j], blk, 64);
+                const uint64_t q0 = __shfl(a[j], blk + 1, 64), q1 = __shfl(b[j], blk + 1, 64);
+                uint64_t w0 = p0, w1 = p1, w2 = q0;
+                if (o >= 8u) {
+                    w0 = p1;
+                    w1 = q0;
+                    w2 = q1;
+                }
+                const uint32_t sh = (o & 7u) * 8u;
+                if (valid) parse_record_regs_t<PK>(funnel64(w0, w1, sh), funnel64(w1, w2, sh), p.pad, k, ext);
+            }
+            const uint64_t hk = key_hash(k);
+            if (s0 < n) {  // uniform: one start / splitter word per 64 consecutive records
+                const bool is_start = valid && ext_bwd(ext) == EXT_F;
+                const uint64_t bal = __ballot(is_start);
+                const uint64_t sb = __ballot(valid && !is_start && is_splitter(hk, p));
+                const uint64_t wb = s0 + (threadIdx.x & ~63u);
+                if ((threadIdx.x & 63) == 0 && wb < n) {
+                    if (start_mask) start_mask[wb >> 6] = bal;
+                    if (split_mask) split_mask[wb >> 6] = sb;
+                }
+            }
+            a[j] = valid ? slot_w0(k, ext, p) : EMPTY;
+            b[j] = (valid && W == 2) ? k.lo : 0;
+            bin[j] = (uint32_t)(hk >> (64 - B1));
+        }
+        const uint64_t nbase = base + TILE;
+        sort_reserve_write<W, TB, NB1, TILE>(
+            a, b, bin, items, sbin, hist, start, gpos, wsum,
+            [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
+            [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
+            [&]() { load(nbase, (tt + 1 < T1) ? min(nbase + TILE, n) : nbase); });
+    }
+}
+
 // pass 2: next 8 hash bits within bucket bk, into the region windows (RC words each)
 template <int W, int TB, bool WIN, int TILE>
 __global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restrict__ buf1, uint64_t n,
@@ -1491,6 +1599,31 @@ static hipError_t win1_launch(const KParams& p, const uint64_t* words, uint64_t 
                ? win1_launch_t<W, PART_TILE>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, wsplits, wsplits_cap)
                : win1_launch_t<W, WIN_TILE>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, wsplits, wsplits_cap);
 }
+template <int W, int PK, int TILE>
+static hipError_t win1_rec_launch_t(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t CAP1,
+                                    uint32_t* wcnt, const PartBuffers& B, uint64_t* start_mask,
+                                    uint64_t* split_mask, uint64_t ovf_cap, unsigned long long* ctr,
+                                    unsigned long long* stats, hipStream_t s) {
+    constexpr size_t L = sort_lds(TILE);
+    hipError_t e;
+    if ((e = allow_lds(k_win1_rec<W, 512, TILE, PK>, L)) != hipSuccess) return e;
+    k_win1_rec<W, 512, TILE, PK><<<(unsigned)win_blocks1(n, TILE), 512, L, s>>>(
+        p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask, B.overflow, ovf_cap, ctr, stats);
+    return hipSuccess;
+}
+template <int W>
+static hipError_t win1_rec_launch(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t CAP1,
+                                  uint32_t* wcnt, const PartBuffers& B, uint64_t* start_mask, uint64_t* split_mask,
+                                  uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats,
+                                  hipStream_t s) {
+    constexpr int PK = W == 2 ? 13 : 5;
+    const char* t = getenv("KH_RTILE");
+    if (t && atoi(t) == PART_TILE)
+        return win1_rec_launch_t<W, PK, PART_TILE>(p, recs, n, CAP1, wcnt, B, start_mask, split_mask, ovf_cap,
+                                                   ctr, stats, s);
+    return win1_rec_launch_t<W, PK, WIN_TILE>(p, recs, n, CAP1, wcnt, B, start_mask, split_mask, ovf_cap, ctr,
+                                              stats, s);
+}
 template <int W, bool WIN, int TILE>
 static hipError_t win2_launch_t(const KParams& p, const PartBuffers& B, uint64_t n, uint32_t RC, uint32_t* rcnt,
                                 uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
@@ -1543,6 +1676,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (mode1 == 3 && (!REC || p.R > 16)) mode1 = REC ? 1 : 0;  // direct parse: records of <= 16 B
     if (mode1 == 4 && !REC) mode1 = 0;
     const bool direct1 = mode1 == 3;
+    if (mode1 == 5 && !(REC && ((p.P == 13 && W == 2) || (p.P == 5 && W == 1)))) mode1 = REC ? 4 : 0;
     if (mode1 == 4) {  // records -> words (input order) in buf2, then the windowed pass 1 on them
         if (p.P == 13 && W == 2)
             k_part1_convert<W, 13><<<nb1, PB, 0, s>>>(p, recs, n, B.buf2, nullptr, start_mask, split_mask);
@@ -1556,7 +1690,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
             after_records = nullptr;
         }
     }
-    const bool fused1 = mode1 == 0 || direct1 || mode1 == 4, rec1 = REC && mode1 == 2;
+    const bool fused1 = mode1 == 0 || direct1 || mode1 == 4 || mode1 == 5, rec1 = REC && mode1 == 2;
     const bool res2 = fused1 || p2_res();
     if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
     uint32_t CAP1 = 0;
@@ -1564,7 +1698,11 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (fused1) {
         CAP1 = part_win1_cap(n);
         if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
-        if (direct1 && p.P == 13 && W == 2 && !getenv("KH_NOMASK"))
+        if (mode1 == 5) {
+            if ((e = win1_rec_launch<W>(p, recs, n, CAP1, wcnt, B, start_mask, split_mask, part_overflow_cap(n),
+                                        ctr, stats, s)) != hipSuccess)
+                return e;
+        } else if (direct1 && p.P == 13 && W == 2 && !getenv("KH_NOMASK"))
             k_part1_direct<W, 13><<<nb1, PB, SORT_LDS, s>>>(p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask,
                                                            B.overflow, part_overflow_cap(n), ctr, stats);
         else if (direct1 && p.P == 5 && W == 1)

@@ -368,7 +368,7 @@ def test_gpu_walk_group_missing_kmer(monkeypatch, G):
 
 # ---- partitioned-build pass variants (KH_P1: record re-parse / word copy; KH_P2: region windows
 # with atomic reservations / histogram + scan) ----------------------------------------------------
-@pytest.mark.parametrize("p1,p2", [("convfused", "res"), ("direct", "res"), ("fused", "res"), ("rec", "res"),
+@pytest.mark.parametrize("p1,p2", [("recwin", "res"), ("convfused", "res"), ("direct", "res"), ("fused", "res"), ("rec", "res"),
                                    ("convert", "res"), ("rec", "scan"), ("convert", "scan")])
 @pytest.mark.parametrize("k,n,batches", [(51, 3_000_000, 1), (60, 2_000_000, 2), (19, 2_000_000, 1),
                                          (29, 1_500_000, 1)])
@@ -383,7 +383,8 @@ def test_gpu_part_pass_variants(monkeypatch, p1, p2, k, n, batches):
     assert s["n_dup"] == 0 and s["n_full"] == 0 and s["n_inserted"] == n
 
 
-@pytest.mark.parametrize("p1,p2", [("direct", "res"), ("fused", "res"), ("convert", "res"), ("convert", "scan")])
+@pytest.mark.parametrize("p1,p2", [("recwin", "res"), ("convfused", "res"), ("direct", "res"), ("fused", "res"),
+                                   ("convert", "res"), ("convert", "scan")])
 def test_gpu_part_pass_variants_duplicates(monkeypatch, p1, p2):
     monkeypatch.setenv("KH_INSERT", "part")
     monkeypatch.setenv("KH_P1", p1)

@@ -16,7 +16,7 @@ import os
 import sys
 
 KERNELS = {"k_insert": ("k_insert<",), "k_walk": ("k_walk<", "k_walk_g<", "k_walk_q<"),
-           "k_win1": ("k_win1<",), "k_win2": ("k_win2<",),
+           "k_win1": ("k_win1<",), "k_win1_rec": ("k_win1_rec<",), "k_win2": ("k_win2<",),
            "k_part1_convert": ("k_part1_convert<",), "k_part1_fused": ("k_part1_fused<",),
            "k_part1_scatter": ("k_part1_scatter<",), "k_part2_hist": ("k_part2_hist<",),
            "k_part2_scatter": ("k_part2_scatter<",), "k_part2_res": ("k_part2_res<",),
@@ -24,7 +24,7 @@ KERNELS = {"k_insert": ("k_insert<",), "k_walk": ("k_walk<", "k_walk_g<", "k_wal
            "membench_gather16": ("k_gather16",), "membench_chase16": ("k_chase16",),
            "membench_chase64q": ("k_chasegILi4",), "membench_chase128o": ("k_chasegILi8",)}
 # kernels of the insert pipeline (whichever of them ran)
-PIPELINE = ["k_part1_convert", "k_part1_fused", "k_win1", "k_part1_scatter", "k_part2_hist", "k_part2_scatter",
+PIPELINE = ["k_part1_convert", "k_part1_fused", "k_win1", "k_win1_rec", "k_part1_scatter", "k_part2_hist", "k_part2_scatter",
             "k_part2_res", "k_win2", "k_part_build", "k_insert_overflow"]
 # random-access kernels: FETCH_SIZE is NOT doubled (the 1/2 correction is for wide coalesced
 # streaming reads); their requests are calibrated against tools/membench (random 16-B loads)
