@@ -169,6 +169,45 @@ __device__ __forceinline__ void load_slot(const uint64_t* slots, uint64_t s, uin
     }
 }
 
+// ---- record loads straight from global memory (aligned 16-B loads, parse in registers) ----
+// Record parse straight from global memory, no LDS staging (records of R <= 16 bytes, K <= 56):
+// lane i loads the aligned 16-B chunk holding record i's first byte and, when the record runs
+// past it, the next one; the 15-B record is funnel-shifted out of the 32-B window in registers.
+// Consecutive lanes read overlapping chunks, so a wave's loads coalesce into ~R*64/16 requests.
+__device__ __forceinline__ uint64_t funnel64(uint64_t lo, uint64_t hi, uint32_t sh) {  // sh in [0,64)
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+__device__ __forceinline__ void load_record_regs(const uint8_t* __restrict__ recs, uint64_t i, uint32_t R,
+                                                 uint64_t& x0, uint64_t& x1) {
+    const uint64_t a = i * R;
+    const uint32_t o = (uint32_t)(a & 15u);
+    const ulonglong2 c0 = *reinterpret_cast<const ulonglong2*>(recs + (a - o));
+    ulonglong2 c1 = make_ulonglong2(0, 0);
+    if (o + R > 16u) c1 = *reinterpret_cast<const ulonglong2*>(recs + (a - o) + 16);
+    uint64_t w0 = c0.x, w1 = c0.y, w2 = c1.x;
+    if (o >= 8u) {
+        w0 = w1;
+        w1 = w2;
+        w2 = c1.y;
+    }
+    const uint32_t sh = (o & 7u) * 8u;
+    x0 = funnel64(w0, w1, sh);
+    x1 = funnel64(w1, w2, sh);
+}
+
+// bytes 0..15 of a record (little-endian in x0, x1) -> key and extension codes (parse_record)
+__device__ __forceinline__ void parse_record_regs(uint64_t x0, uint64_t x1, const KParams& p, Key& k,
+                                                  uint32_t& ext) {
+    const unsigned __int128 be = ((unsigned __int128)__builtin_bswap64(x0) << 64) | __builtin_bswap64(x1);
+    const unsigned __int128 B = (be >> (8 * (16 - p.P))) >> (2 * p.pad);
+    k.lo = (uint64_t)B & LO_MASK;
+    k.hi = (uint64_t)(B >> 62);
+    const unsigned __int128 xx = ((unsigned __int128)x1 << 64) | x0;
+    const uint32_t e = (uint32_t)(xx >> (8 * p.P)) & 0xFFFFu;
+    ext = base_code((uint8_t)e) | (base_code((uint8_t)(e >> 8)) << 3);
+}
+
 template <int W>
 __device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p, uint64_t* slots,
                                            uint64_t cap, unsigned long long* stats) {

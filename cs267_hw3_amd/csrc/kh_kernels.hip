@@ -86,7 +86,13 @@ __global__ __launch_bounds__(BLOCK) void k_scatter_starts(KParams p, const uint8
     auto put = [&](uint64_t i, uint64_t o) {
         Key k;
         uint32_t ext;
-        parse_record(recs + i * (uint64_t)p.R, p, k, ext);
+        if (p.R <= 16) {  // uniform: two aligned 16-B loads instead of R byte loads
+            uint64_t x0, x1;
+            load_record_regs(recs, i, (uint32_t)p.R, x0, x1);
+            parse_record_regs(x0, x1, p, k, ext);
+        } else {
+            parse_record(recs + i * (uint64_t)p.R, p, k, ext);
+        }
         starts[o * W] = slot_w0(k, ext, p);
         if (W == 2) starts[o * W + 1] = k.lo;
     };
