@@ -1182,6 +1182,24 @@ __device__ __forceinline__ void stage_records(const uint8_t* recs, uint64_t sub,
     for (uint32_t x = (nvec << 4) + threadIdx.x; x < bytes; x += BLOCK) st[x] = recs[sub * R + x];
 }
 
+// Record sub + threadIdx.x (< cnt) -> key + ext: two aligned 16-B loads and a register parse for
+// records of <= 16 bytes, else through the LDS stage (whole block).
+__device__ __forceinline__ void load_parse_record(const KParams& p, const uint8_t* __restrict__ recs, uint64_t sub,
+                                                  uint32_t cnt, uint8_t* st, Key& k, uint32_t& ext) {
+    if (p.R <= 16) {  // uniform
+        if (threadIdx.x < cnt) {
+            uint64_t x0, x1;
+            load_record_regs(recs, sub + threadIdx.x, (uint32_t)p.R, x0, x1);
+            parse_record_regs(x0, x1, p, k, ext);
+        }
+    } else {
+        __syncthreads();
+        stage_records(recs, sub, cnt, (uint32_t)p.R, st);
+        __syncthreads();
+        if (threadIdx.x < cnt) parse_record(st + threadIdx.x * p.R, p, k, ext);
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
                                                      uint32_t P, uint8_t* own, uint64_t* hist,
                                                      uint64_t* start_mask) {
@@ -1193,17 +1211,16 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* _
         const uint64_t sub = b0 + (uint64_t)j * BLOCK;
         if (sub >= n) break;  // uniform
         const uint32_t cnt = n - sub < (uint64_t)BLOCK ? (uint32_t)(n - sub) : (uint32_t)BLOCK;
-        __syncthreads();
-        stage_records(recs, sub, cnt, (uint32_t)p.R, st);
-        __syncthreads();
+        Key k{0, 0};
+        uint32_t ext = 0;
+        load_parse_record(p, recs, sub, cnt, st, k, ext);
         if (threadIdx.x < cnt) {
-            const Key k = key_from_packed(st + threadIdx.x * p.R, p);
             const uint32_t q = owner_key(k, p, P);
             own[sub + threadIdx.x] = (uint8_t)q;
             atomicAdd(&h[q], 1u);
         }
         if (start_mask) {  // kmer_hash.cpp:27-31 start bits, same pass (ROUTE_TILE is 64-aligned)
-            const uint64_t bal = __ballot(threadIdx.x < cnt && st[threadIdx.x * p.R + p.P] == 'F');
+            const uint64_t bal = __ballot(threadIdx.x < cnt && ext_bwd(ext) == EXT_F);
             const uint64_t wb = sub + (threadIdx.x & ~63u);
             if ((threadIdx.x & 63) == 0 && wb < n) start_mask[wb >> 6] = bal;
         }
@@ -1224,13 +1241,10 @@ __global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p, const uint8_
         const uint64_t sub = b0 + (uint64_t)j * BLOCK;
         if (sub >= n) break;  // uniform
         const uint32_t cnt = n - sub < (uint64_t)BLOCK ? (uint32_t)(n - sub) : (uint32_t)BLOCK;
-        __syncthreads();
-        stage_records(recs, sub, cnt, (uint32_t)p.R, st);
-        __syncthreads();
+        Key k{0, 0};
+        uint32_t ext = 0;
+        load_parse_record(p, recs, sub, cnt, st, k, ext);
         if (threadIdx.x < cnt) {
-            Key k;
-            uint32_t ext;
-            parse_record(st + threadIdx.x * p.R, p, k, ext);
             const uint32_t q = own[sub + threadIdx.x];
             const uint64_t d = off[(uint64_t)q * nb + blockIdx.x] + atomicAdd(&h[q], 1u);
             if (W == 2)
