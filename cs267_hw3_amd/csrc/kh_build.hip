@@ -1403,7 +1403,8 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __res
     uint32_t* gpos = start + NB1;
     __shared__ uint32_t wsum[TB / 64];
     const uint32_t sub = blockIdx.x % S1;
-    const uint64_t b0 = (uint64_t)blockIdx.x * T1 * TILE;
+    // persistent blocks: tile t, t + gridDim.x, ...; the next tile's loads are always in flight
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
     // a wave's 64 records are one contiguous run of 64 * R bytes: lane l loads the run's l-th
     // aligned 16-B block (coalesced, no straddling), and each lane later gathers the two blocks
     // holding its record by cross-lane shuffles
@@ -1424,10 +1425,10 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __res
             }
         }
     };
-    load(b0, min(b0 + TILE, n));
-    for (int tt = 0; tt < T1; ++tt) {
-        const uint64_t base = b0 + (uint64_t)tt * TILE;
-        if (base >= n) break;  // uniform
+    uint64_t t = blockIdx.x;
+    if (t < ntiles) load(t * TILE, min(t * TILE + TILE, n));
+    for (; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * TILE;
         uint32_t bin[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
@@ -1466,12 +1467,12 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __res
             b[j] = (valid && W == 2) ? k.lo : 0;
             bin[j] = (uint32_t)(hk >> (64 - B1));
         }
-        const uint64_t nbase = base + TILE;
+        const uint64_t nt = t + gridDim.x, nbase = nt * TILE;
         sort_reserve_write<W, TB, NB1, TILE>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
             [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
             [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
-            [&]() { load(nbase, (tt + 1 < T1) ? min(nbase + TILE, n) : nbase); });
+            [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
     }
 }
 
@@ -1569,7 +1570,21 @@ static hipError_t win1_rec_launch_t(const KParams& p, const uint8_t* recs, uint6
     constexpr size_t L = sort_lds(TILE);
     hipError_t e;
     if ((e = allow_lds(k_win1_rec<W, 512, TILE, PK>, L)) != hipSuccess) return e;
-    k_win1_rec<W, 512, TILE, PK><<<(unsigned)win_blocks1(n, TILE), 512, L, s>>>(
+    // persistent: a few blocks per CU slot (one 152-KiB block fits a CU), a multiple of S1
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const char* gb = getenv("KH_RWIN_BLOCKS");
+    uint64_t grid = gb ? (uint64_t)atoi(gb) : (uint64_t)ncu;
+    grid = (grid + S1 - 1) / S1 * S1;
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
+    if (grid > ntiles) grid = (ntiles + S1 - 1) / S1 * S1;
+    if (grid == 0) grid = S1;
+    k_win1_rec<W, 512, TILE, PK><<<(unsigned)grid, 512, L, s>>>(
         p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask, B.overflow, ovf_cap, ctr, stats);
     return hipSuccess;
 }
@@ -1591,7 +1606,8 @@ static hipError_t win2_launch_t(const KParams& p, const PartBuffers& B, uint64_t
                                 uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
                                 const uint32_t* wcnt, hipStream_t s) {
     constexpr size_t L = sort_lds(TILE);
-    const uint64_t G = win_G(n, TILE);
+    uint64_t G = win_G(n, TILE);
+    if (const char* e = getenv("KH_WIN2_G")) G = (uint64_t)atoi(e) > 0 ? (uint64_t)atoi(e) : G;
     hipError_t e;
     if ((e = allow_lds(k_win2<W, 512, WIN, TILE>, L)) != hipSuccess) return e;
     k_win2<W, 512, WIN, TILE><<<(unsigned)(NB1 * G), 512, L, s>>>(p, B.buf1, n, B.off1, G, RC, rcnt, B.buf2,
