@@ -526,17 +526,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __r
             w0[j] = EMPTY;
             w1[j] = 0;
             if (sj[j] != ~0ull && my < cap) {
-                // non-temporal: a random 64-B block of a 6.4 GB table is not re-read before it
-                // would be evicted; the hint keeps the probes from churning the caches (C3 walk
-                // 6.00 -> 5.72 ms)
-                if (W == 2) {
-                    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-                    const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(slots + 2 * my));
-                    w0[j] = v.x;
-                    w1[j] = v.y;
-                } else {
-                    w0[j] = __builtin_nontemporal_load(slots + my);
-                }
+                load_slot_nt<W>(slots, my, w0[j], w1[j]);
             }
         }
         uint64_t kh_[4], kl_[4];
@@ -741,7 +731,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_g(KParams p, const uint64_t* __r
             const uint64_t my = (s[i] & ~(uint64_t)(G - 1)) + q;
             w0[i] = EMPTY;
             w1[i] = 0;
-            if (active[i] && my < cap) load_slot<W>(slots, my, w0[i], w1[i]);
+            if (active[i] && my < cap) load_slot_nt<W>(slots, my, w0[i], w1[i]);
         }
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
