@@ -6,9 +6,9 @@ materialise the contig text (test_<rank>.dat bytes) in HBM. Inputs are generated
 copied to HBM before timing; the D2H of the contigs is outside the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2] [--n N]
-  N > 1: torch.distributed.run, one rank per GPU; the table is sharded by key hash and the
-         walk exchanges queries with RCCL all-to-all (cs267_hw3_amd.dist); weak scaling
-         (n k-mers per GPU).
+  N > 1: torch.distributed.run, one rank per GPU; the table is sharded by a hash of each
+         k-mer's minimizer, routed words and migrating walkers move with RCCL all-to-all
+         (cs267_hw3_amd.dist); weak scaling (n k-mers per GPU).
 """
 import argparse
 import json
