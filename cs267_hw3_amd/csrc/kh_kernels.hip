@@ -804,8 +804,17 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     const int G = walk_group(p);
     if (const char* e = getenv("KH_WALK_BLOCKS")) grid_blocks = atoi(e);  // experiments
     if (G == -4) {  // quad-transposed: one walker per lane
+        // two blocks per CU (512 on MI355X): with non-temporal probes fewer walkers in flight
+        // contend less (C3 walk 5.71 -> 5.48-5.54 ms vs 2048 blocks, C2 0.67 -> 0.54; 384: 6.10)
+        static int ncu = 0;
+        if (!ncu) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                ncu = 256;
+        }
         const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
-                                             (uint64_t)(grid_blocks > 0 ? grid_blocks : 2048));
+                                             (uint64_t)(grid_blocks > 0 ? grid_blocks : 2 * ncu));
         if (p.W == 1)
             k_walk_q<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
         else
