@@ -39,7 +39,6 @@ class KhStats(ctypes.Structure):
 
 
 # name -> (restype, argtypes)
-SEG_SUBS = 8  # KH_SEG_SUBS: sub-segments per peer segment of the fixed walk rounds
 MSG_WORDS = 5  # KH_MSG_WORDS: migrating-walker message
 TEXT_REC_WORDS = 2  # KH_TEXT_REC_WORDS
 LINK_WORDS = 4  # KH_LINK_WORDS
@@ -56,6 +55,7 @@ _SIGS = {
                                  ctypes.c_int]),
     "kh_destroy": (ctypes.c_int, [c_vp]),
     "kh_clear": (ctypes.c_int, [c_vp]),
+    "kh_reserve": (ctypes.c_int, [c_vp, c_u64]),
     "kh_set_stream": (ctypes.c_int, [c_vp, c_vp]),
     "kh_sync": (ctypes.c_int, [c_vp]),
     "kh_capacity": (c_u64, [c_vp]),
@@ -77,15 +77,6 @@ _SIGS = {
     "kh_insert_words_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_insert_words_stage_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_u64]),
     "kh_insert_words_finish": (ctypes.c_int, [c_vp]),
-    "kh_walk_begin": (ctypes.c_int, [c_vp, c_u64, ctypes.POINTER(c_u64)]),
-    "kh_walk_emit_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp]),
-    "kh_find_ext_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp]),
-    "kh_walk_apply_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
-    "kh_walk_end_dev": (ctypes.c_int, [c_vp]),
-    "kh_walk_step_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp]),
-    "kh_find_ext_fixed_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64, c_vp, c_vp]),
-    "kh_walk_active_dev": (ctypes.c_int, [c_vp, c_vp]),
-    "kh_walk_signature": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "kh_pack_text_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, ctypes.POINTER(c_u64)]),
     "kh_mwalk_begin": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u64, ctypes.POINTER(c_u64)]),
     "kh_mwalk_round_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),

@@ -71,11 +71,21 @@ struct DevBuf {
 
 void kh_set_error_internal(const char* msg) { g_err = msg ? msg : ""; }
 
+bool kh::debug_flag(const char* name) {
+    const char* e = getenv("KH_DEBUG");
+    if (!e || !*e) return false;
+    const size_t n = strlen(name);
+    for (const char* p = e; (p = strstr(p, name)) != nullptr; p += n)
+        if ((p == e || p[-1] == ',') && (p[n] == 0 || p[n] == ',')) return true;
+    return false;
+}
+
 struct kh_table {
     int device = 0;
     kh::KParams kp{};
     uint64_t cap = 0;       // slots
-    uint64_t n_kmers = 0;   // k-mers the table was created for
+    uint64_t n_kmers = 0;   // k-mers the table was created (or last reserved) for
+    double load = 0.5;      // load factor
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
 
@@ -87,13 +97,12 @@ struct kh_table {
     DevBuf stage2, stage3;
     DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text;
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
-    DevBuf pb_buf1, pb_buf2, pb_hist1, pb_off1, pb_hist2, pb_off2, pb_scratch, pb_ovf;  // part build
+    DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
     bool last_insert_part = false;
     bool staging = false, stage_part = false, stage_fresh = false;  // kh_insert_words_stage_dev build
     uint64_t stage_total = 0, stage_n = 0;
     uint64_t collected_n = 0;  // records passed to kh_route_starts_dev since the last clear
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
-    DevBuf rw_hi, rw_lo, rw_buf, rw_steps, rw_chunk, rw_state, rw_qperm, rw_pos, rw_ctl;  // round walker
     DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
     // splitter segments of the migrating walk (kh_mseg.hip)
     DevBuf ms_len, ms_hi, ms_lo, ms_has, ms_done, ms_jump, ms_acc, ms_stab, ms_stab_id, ms_qsrc, ms_misc;
@@ -103,9 +112,7 @@ struct kh_table {
     uint64_t mw_store_n = 0;   // text records in mw_store
     uint32_t mw_P = 0, mw_rank = 0;
     bool mw_live = false, mw_stepped = false;
-    uint64_t rw_n = 0, rw_total = 0;
-    bool rw_live = false;
-    bool rw_stepped = false;   // a fixed-round step has run since kh_walk_begin
+    uint64_t rw_n = 0, rw_total = 0;  // migrating walk: local walkers, bound on contig length
     uint64_t starts_cap = 0;                 // start entries the starts buffer holds
     uint64_t splits_cap = 0, splits_w_cap = 0;
     bool split_ok = true;                    // every inserted k-mer was checked for splitters
@@ -136,6 +143,7 @@ int ensure_list(kh_table* t, DevBuf& buf, uint64_t& cap, uint64_t need) {
     if (need <= cap) return KH_OK;
     const uint64_t W = (uint64_t)t->kp.W;
     uint64_t newcap = need < 1024 ? 1024 : need;
+    if (newcap < 2 * cap) newcap = 2 * cap;  // geometric: many small batches stay O(n) copies
     DevBuf nb;
     int rc = nb.ensure(newcap * W * 8);
     if (rc) return rc;
@@ -202,29 +210,40 @@ bool use_part_build(const kh_table* t, uint64_t n) {
 }
 
 int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
-    const kh::PartPlan pl = kh::part_plan(n);
-    const uint64_t W = (uint64_t)t->kp.W, hw = kh::part_hist_words(pl);
+    const uint64_t W = (uint64_t)t->kp.W;
     int rc;
     if ((rc = t->pb_buf1.ensure(kh::part_buf1_words(t->kp, n) * 8)) || (rc = t->pb_buf2.ensure(kh::part_buf2_words(t->kp, n) * 8)) ||
-        (rc = t->pb_hist1.ensure(hw * 8)) || (rc = t->pb_off1.ensure(hw * 8)) ||
-        (rc = t->pb_hist2.ensure(hw * 8)) || (rc = t->pb_off2.ensure(hw * 8)) ||
-        (rc = t->pb_scratch.ensure(kh::part_scratch_words(pl) * 8)) ||
+        (rc = t->pb_cnt.ensure(kh::part_count_words() * 8)) ||
         (rc = t->pb_ovf.ensure(kh::part_overflow_cap(n) * W * 8)))
         return rc;
     b.buf1 = t->pb_buf1.as<uint64_t>();
     b.buf2 = t->pb_buf2.as<uint64_t>();
-    b.hist1 = t->pb_hist1.as<uint64_t>();
-    b.off1 = t->pb_off1.as<uint64_t>();
-    b.hist2 = t->pb_hist2.as<uint64_t>();
-    b.off2 = t->pb_off2.as<uint64_t>();
-    b.scratch = t->pb_scratch.as<uint64_t>();
+    b.wcnt = t->pb_cnt.as<uint32_t>();
+    b.rcnt = b.wcnt + kh::PART_W1_COUNTERS;
     b.overflow = t->pb_ovf.as<uint64_t>();
     return KH_OK;
 }
 
+// Capacity and splitter density for n_kmers (kh_create, kh_reserve).
+void size_table(kh_table* t, uint64_t n_kmers) {
+    t->n_kmers = n_kmers;
+    // splitter density: ~1 per 2^bits k-mers; enough extra walkers for long-chain inputs (C2, C5)
+    // at a few % more walkers on short-contig inputs. KH_SPLIT_BITS overrides (0 = off).
+    // Collected at insert: 1 per 2^bits k-mers, bits = clamp(log2(n / 2^20) + 1, 4, 12); the walk
+    // then uses a subset sized from the start count (kh_assemble_dev).
+    int bits = 1;
+    while (bits < 12 && (n_kmers >> (20 + bits)) != 0) ++bits;
+    bits = bits < 4 ? 4 : bits;
+    if (const char* e = getenv("KH_SPLIT_BITS")) bits = atoi(e);
+    t->kp.split_bits = bits < 0 ? 0 : (bits > 30 ? 30 : bits);
+    const double c = (double)(n_kmers ? n_kmers : 1) / t->load;
+    t->cap = (uint64_t)c;
+    if ((double)t->cap < c) t->cap++;
+    if (t->cap < 2) t->cap = 2;
+}
+
 }  // namespace
 
-static_assert(KH_SEG_SUBS == kh::SEG_SUBS, "segment layout");
 static_assert(KH_MSG_WORDS == kh::MSG_WORDS, "message layout");
 
 extern "C" {
@@ -255,23 +274,9 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     if (!t) return fail(KH_ERR_NOMEM, "host allocation failed");
     t->device = device;
     t->kp = kh::make_params(k);
-    t->n_kmers = n_kmers;
+    t->load = load_factor;
     if (const char* e = getenv("KH_OWNER")) t->kp.owner_mode = strcmp(e, "hash") == 0 ? 1 : 0;
-    // splitter density: ~1 per 2^bits k-mers; enough extra walkers for long-chain inputs (C2, C5)
-    // at a few % more walkers on short-contig inputs. KH_SPLIT_BITS overrides (0 = off).
-    // Collected at insert: 1 per 2^bits k-mers, bits = clamp(log2(n / 2^20) + 1, 4, 12); the walk
-    // then uses a subset sized from the start count (kh_assemble_dev).
-    {
-        int bits = 1;
-        while (bits < 12 && (n_kmers >> (20 + bits)) != 0) ++bits;
-        bits = bits < 4 ? 4 : bits;
-        if (const char* e = getenv("KH_SPLIT_BITS")) bits = atoi(e);
-        t->kp.split_bits = bits < 0 ? 0 : (bits > 30 ? 30 : bits);
-    }
-    double c = (double)(n_kmers ? n_kmers : 1) / load_factor;
-    t->cap = (uint64_t)c;
-    if ((double)t->cap < c) t->cap++;
-    if (t->cap < 2) t->cap = 2;
+    size_table(t, n_kmers);
     int rc = KH_OK;
     auto bail = [&](int r) {
         kh_destroy(t);
@@ -307,13 +312,11 @@ int kh_destroy(kh_table* t) {
                       &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
                       &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->splits, &t->splits_w, &t->seg_next,
-                      &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id, &t->rw_hi, &t->rw_lo,
-                      &t->rw_buf, &t->rw_steps, &t->rw_chunk, &t->rw_state, &t->rw_qperm, &t->rw_pos, &t->rw_ctl,
+                      &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id,
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
-                      &t->pb_buf1, &t->pb_buf2, &t->pb_hist1, &t->pb_off1, &t->pb_hist2,
-                      &t->pb_off2, &t->pb_scratch, &t->pb_ovf};
+                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf};
     for (auto* b : bufs) b->release();
     if (t->side) (void)hipStreamSynchronize(t->side);
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_conv,
@@ -323,6 +326,27 @@ int kh_destroy(kh_table* t) {
     if (t->side) (void)hipStreamDestroy(t->side);
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
     delete t;
+    return KH_OK;
+}
+
+int kh_reserve(kh_table* t, uint64_t n_kmers) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (n_kmers <= t->n_kmers) return KH_OK;
+    if (t->n_inserted || t->staging)
+        return fail(KH_ERR_STATE, "kh_reserve on a table holding %llu k-mers (clear it first)",
+                    (unsigned long long)t->n_inserted);
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(hipStreamSynchronize(t->stream));
+    const uint64_t old_n = t->n_kmers;
+    const int old_bits = t->kp.split_bits;
+    size_table(t, n_kmers);
+    t->slots.release();
+    if (int rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8)) {
+        size_table(t, old_n);
+        t->kp.split_bits = old_bits;
+        return rc;
+    }
+    t->slots_stale = true;
     return KH_OK;
 }
 
@@ -386,7 +410,7 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
     // partitioned build: the start / splitter bits exist once the record pass has run, so their
     // compaction runs on the side stream, overlapped with the partition passes and the build
-    const bool overlap = part && !getenv("KH_NO_OVERLAP");
+    const bool overlap = part && !kh::debug_flag("no_overlap");
     hipStream_t cs = overlap ? t->side : t->stream;
     if (part)
         KH_HIP(kh::launch_part_insert(t->kp, (const uint8_t*)dev_recs, nullptr, n, view(t),
@@ -529,7 +553,6 @@ int kh_assemble_dev(kh_table* t) {
     if ((rc = t->chunk_data.ensure(chunk_cap * kh::CHUNK_WORDS * 8))) return rc;
     if ((rc = t->chunk_owner.ensure(chunk_cap * 4))) return rc;
     if ((rc = t->chunk_seq.ensure(chunk_cap * 4))) return rc;
-    if ((rc = t->text.ensure(n + ns * ((uint64_t)t->kp.K + 1) + 64))) return rc;
     if ((rc = t->scratch.ensure(kh::scan_scratch_words(ns) * 8 + 64))) return rc;
     t->chunk_cap = chunk_cap;
     kh::WalkBuffers wb{};
@@ -565,18 +588,50 @@ int kh_assemble_dev(kh_table* t) {
         KH_HIP(hipMemsetAsync(wb.seg_next, 0xff, nseg * 4, t->stream));
     }
     unsigned long long* ctr = t->ctr.as<unsigned long long>();
-    KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
-    KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
-    KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, t->stats.as<unsigned long long>(), 0, t->stream));
-    if (kp.split_bits)
-        KH_HIP(kh::launch_segments(kp, wb, sb, t->stats.as<unsigned long long>(), t->stream));
-    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
+    unsigned long long* stats = t->stats.as<unsigned long long>();
+    // Walk, then the offsets scan; the text is sized from the scanned total (walks that overlap,
+    // e.g. two explicit starts on one contig, make it longer than the k-mer count). The chunk
+    // pool is an upper bound for disjoint walks; if overlapping walks exhaust it the walk is
+    // redone once with the pool the first attempt asked for.
+    for (int attempt = 0;; ++attempt) {
+        KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
+        KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
+        KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, 0, t->stream));
+        if (kp.split_bits) KH_HIP(kh::launch_segments(kp, wb, sb, stats, t->stream));
+        KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
+        if (kp.split_bits)
+            KH_HIP(kh::launch_materialize_seg(kp, wb, sb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                              nullptr, ctr, t->stream, kh::MAT_SCAN));
+        else
+            KH_HIP(kh::launch_materialize(kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                          nullptr, ctr, t->stream, kh::MAT_SCAN));
+        unsigned long long hv[2], ovf = 0;
+        KH_HIP(hipMemcpyAsync(hv, ctr + kh::CT_CHUNK_NEXT, sizeof hv, hipMemcpyDeviceToHost, t->stream));
+        KH_HIP(hipMemcpyAsync(&ovf, stats + kh::ST_CHUNK_OVF, 8, hipMemcpyDeviceToHost, t->stream));
+        KH_HIP(hipStreamSynchronize(t->stream));
+        if (ns == 0) hv[1] = 0;
+        if (ovf && attempt == 0) {
+            const uint64_t need = nseg + hv[0] + 64;
+            if ((rc = t->chunk_data.ensure(need * kh::CHUNK_WORDS * 8)) || (rc = t->chunk_owner.ensure(need * 4)) ||
+                (rc = t->chunk_seq.ensure(need * 4)))
+                return rc;
+            t->chunk_cap = wb.chunk_cap = need;
+            wb.chunk_data = t->chunk_data.as<uint64_t>();
+            wb.chunk_owner = t->chunk_owner.as<uint32_t>();
+            wb.chunk_seq = t->chunk_seq.as<uint32_t>();
+            KH_HIP(hipMemsetAsync(stats + kh::ST_CHUNK_OVF, 0, 8, t->stream));
+            if (kp.split_bits) KH_HIP(hipMemsetAsync(wb.seg_next, 0xff, nseg * 4, t->stream));
+            continue;
+        }
+        if ((rc = t->text.ensure(hv[1] + 64))) return rc;
+        break;
+    }
     if (kp.split_bits)
         KH_HIP(kh::launch_materialize_seg(kp, wb, sb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                          t->text.as<char>(), ctr, t->stream));
+                                          t->text.as<char>(), ctr, t->stream, kh::MAT_WRITE));
     else
         KH_HIP(kh::launch_materialize(kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                      t->text.as<char>(), ctr, t->stream));
+                                      t->text.as<char>(), ctr, t->stream, kh::MAT_WRITE));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = ns;
@@ -701,25 +756,6 @@ int ensure_route(kh_table* t, uint64_t n, int nranks) {
     return KH_OK;
 }
 
-kh::RoundWalk round_walk(kh_table* t) {
-    kh::RoundWalk rw;
-    rw.n = t->rw_n;
-    rw.hi = t->rw_hi.as<uint64_t>();
-    rw.lo = t->rw_lo.as<uint64_t>();
-    rw.buf = t->rw_buf.as<uint64_t>();
-    rw.steps = t->rw_steps.as<uint32_t>();
-    rw.chunk = t->rw_chunk.as<uint32_t>();
-    rw.state = t->rw_state.as<uint8_t>();
-    rw.qperm = t->rw_qperm.as<uint32_t>();
-    rw.pos = t->rw_pos.as<uint32_t>();
-    rw.contig_len = t->contig_len.as<uint32_t>();
-    rw.chunk_data = t->chunk_data.as<uint64_t>();
-    rw.chunk_owner = t->chunk_owner.as<uint32_t>();
-    rw.chunk_seq = t->chunk_seq.as<uint32_t>();
-    rw.chunk_cap = t->chunk_cap;
-    rw.max_steps = t->rw_total;
-    return rw;
-}
 }  // namespace
 
 int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n) {
@@ -779,16 +815,13 @@ static bool mseg_enabled(const kh_table* t) {
     return t->kp.split_bits > 0 && !(e && !strcmp(e, "0"));
 }
 
-// Splitter density of the migrating walk: the table's (1 per 256 k-mers at C3 sizes;
-// KH_MW_SPLIT_EXTRA adds bits). Measured at one rank (C3 / C5 ms per step): off 15.4 / 2159,
-// +0 17.8 / 36.5, +2 17.3 / 66.6 — the segment phase is mostly a fixed cost (link, jump, retag
-// rounds), while sparser splitters leave longer segments (more rounds) on long chains.
+// Splitter density of the migrating walk: the table's (1 per 256 k-mers at C3 sizes). Measured
+// at one rank (C3 / C5 ms per step): segments off 15.4 / 2159, table density 17.8 / 36.5, 4x
+// sparser 17.3 / 66.6 — the segment phase is mostly a fixed cost (link, jump, retag rounds),
+// while sparser splitters leave longer segments (more rounds) on long chains.
 static kh::KParams mseg_params(const kh_table* t) {
     kh::KParams p = t->kp;
-    int extra = 0;
-    if (const char* e = getenv("KH_MW_SPLIT_EXTRA")) extra = atoi(e);
-    int b = p.split_bits + extra;
-    p.split_bits = b < 1 ? 1 : (b > 30 ? 30 : b);
+    if (p.split_bits < 1) p.split_bits = 1;
     return p;
 }
 
@@ -846,7 +879,7 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     if (int rc = set_device(t)) return rc;
     t->split_ok = false;  // routed words carry no splitter marks: walks on this table use none
     const bool part = use_part_build(t, m);
-    const bool coll = part && kh::part_words_collect_splits() && mseg_enabled(t) && t->words_split;
+    const bool coll = part && mseg_enabled(t) && t->words_split;
     if (int rc = collect_word_splits(t, words, m, coll)) return rc;
     kh::PartBuffers pb{};
     if (part)
@@ -908,7 +941,7 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
         return fail(KH_ERR_FULL, "staged %llu + %llu words exceed the build's %llu",
                     (unsigned long long)t->stage_n, (unsigned long long)m, (unsigned long long)t->stage_total);
     if (m == 0) return KH_OK;
-    const bool coll = t->stage_part && kh::part_words_collect_splits() && mseg_enabled(t) && t->words_split;
+    const bool coll = t->stage_part && mseg_enabled(t) && t->words_split;
     if (int rc = collect_word_splits(t, words, m, coll)) return rc;
     if (t->stage_part) {
         kh::PartBuffers b{};
@@ -943,130 +976,6 @@ int kh_insert_words_finish(kh_table* t) {
     t->staging = false;
     t->stage_n = 0;
     t->assembled = false;
-    return KH_OK;
-}
-
-int kh_walk_begin(kh_table* t, uint64_t total_kmers, uint64_t* n_walkers) {
-    if (!t) return fail(KH_ERR_ARG, "null table");
-    if (int rc = set_device(t)) return rc;
-    if (int rc = clean_slots(t)) return rc;
-    int rc;
-    uint64_t ns = 0;
-    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
-    const uint64_t tot = total_kmers > ns ? total_kmers : ns;
-    const uint64_t chunk_cap = tot / kh::CHUNK_BASES + ns + 64;
-    if ((rc = t->contig_len.ensure((ns + 1) * 4))) return rc;
-    if ((rc = t->contig_off.ensure((ns + 1) * 8))) return rc;
-    if ((rc = t->chunk_data.ensure(chunk_cap * kh::CHUNK_WORDS * 8))) return rc;
-    if ((rc = t->chunk_owner.ensure(chunk_cap * 4))) return rc;
-    if ((rc = t->chunk_seq.ensure(chunk_cap * 4))) return rc;
-    if ((rc = t->text.ensure(tot + ns * ((uint64_t)t->kp.K + 1) + 64))) return rc;
-    if ((rc = t->scratch.ensure(kh::scan_scratch_words(ns) * 8 + 64))) return rc;
-    const uint64_t nn = ns + 1;
-    if ((rc = t->rw_hi.ensure(nn * 8)) || (rc = t->rw_lo.ensure(nn * 8)) || (rc = t->rw_buf.ensure(nn * 8)) ||
-        (rc = t->rw_steps.ensure(nn * 4)) || (rc = t->rw_chunk.ensure(nn * 4)) ||
-        (rc = t->rw_state.ensure((nn + 7) & ~7ull)) || (rc = t->rw_qperm.ensure(nn * 4)) ||
-        (rc = t->rw_pos.ensure(nn * 4)) || (rc = t->rw_ctl.ensure(kh::CTL_WORDS * 8)))
-        return rc;
-    t->chunk_cap = chunk_cap;
-    t->rw_n = ns;
-    t->rw_total = tot;
-    KH_HIP(hipMemsetAsync(t->ctr.as<unsigned long long>() + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));
-    KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
-    KH_HIP(hipMemsetAsync(t->rw_ctl.p, 0, kh::CTL_WORDS * 8, t->stream));
-    KH_HIP(kh::launch_rw_init(t->kp, round_walk(t), t->starts.as<uint64_t>(), t->stream));
-    t->rw_live = true;
-    t->rw_stepped = false;
-    t->assembled = false;
-    if (n_walkers) *n_walkers = ns;
-    return KH_OK;
-}
-
-int kh_walk_emit_dev(kh_table* t, int nranks, void* keys_out, void* counts_out) {
-    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
-    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
-    if (!counts_out || (t->rw_n && !keys_out)) return fail(KH_ERR_ARG, "null buffer");
-    if (int rc = set_device(t)) return rc;
-    if (int rc = ensure_route(t, t->rw_n, nranks)) return rc;
-    KH_HIP(kh::launch_rw_emit(t->kp, round_walk(t), (uint32_t)nranks, t->route_hist.as<uint64_t>(),
-                              t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(),
-                              (uint64_t*)keys_out, (uint64_t*)counts_out,
-                              t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(),
-                              t->stream));
-    return KH_OK;
-}
-
-int kh_find_ext_dev(kh_table* t, const void* keys, uint64_t m, void* ext_out) {
-    if (!t) return fail(KH_ERR_ARG, "null table");
-    if (m == 0) return KH_OK;
-    if (!keys || !ext_out) return fail(KH_ERR_ARG, "null buffer");
-    if (int rc = set_device(t)) return rc;
-    if (int rc = clean_slots(t)) return rc;
-    KH_HIP(kh::launch_find_ext(t->kp, (const uint64_t*)keys, m, view(t), (uint8_t*)ext_out, t->stream));
-    return KH_OK;
-}
-
-int kh_walk_apply_dev(kh_table* t, const void* ext, uint64_t m) {
-    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
-    if (m == 0) return KH_OK;
-    if (!ext) return fail(KH_ERR_ARG, "null replies");
-    if (m > t->rw_n) return fail(KH_ERR_ARG, "%llu replies for %llu walkers", (unsigned long long)m,
-                                 (unsigned long long)t->rw_n);
-    if (int rc = set_device(t)) return rc;
-    KH_HIP(kh::launch_rw_apply(t->kp, round_walk(t), (const uint8_t*)ext, m,
-                               t->stats.as<unsigned long long>(), t->stream));
-    return KH_OK;
-}
-
-int kh_walk_end_dev(kh_table* t) {
-    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
-    if (int rc = set_device(t)) return rc;
-    kh::WalkBuffers wb{};
-    wb.starts = t->starts.as<uint64_t>();
-    wb.n_starts = t->rw_n;
-    wb.contig_len = t->contig_len.as<uint32_t>();
-    wb.chunk_data = t->chunk_data.as<uint64_t>();
-    wb.chunk_owner = t->chunk_owner.as<uint32_t>();
-    wb.chunk_seq = t->chunk_seq.as<uint32_t>();
-    wb.chunk_cap = t->chunk_cap;
-    wb.max_steps = t->rw_total;
-    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
-    KH_HIP(kh::launch_materialize(t->kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                  t->text.as<char>(), t->ctr.as<unsigned long long>(), t->stream));
-    KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
-    t->walk_timed = true;
-    t->last_contigs = t->rw_n;
-    t->assembled = true;
-    t->rw_live = false;
-    return KH_OK;
-}
-
-int kh_walk_step_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* reply_prev, void* send) {
-    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
-    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
-    if (!send) return fail(KH_ERR_ARG, "null buffer");
-    if (cap == 0 || cap % KH_SEG_SUBS) return fail(KH_ERR_ARG, "cap must be a positive multiple of %d", KH_SEG_SUBS);
-    if (cap * (uint64_t)nranks > 0xFFFFFFFFull) return fail(KH_ERR_ARG, "nranks * cap exceeds 2^32");
-    if (t->rw_stepped && !reply_prev)
-        return fail(KH_ERR_STATE, "queries in flight: pass the previous round's replies");
-    if (int rc = set_device(t)) return rc;
-    KH_HIP(kh::launch_rw_step_fixed(t->kp, round_walk(t), (uint32_t)nranks, cap,
-                                    t->rw_stepped ? (const uint8_t*)reply_prev : nullptr, (uint64_t*)send,
-                                    t->rw_ctl.as<unsigned long long>(), t->ctr.as<unsigned long long>(),
-                                    t->stats.as<unsigned long long>(), t->stream));
-    t->rw_stepped = true;
-    return KH_OK;
-}
-
-int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* recv, void* reply) {
-    if (!t) return fail(KH_ERR_ARG, "null table");
-    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "bad nranks %d", nranks);
-    if (!recv || !reply) return fail(KH_ERR_ARG, "null buffer");
-    if (cap == 0 || cap % KH_SEG_SUBS) return fail(KH_ERR_ARG, "cap must be a positive multiple of %d", KH_SEG_SUBS);
-    if (int rc = set_device(t)) return rc;
-    if (int rc = clean_slots(t)) return rc;
-    KH_HIP(kh::launch_find_ext_fixed(t->kp, (const uint64_t*)recv, (uint32_t)nranks, cap, view(t),
-                                     (uint8_t*)reply, t->stream));
     return KH_OK;
 }
 
@@ -1386,36 +1295,6 @@ int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
     t->last_contigs = nc;
     t->assembled = true;
     t->mw_live = false;
-    return KH_OK;
-}
-
-int kh_walk_signature(kh_table* t, uint64_t* sig) {
-    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
-    if (!sig) return fail(KH_ERR_ARG, "null output");
-    // everything the fixed-round launches take as kernel arguments (besides the caller's buffers)
-    const kh::RoundWalk rw = round_walk(t);
-    const uint64_t v[] = {(uint64_t)(uintptr_t)rw.hi, (uint64_t)(uintptr_t)rw.lo, (uint64_t)(uintptr_t)rw.buf,
-                          (uint64_t)(uintptr_t)rw.steps, (uint64_t)(uintptr_t)rw.chunk,
-                          (uint64_t)(uintptr_t)rw.state, (uint64_t)(uintptr_t)rw.pos,
-                          (uint64_t)(uintptr_t)rw.contig_len, (uint64_t)(uintptr_t)rw.chunk_data,
-                          (uint64_t)(uintptr_t)rw.chunk_owner, (uint64_t)(uintptr_t)rw.chunk_seq, rw.chunk_cap,
-                          rw.n, rw.max_steps, (uint64_t)(uintptr_t)t->slots.p, t->cap, (uint64_t)t->kp.K,
-                          (uint64_t)(uintptr_t)t->ctr.p, (uint64_t)(uintptr_t)t->stats.p,
-                          (uint64_t)(uintptr_t)t->rw_ctl.p, (uint64_t)(uintptr_t)t->stream};
-    uint64_t h = 0x9E3779B97F4A7C15ull;
-    for (uint64_t x : v) h = (h ^ x) * 0x100000001B3ull + (h >> 29);
-    *sig = h;
-    return KH_OK;
-}
-
-int kh_walk_active_dev(kh_table* t, void* out) {
-    if (!t || !t->rw_live) return fail(KH_ERR_STATE, "kh_walk_begin first");
-    if (!out) return fail(KH_ERR_ARG, "null buffer");
-    if (int rc = set_device(t)) return rc;
-    const void* src = t->rw_stepped ? (const void*)(t->rw_ctl.as<unsigned long long>() + kh::CTL_LIVE)
-                                    : (const void*)&t->rw_n;
-    KH_HIP(hipMemcpyAsync(out, src, 8, t->rw_stepped ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                          t->stream));
     return KH_OK;
 }
 

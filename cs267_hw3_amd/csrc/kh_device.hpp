@@ -403,4 +403,18 @@ static inline hipError_t group_by_owner(Op op, uint64_t n, uint32_t P, uint64_t*
     return hipGetLastError();
 }
 
+// multiprocessor count of the current device (per device: tables on several GPUs in one process)
+inline int cu_count() {
+    static int ncu[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return 256;
+    int v = __atomic_load_n(&ncu[dev], __ATOMIC_RELAXED);
+    if (!v) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        __atomic_store_n(&ncu[dev], v, __ATOMIC_RELAXED);
+    }
+    return v;
+}
+
 }  // namespace kh

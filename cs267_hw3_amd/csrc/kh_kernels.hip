@@ -253,150 +253,15 @@ __device__ __forceinline__ uint64_t walk_splits(const WalkBuffers& wb) {
     return wb.n_splits_dev ? (uint64_t)*wb.n_splits_dev : wb.n_splits;
 }
 
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_walk(KParams p, const uint64_t* __restrict__ slots,
-                                                uint64_t cap, WalkBuffers wb,
-                                                unsigned long long* ctr,
-                                                unsigned long long* stats) {
-    const uint32_t lane = lane_id();
-    const uint64_t n = wb.n_starts + walk_splits(wb);  // walkers: contig starts, then splitter segments
-    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
-    // wave-uniform batch window: contigs [bbase, bbase + WALK_GRAB), bused of them handed out
-    uint64_t bbase = 0;
-    uint32_t bused = WALK_GRAB;
-    bool bdry = false;
-    uint64_t bw0 = 0, bw1 = 0;  // this lane's preloaded start record of the batch
-
-    bool active = false, done = false, resolved = false;
-    uint64_t c = 0, s = 0, buf = 0;
-    Key k{0, 0};
-    uint32_t fwd = 0, steps = 0, chunk = 0;
-    while (true) {
-        // -- refill / finish until no lane finishes (single-k-mer contigs finish at once) ----
-        while (true) {
-            const bool need = !active && !done;
-            const uint64_t m = __ballot(need);
-            if (m) {
-                const uint32_t cnt = (uint32_t)__popcll(m);
-                const uint32_t rank = mbcnt64(m);
-                const uint32_t avail = WALK_GRAB - bused;
-                const uint32_t src_old = min(bused + rank, (uint32_t)WALK_GRAB - 1);
-                const uint64_t o0 = __shfl(bw0, (int)src_old, 64);
-                const uint64_t o1 = __shfl(bw1, (int)src_old, 64);
-                const uint64_t oc = bbase + src_old;
-                uint64_t n0 = 0, n1 = 0, nc = ~0ull;
-                if (cnt > avail) {
-                    if (!bdry) {
-                        unsigned long long g = 0;
-                        if (lane == 0) g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB);
-                        bbase = __shfl(g, 0, 64);
-                        if (bbase >= n) bdry = true;
-                        const uint64_t mi = bbase + lane;
-                        if (mi < n) {
-                            const uint64_t* src = mi < wb.n_starts ? wb.starts + mi * W
-                                                                   : wb.splits + (mi - wb.n_starts) * W;
-                            bw0 = src[0];
-                            bw1 = (W == 2) ? src[1] : 0;
-                        }
-                        const uint32_t src_new = min(rank - min(rank, avail), (uint32_t)WALK_GRAB - 1);
-                        n0 = __shfl(bw0, (int)src_new, 64);
-                        n1 = __shfl(bw1, (int)src_new, 64);
-                        nc = bbase + src_new;
-                    }
-                    bused = cnt - avail;
-                } else {
-                    bused += cnt;
-                }
-                if (need) {
-                    uint64_t cc = ~0ull, x0 = 0, x1 = 0;
-                    if (rank < avail) {
-                        cc = oc;
-                        x0 = o0;
-                        x1 = o1;
-                    } else {
-                        cc = nc;
-                        x0 = n0;
-                        x1 = n1;
-                    }
-                    if (cc < n) {
-                        c = cc;
-                        k = slot_key(x0, x1, p);
-                        fwd = ext_fwd(slot_ext(x0));
-                        steps = 0;
-                        buf = 0;
-                        active = true;
-                        resolved = true;
-                    } else {
-                        done = true;
-                    }
-                }
-            }
-            const bool fin = active && resolved && fwd > 3;
-            if (fin) {
-                if (fwd != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
-                finish_contig(o, c, steps, chunk, buf);
-                active = false;
-            }
-            if (!__any(fin)) break;
-        }
-        if (!__any(active)) break;
-        // -- advance: resolved lanes append their forward base and move to the next k-mer --------
-        if (active && resolved) {
-            append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
-            k = key_next(k, fwd, p);
-            const uint64_t h = key_hash(k);
-            if (is_splitter(h, p)) {  // the next k-mer heads a segment of its own walker
-                finish_contig(o, c, steps, chunk, buf);
-                wb.seg_next[c] = SEG_AT_SPLIT;
-                wb.seg_key[2 * c] = k.hi;
-                wb.seg_key[2 * c + 1] = k.lo;
-                active = false;
-            } else {
-                s = home_slot(h, cap);
-                resolved = false;
-            }
-        }
-        // -- one table load per active lane ---------------------------------------------------
-        if (active) {
-            uint64_t w0, w1;
-            load_slot<W>(slots, s, w0, w1);
-            const bool empty = w0 == EMPTY;
-            const bool hit = !empty & ((w0 >> 6) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
-            if (hit) {
-                fwd = ext_fwd(slot_ext(w0));
-                resolved = true;
-                if (steps > wb.max_steps) {
-                    atomicAdd(&stats[ST_CYCLE], 1ull);
-                    finish_contig(o, c, steps, chunk, buf);
-                    active = false;
-                }
-            } else if (empty) {
-                atomicAdd(&stats[ST_MISSING], 1ull);
-                finish_contig(o, c, steps, chunk, buf);
-                active = false;
-            } else {
-                s = (s + 1 == cap) ? 0 : s + 1;
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
-// Cooperative walker: G lanes per contig, each probe fetches the whole G-slot block (64 or 128 B,
-// one memory line) that holds the probe position, G slots compared at once. The walk is bound by
-// the number of random line requests the memory system serves (~51 G/s whether a request is a
-// 16-B slot or a full 128-B line: tools/membench chase16 / chase64q / chase128o), and a per-lane
-// walker spends ~1.5 requests per lookup at load 0.5 (linear-probing displacement), a block
-// probe ~1 + P(the run crosses the block end).
-// Walker state is replicated in the G lanes of a group; the group's lane 0 (the leader) performs
-// every side effect (chunk allocation, base words, contig length, segment records).
-// ---------------------------------------------------------------------------------------------
-// Quad-transposed walker (KH_WALK_G=-4, the default): one walker per lane as in k_walk (no
-// redundant per-walker ALU), but every probe reads the walker's whole 4-slot block (64 B at 16-B
-// slots): lane q of a quad loads slot q of the block of each of the quad's 4 walkers, so a lookup
-// costs ~1.06 random requests instead of ~1.3 (linear-probing displacement crossing a slot). All
-// intra-quad exchange is DPP quad_perm (ALU, no LDS): each walker's probe position and key are
-// broadcast to its quad, and the hit slot's extension comes back by a quad OR-reduction.
+// Quad-transposed walker: one walker per lane, every probe reads the walker's whole 4-slot block
+// (64 B at 16-B slots): lane q of a quad loads slot q of the block of each of the quad's 4
+// walkers, so a lookup costs ~1.06 random requests instead of ~1.3 for slot-by-slot probes
+// (linear-probing displacement crossing a slot). The walk is bound by the number of random line
+// requests the memory system serves (~51 G/s whether a request is a 16-B slot or a full 128-B
+// line: tools/membench chase16 / chase64q / chase128o). All intra-quad exchange is DPP quad_perm
+// (ALU, no LDS): each walker's probe position and key are broadcast to its quad, and the hit
+// slot's extension comes back by a quad OR-reduction.
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
@@ -578,267 +443,18 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __r
     }
 }
 
-// NS walkers per group (KH_WALK_NS): the group's NS block loads are issued back to back, so
-// each group keeps NS requests in flight (at G=4 one walker per group leaves the walk latency-
-// bound: 8 waves/SIMD hold only 131K walkers).
-template <int W, int G, int NS>
-__global__ __launch_bounds__(BLOCK) void k_walk_g(KParams p, const uint64_t* __restrict__ slots,
-                                                  uint64_t cap, WalkBuffers wb,
-                                                  unsigned long long* ctr,
-                                                  unsigned long long* stats) {
-    static_assert(G >= 2 && G <= 16 && (G & (G - 1)) == 0, "group size");
-    const uint32_t lane = lane_id();
-    const uint32_t q = lane & (G - 1), gl = lane & ~(uint32_t)(G - 1);
-    const bool lead = q == 0;
-    constexpr uint64_t GM = (1ull << G) - 1;
-    uint64_t LM = 0;  // one bit per group leader
-#pragma unroll
-    for (int i = 0; i < 64; i += G) LM |= 1ull << i;
-    const uint64_t below = (1ull << gl) - 1;
-    const uint64_t n = wb.n_starts + walk_splits(wb);
-    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
-    uint64_t bbase = 0;
-    uint32_t bused = WALK_GRAB;
-    bool bdry = false;
-    uint64_t bw0 = 0, bw1 = 0;
-
-    bool active[NS], done[NS], resolved[NS];
-    uint64_t c[NS], s[NS], buf[NS];
-    Key k[NS];
-    uint32_t fwd[NS], steps[NS], chunk[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        active[i] = done[i] = resolved[i] = false;
-        c[i] = s[i] = buf[i] = 0;
-        k[i] = Key{0, 0};
-        fwd[i] = steps[i] = chunk[i] = 0;
-    }
-    while (true) {
-        while (true) {
-            bool need[NS];
-            uint32_t rank[NS];
-            uint32_t cnt = 0;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                need[i] = !active[i] && !done[i];  // uniform within a group
-                const uint64_t m = __ballot(need[i]) & LM;
-                rank[i] = cnt + (uint32_t)__popcll(m & below);
-                cnt += (uint32_t)__popcll(m);
-            }
-            if (cnt) {
-                const uint32_t avail = WALK_GRAB - bused;
-                uint64_t x0[NS], x1[NS], xc[NS];
-#pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    const uint32_t src_old = min(bused + rank[i], (uint32_t)WALK_GRAB - 1);
-                    x0[i] = __shfl(bw0, (int)src_old, 64);
-                    x1[i] = __shfl(bw1, (int)src_old, 64);
-                    xc[i] = rank[i] < avail ? bbase + src_old : ~0ull;
-                }
-                if (cnt > avail) {
-                    if (!bdry) {
-                        unsigned long long g = 0;
-                        if (lane == 0) g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB);
-                        bbase = __shfl(g, 0, 64);
-                        if (bbase >= n) bdry = true;
-                        const uint64_t mi = bbase + lane;
-                        if (mi < n) {
-                            const uint64_t* src = mi < wb.n_starts ? wb.starts + mi * W
-                                                                   : wb.splits + (mi - wb.n_starts) * W;
-                            bw0 = src[0];
-                            bw1 = (W == 2) ? src[1] : 0;
-                        }
-#pragma unroll
-                        for (int i = 0; i < NS; ++i) {
-                            const uint32_t src_new = min(rank[i] - min(rank[i], avail), (uint32_t)WALK_GRAB - 1);
-                            const uint64_t n0 = __shfl(bw0, (int)src_new, 64);
-                            const uint64_t n1 = __shfl(bw1, (int)src_new, 64);
-                            if (rank[i] >= avail) {
-                                x0[i] = n0;
-                                x1[i] = n1;
-                                xc[i] = bbase + src_new;
-                            }
-                        }
-                    }
-                    bused = cnt - avail;
-                } else {
-                    bused += cnt;
-                }
-#pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    if (need[i]) {
-                        if (xc[i] < n) {
-                            c[i] = xc[i];
-                            k[i] = slot_key(x0[i], x1[i], p);
-                            fwd[i] = ext_fwd(slot_ext(x0[i]));
-                            steps[i] = 0;
-                            buf[i] = 0;
-                            active[i] = true;
-                            resolved[i] = true;
-                        } else {
-                            done[i] = true;
-                        }
-                    }
-                }
-            }
-            bool anyfin = false;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                const bool fin = active[i] && resolved[i] && fwd[i] > 3;
-                if (fin) {
-                    if (lead) {
-                        if (fwd[i] != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
-                        finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
-                    }
-                    active[i] = false;
-                }
-                anyfin |= fin;
-            }
-            if (!__any(anyfin)) break;
-        }
-        bool anyact = false;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) anyact |= active[i];
-        if (!__any(anyact)) break;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            if (active[i] && resolved[i]) {
-                if (lead) {
-                    append_base(o, c[i], fwd[i], steps[i], chunk[i], buf[i], ctr, stats);
-                } else {
-                    ++steps[i];
-                }
-                k[i] = key_next(k[i], fwd[i], p);
-                const uint64_t h = key_hash(k[i]);
-                if (is_splitter(h, p)) {
-                    if (lead) {
-                        finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
-                        wb.seg_next[c[i]] = SEG_AT_SPLIT;
-                        wb.seg_key[2 * c[i]] = k[i].hi;
-                        wb.seg_key[2 * c[i] + 1] = k[i].lo;
-                    }
-                    active[i] = false;
-                } else {
-                    s[i] = home_slot(h, cap);
-                    resolved[i] = false;
-                }
-            }
-        }
-        // -- NS block loads per active group, all in flight together ------------------------------
-        uint64_t w0[NS], w1[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const uint64_t my = (s[i] & ~(uint64_t)(G - 1)) + q;
-            w0[i] = EMPTY;
-            w1[i] = 0;
-            if (active[i] && my < cap) load_slot_nt<W>(slots, my, w0[i], w1[i]);
-        }
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const uint64_t lb = s[i] & ~(uint64_t)(G - 1);
-            const uint64_t my = lb + q;
-            const bool valid = active[i] && my >= s[i] && my < cap;
-            const bool empty = w0[i] == EMPTY;
-            const bool hit = !empty & ((w0[i] >> 6) == ((W == 1) ? k[i].lo : k[i].hi)) &
-                             ((W == 1) | (w1[i] == k[i].lo));
-            const uint64_t bh = (__ballot(valid && hit) >> gl) & GM;
-            const uint64_t be = (__ballot(valid && empty) >> gl) & GM;
-            const uint32_t fh = bh ? (uint32_t)__builtin_ctzll(bh) : (uint32_t)G;
-            const uint32_t fe = be ? (uint32_t)__builtin_ctzll(be) : (uint32_t)G;
-            const uint64_t hw0 = __shfl(w0[i], (int)(gl + (fh & (G - 1))), 64);
-            if (active[i]) {
-                if (fh < fe) {
-                    fwd[i] = ext_fwd(slot_ext(hw0));
-                    resolved[i] = true;
-                    if (steps[i] > wb.max_steps) {
-                        if (lead) {
-                            atomicAdd(&stats[ST_CYCLE], 1ull);
-                            finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
-                        }
-                        active[i] = false;
-                    }
-                } else if (fe < (uint32_t)G) {
-                    if (lead) {
-                        atomicAdd(&stats[ST_MISSING], 1ull);
-                        finish_contig(o, c[i], steps[i], chunk[i], buf[i]);
-                    }
-                    active[i] = false;
-                } else {
-                    s[i] = (lb + G >= cap) ? 0 : lb + G;
-                }
-            }
-        }
-    }
-}
-
-// Walker shape (KH_WALK_G): -4 = quad-transposed block probes (k_walk_q, default), 1 = per-lane
-// walker (k_walk), G = 2..16 lanes per contig (k_walk_g). C3 k_walk on one box: -4: 5.38 ms,
-// 4: 5.50, 1: 5.59; 8: 7.6 (too few walkers resident). C2: 4 beat 1 by 9 %.
-static int walk_group(const KParams& p) {
-    const char* e = getenv("KH_WALK_G");
-    if (e && *e) return atoi(e);
-    (void)p;
-    return -4;
-}
-
-static int walk_states() {
-    const char* e = getenv("KH_WALK_NS");
-    return (e && *e) ? atoi(e) : 1;
-}
-
-template <int W, int G>
-static void launch_walk_g(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
-                          unsigned long long* stats, unsigned grid, hipStream_t s) {
-    switch (walk_states()) {
-        case 2: k_walk_g<W, G, 2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); break;
-        case 3: k_walk_g<W, G, 3><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); break;
-        case 4: k_walk_g<W, G, 4><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); break;
-        default: k_walk_g<W, G, 1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
-    }
-}
-
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s) {
     const uint64_t nw = wb.n_starts + wb.n_splits;
     if (nw == 0) return hipSuccess;
-    const int G = walk_group(p);
-    if (const char* e = getenv("KH_WALK_BLOCKS")) grid_blocks = atoi(e);  // experiments
-    if (G == -4) {  // quad-transposed: one walker per lane
-        // two blocks per CU (512 on MI355X): with non-temporal probes fewer walkers in flight
-        // contend less (C3 walk 5.71 -> 5.48-5.54 ms vs 2048 blocks, C2 0.67 -> 0.54; 384: 6.10)
-        static int ncu = 0;
-        if (!ncu) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-                ncu = 256;
-        }
-        const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
-                                             (uint64_t)(grid_blocks > 0 ? grid_blocks : 2 * ncu));
-        if (p.W == 1)
-            k_walk_q<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
-        else
-            k_walk_q<2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
-        return hipGetLastError();
-    }
-    const uint64_t lanes = nw * (uint64_t)(G > 1 ? G : 1) / (uint64_t)(G > 1 ? walk_states() : 1) + 1;
-    uint64_t want = (lanes + BLOCK - 1) / BLOCK;
-    unsigned grid = (unsigned)hmin(want, (uint64_t)(grid_blocks > 0 ? grid_blocks : 2048));
-    if (p.W == 1) {
-        switch (G) {
-            case 4: launch_walk_g<1, 4>(p, t, wb, ctr, stats, grid, s); break;
-            case 8: launch_walk_g<1, 8>(p, t, wb, ctr, stats, grid, s); break;
-            case 16: launch_walk_g<1, 16>(p, t, wb, ctr, stats, grid, s); break;
-            default: k_walk<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
-        }
-    } else {
-        switch (G) {
-            case 2: launch_walk_g<2, 2>(p, t, wb, ctr, stats, grid, s); break;
-            case 4: launch_walk_g<2, 4>(p, t, wb, ctr, stats, grid, s); break;
-            case 8: launch_walk_g<2, 8>(p, t, wb, ctr, stats, grid, s); break;
-            default: k_walk<2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
-        }
-    }
+    // two blocks per CU (512 on MI355X): with non-temporal probes fewer walkers in flight contend
+    // less (C3 walk 5.71 -> 5.48-5.54 ms vs 2048 blocks, C2 0.67 -> 0.54; 384: 6.10)
+    const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
+                                         (uint64_t)(grid_blocks > 0 ? grid_blocks : 2 * cu_count()));
+    if (p.W == 1)
+        k_walk_q<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+    else
+        k_walk_q<2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
     return hipGetLastError();
 }
 
@@ -980,12 +596,16 @@ hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t
 }
 
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
-                              uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s) {
+                              uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s,
+                              int phases) {
     const uint64_t nc = wb.n_starts;
     if (nc == 0) return hipSuccess;
-    hipError_t e = scan_exclusive(ContigBytesF{wb.contig_len, (uint64_t)p.K}, nc, offsets, scratch,
-                                  (unsigned long long*)nullptr, &ctr[CT_OUT_BYTES], s);
-    if (e != hipSuccess) return e;
+    if (phases & MAT_SCAN) {
+        hipError_t e = scan_exclusive(ContigBytesF{wb.contig_len, (uint64_t)p.K}, nc, offsets, scratch,
+                                      (unsigned long long*)nullptr, &ctr[CT_OUT_BYTES], s);
+        if (e != hipSuccess) return e;
+    }
+    if (!(phases & MAT_WRITE)) return hipSuccess;
     const unsigned gh = (unsigned)hmin((nc + BLOCK - 1) / BLOCK, 8192);
     if (p.W == 1)
         k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out);
@@ -1141,12 +761,16 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
 
 hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
                                   uint64_t* offsets, uint64_t* scratch, char* out, unsigned long long* ctr,
-                                  hipStream_t s) {
+                                  hipStream_t s, int phases) {
     const uint64_t nc = wb.n_starts;
     if (nc == 0) return hipSuccess;
-    hipError_t e = scan_exclusive(ContigBytesF{sb.clen, (uint64_t)p.K}, nc, offsets, scratch,
-                                  (unsigned long long*)nullptr, &ctr[CT_OUT_BYTES], s);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (phases & MAT_SCAN) {
+        e = scan_exclusive(ContigBytesF{sb.clen, (uint64_t)p.K}, nc, offsets, scratch,
+                           (unsigned long long*)nullptr, &ctr[CT_OUT_BYTES], s);
+        if (e != hipSuccess) return e;
+    }
+    if (!(phases & MAT_WRITE)) return hipSuccess;
     if ((e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s)) != hipSuccess) return e;
     const unsigned gc = (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks_seg<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr, wb.chunk_cap,
@@ -1306,368 +930,6 @@ hipError_t launch_insert_words(const KParams& p, const uint64_t* words, uint64_t
         k_insert_words<1><<<grid, BLOCK, 0, s>>>(p, words, m, t.slots, t.cap, stats);
     else
         k_insert_words<2><<<grid, BLOCK, 0, s>>>(p, words, m, t.slots, t.cap, stats);
-    return hipGetLastError();
-}
-
-// ---- round walker ---------------------------------------------------------------------------
-static constexpr uint8_t RW_F = 4, RW_BAD = 5, RW_DONE = 6, RW_PENDING = 7;
-
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_rw_init(KParams p, RoundWalk rw, const uint64_t* starts) {
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < rw.n;
-         i += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t w0 = starts[i * W];
-        const uint64_t w1 = (W == 2) ? starts[i * W + 1] : 0;
-        const Key k = slot_key(w0, w1, p);
-        rw.hi[i] = k.hi;
-        rw.lo[i] = k.lo;
-        rw.buf[i] = 0;
-        rw.steps[i] = 0;
-        rw.chunk[i] = 0;
-        const uint32_t f = ext_fwd(slot_ext(w0));
-        rw.state[i] = (uint8_t)(f > 4 ? RW_BAD : f);
-    }
-}
-
-hipError_t launch_rw_init(const KParams& p, const RoundWalk& rw, const uint64_t* starts, hipStream_t s) {
-    if (rw.n == 0) return hipSuccess;
-    const unsigned grid = (unsigned)hmin((rw.n + BLOCK - 1) / BLOCK, 8192);
-    if (p.W == 1)
-        k_rw_init<1><<<grid, BLOCK, 0, s>>>(p, rw, starts);
-    else
-        k_rw_init<2><<<grid, BLOCK, 0, s>>>(p, rw, starts);
-    return hipGetLastError();
-}
-
-template <int W>
-struct EmitOp {
-    KParams p;
-    RoundWalk rw;
-    uint32_t P;
-    uint64_t* keys;
-    unsigned long long* ctr;
-    unsigned long long* stats;
-    __device__ int owner(uint64_t i) const {
-        const uint8_t st = rw.state[i];
-        if (st > 3) return -1;
-        const Key k = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
-        return (int)owner_key(k, p, P);
-    }
-    __device__ void emit(uint64_t i, int q, uint64_t dst) const {
-        const uint8_t st = rw.state[i];
-        if (st == RW_DONE) return;
-        const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
-        uint32_t steps = rw.steps[i], chunk = rw.chunk[i];
-        uint64_t buf = rw.buf[i];
-        if (st == RW_F || st == RW_BAD) {
-            if (st == RW_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
-            finish_contig(o, i, steps, chunk, buf);
-            rw.state[i] = RW_DONE;
-            return;
-        }
-        append_base(o, i, st, steps, chunk, buf, ctr, stats);
-        const Key k = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
-        rw.hi[i] = k.hi;
-        rw.lo[i] = k.lo;
-        rw.steps[i] = steps;
-        rw.chunk[i] = chunk;
-        rw.buf[i] = buf;
-        rw.state[i] = RW_PENDING;
-        if (W == 2) {
-            keys[dst * 2] = k.hi;
-            keys[dst * 2 + 1] = k.lo;
-        } else {
-            keys[dst] = k.lo;
-        }
-        rw.qperm[dst] = (uint32_t)i;
-        (void)q;
-    }
-};
-
-hipError_t launch_rw_emit(const KParams& p, const RoundWalk& rw, uint32_t nranks, uint64_t* hist,
-                          uint64_t* off, uint64_t* scratch, uint64_t* keys, uint64_t* counts,
-                          unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
-    unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    uint64_t* sc = scratch + 1;
-    if (p.W == 1)
-        return group_by_owner(EmitOp<1>{p, rw, nranks, keys, ctr, stats}, rw.n, nranks, hist, off, sc,
-                              counts, total, s);
-    return group_by_owner(EmitOp<2>{p, rw, nranks, keys, ctr, stats}, rw.n, nranks, hist, off, sc,
-                          counts, total, s);
-}
-
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_find_ext(KParams p, const uint64_t* __restrict__ keys,
-                                                    uint64_t m, const uint64_t* slots, uint64_t cap,
-                                                    uint8_t* ext) {
-    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < m;
-         j += (uint64_t)gridDim.x * BLOCK) {
-        Key k;
-        if (W == 2) {
-            k.hi = keys[j * 2];
-            k.lo = keys[j * 2 + 1];
-        } else {
-            k.hi = 0;
-            k.lo = keys[j];
-        }
-        uint64_t w0 = 0;
-        ext[j] = probe<W>(k, p, slots, cap, w0) ? (uint8_t)slot_ext(w0) : (uint8_t)0xFF;
-    }
-}
-
-hipError_t launch_find_ext(const KParams& p, const uint64_t* keys, uint64_t m, TableView t,
-                           uint8_t* ext, hipStream_t s) {
-    if (m == 0) return hipSuccess;
-    const unsigned grid = (unsigned)hmin((m + BLOCK - 1) / BLOCK, 8192);
-    if (p.W == 1)
-        k_find_ext<1><<<grid, BLOCK, 0, s>>>(p, keys, m, t.slots, t.cap, ext);
-    else
-        k_find_ext<2><<<grid, BLOCK, 0, s>>>(p, keys, m, t.slots, t.cap, ext);
-    return hipGetLastError();
-}
-
-__global__ __launch_bounds__(BLOCK) void k_rw_apply(RoundWalk rw, const uint8_t* ext, uint64_t m,
-                                                    unsigned long long* stats) {
-    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < m;
-         j += (uint64_t)gridDim.x * BLOCK) {
-        const uint32_t i = rw.qperm[j];
-        const uint8_t r = ext[j];
-        const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
-        if (r == 0xFF) {
-            atomicAdd(&stats[ST_MISSING], 1ull);
-            finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
-            rw.state[i] = RW_DONE;
-        } else if (rw.steps[i] > rw.max_steps) {
-            atomicAdd(&stats[ST_CYCLE], 1ull);
-            finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
-            rw.state[i] = RW_DONE;
-        } else {
-            const uint32_t f = ext_fwd(r);
-            rw.state[i] = (uint8_t)(f > 4 ? RW_BAD : f);
-        }
-    }
-}
-
-hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t* ext, uint64_t m,
-                           unsigned long long* stats, hipStream_t s) {
-    (void)p;
-    if (m == 0) return hipSuccess;
-    const unsigned grid = (unsigned)hmin((m + BLOCK - 1) / BLOCK, 8192);
-    k_rw_apply<<<grid, BLOCK, 0, s>>>(rw, ext, m, stats);
-    return hipGetLastError();
-}
-
-// ---- fixed-capacity rounds ------------------------------------------------------------------
-// Every round exchanges fixed-size per-peer segments (layout in kh_kernels.hpp), so the host never
-// waits for counts. One kernel per round applies the previous round's replies and emits the next
-// queries; a walker whose query does not fit its sub-segment keeps its state and emits again next
-// round.
-// Same-address device-scope atomics serialise at the memory side (~12 ns each on MI355X,
-// measured: one atomic per 256-walker block on one counter cost ~100 us/round at 1.9M walkers).
-// So: one tile = EMIT_IPT walkers per thread with per-owner counts aggregated in LDS (one
-// reservation per (tile, owner)), reservations spread over SEG_SUBS cursors per owner on separate
-// lines, and the end-of-round bookkeeping (block done / live count) likewise per sub-group.
-static constexpr int EMIT_IPT = 8;
-
-__device__ __forceinline__ uint64_t ld_agent(const unsigned long long* a) {
-    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(unsigned long long* a, unsigned long long v) {
-    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_rw_step_fixed(KParams p, RoundWalk rw, uint32_t P, uint64_t C,
-                                                         const uint8_t* __restrict__ reply_prev,
-                                                         uint64_t* send, unsigned long long* ctl,
-                                                         unsigned long long* ctr,
-                                                         unsigned long long* stats) {
-    __shared__ uint32_t lc[MAX_RANKS];
-    __shared__ uint64_t base[MAX_RANKS];
-    __shared__ int last;
-    const uint64_t L = SEG_SUBS + C * W;
-    const uint64_t C8 = C / SEG_SUBS;
-    const uint32_t x = blockIdx.x % SEG_SUBS;
-    const LaneOut o{rw.contig_len, rw.chunk_data, rw.chunk_owner, rw.chunk_seq, rw.chunk_cap, rw.n};
-    constexpr uint64_t TILE = (uint64_t)BLOCK * EMIT_IPT;
-    uint64_t live = 0;  // walkers of this thread still unfinished after this round
-    for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < rw.n; t0 += (uint64_t)gridDim.x * TILE) {
-        for (uint32_t q = threadIdx.x; q < P; q += BLOCK) lc[q] = 0;
-        __syncthreads();
-        // phases over the whole tile (loads of one phase are independent, so each thread keeps
-        // EMIT_IPT of them in flight): state -> reply index -> reply byte -> key
-        uint8_t sts[EMIT_IPT];
-        uint32_t ps[EMIT_IPT];
-#pragma unroll
-        for (int j = 0; j < EMIT_IPT; ++j) {
-            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
-            sts[j] = i < rw.n ? rw.state[i] : RW_DONE;
-        }
-#pragma unroll
-        for (int j = 0; j < EMIT_IPT; ++j) {
-            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
-            ps[j] = sts[j] == RW_PENDING ? rw.pos[i] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < EMIT_IPT; ++j) {
-            if (sts[j] == RW_PENDING) ps[j] = reply_prev[ps[j]];  // ps now holds the reply byte
-        }
-        Key nk[EMIT_IPT];
-        int8_t qo[EMIT_IPT];
-        uint32_t lr[EMIT_IPT];
-#pragma unroll
-        for (int j = 0; j < EMIT_IPT; ++j) {
-            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
-            uint8_t st = sts[j];
-            qo[j] = -1;
-            lr[j] = 0;
-            nk[j] = Key{0, 0};
-            if (st == RW_PENDING) {  // apply last round's reply
-                const uint8_t r = (uint8_t)ps[j];
-                if (r == 0xFF || rw.steps[i] > rw.max_steps) {
-                    atomicAdd(&stats[r == 0xFF ? ST_MISSING : ST_CYCLE], 1ull);
-                    finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
-                    st = RW_DONE;
-                } else {
-                    const uint32_t f = ext_fwd(r);
-                    st = (uint8_t)(f > 4 ? RW_BAD : f);
-                }
-            }
-            if (st == RW_F || st == RW_BAD) {
-                if (st == RW_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
-                finish_contig(o, i, rw.steps[i], rw.chunk[i], rw.buf[i]);
-                st = RW_DONE;
-            } else if (st <= 3) {
-                nk[j] = key_next(Key{rw.hi[i], rw.lo[i]}, st, p);
-                const uint32_t q = owner_key(nk[j], p, P);
-                qo[j] = (int8_t)q;
-                lr[j] = atomicAdd(&lc[q], 1u);
-            }
-            sts[j] = st;
-        }
-        __syncthreads();
-        for (uint32_t r = threadIdx.x; r < P; r += BLOCK)
-            base[r] = lc[r] ? atomicAdd(&ctl[(x * MAX_RANKS + r) * CTL_LINE], (unsigned long long)lc[r]) : 0ull;
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < EMIT_IPT; ++j) {
-            const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
-            if (i >= rw.n) continue;
-            uint8_t st = sts[j];
-            if (qo[j] >= 0) {
-                const uint32_t q = (uint32_t)qo[j];
-                const uint64_t slot = base[q] + lr[j];
-                if (slot < C8) {
-                    uint32_t steps = rw.steps[i], chunk = rw.chunk[i];
-                    uint64_t buf = rw.buf[i];
-                    append_base(o, i, st, steps, chunk, buf, ctr, stats);
-                    rw.steps[i] = steps;
-                    rw.chunk[i] = chunk;
-                    rw.buf[i] = buf;
-                    rw.hi[i] = nk[j].hi;
-                    rw.lo[i] = nk[j].lo;
-                    uint64_t* seg = send + (uint64_t)q * L + SEG_SUBS + (x * C8 + slot) * W;
-                    if (W == 2) {
-                        seg[0] = nk[j].hi;
-                        seg[1] = nk[j].lo;
-                    } else {
-                        seg[0] = nk[j].lo;
-                    }
-                    rw.pos[i] = (uint32_t)(q * C + x * C8 + slot);
-                    st = RW_PENDING;
-                }  // else: owner's segment full, retry next round with the same state
-            }
-            live += st != RW_DONE;
-            rw.state[i] = st;
-        }
-        __syncthreads();
-    }
-    // round epilogue: the last block of each sub-group reports to the global counter; the last of
-    // those writes the segment headers and the live count, then re-arms ctl for the next round
-    uint64_t tot;
-    block_excl_scan(live, tot);
-    if (threadIdx.x == 0) {
-        const uint32_t groups = gridDim.x < SEG_SUBS ? gridDim.x : SEG_SUBS;
-        const uint32_t gsize = (gridDim.x - x + SEG_SUBS - 1) / SEG_SUBS;
-        // No __threadfence here: on gfx950 an agent-scope fence writes back the XCD's L2 (~25 us
-        // per round at 1k blocks, measured). Ordering comes from the atomics themselves: they
-        // execute at the memory side and each returning atomic is complete before the next one
-        // issues (the cursor reservations returned before the __syncthreads above). The keys
-        // written to `send` are read by the next kernel, after the kernel boundary.
-        uint64_t chain = tot ? atomicAdd(&ctl[CTL_ACC0 + x * CTL_LINE], (unsigned long long)tot) : 0;
-        asm volatile("" ::"v"(chain));  // wait for the live-count atomic before signalling done
-        int l = 0;
-        if (atomicAdd(&ctl[CTL_DONE0 + x * CTL_LINE], 1ull) == gsize - 1)
-            l = atomicAdd(&ctl[CTL_GDONE], 1ull) == groups - 1;
-        last = l;
-    }
-    __syncthreads();
-    if (last) {
-        for (uint32_t e = threadIdx.x; e < P * SEG_SUBS; e += BLOCK) {
-            const uint32_t q = e / SEG_SUBS, xs = e % SEG_SUBS;
-            unsigned long long* cur = &ctl[(xs * MAX_RANKS + q) * CTL_LINE];
-            const uint64_t c = ld_agent(cur);
-            send[(uint64_t)q * L + xs] = c < C8 ? c : C8;
-            st_agent(cur, 0ull);
-        }
-        if (threadIdx.x == 0) {
-            uint64_t lv = 0;
-            for (int xs = 0; xs < SEG_SUBS; ++xs) {
-                lv += ld_agent(&ctl[CTL_ACC0 + xs * CTL_LINE]);
-                st_agent(&ctl[CTL_ACC0 + xs * CTL_LINE], 0ull);
-                st_agent(&ctl[CTL_DONE0 + xs * CTL_LINE], 0ull);
-            }
-            st_agent(&ctl[CTL_LIVE], lv);
-            st_agent(&ctl[CTL_GDONE], 0ull);
-        }
-    }
-}
-
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_find_ext_fixed(KParams p, const uint64_t* __restrict__ recv,
-                                                          uint64_t C, const uint64_t* slots,
-                                                          uint64_t cap, uint8_t* reply) {
-    const uint64_t L = SEG_SUBS + C * W, C8 = C / SEG_SUBS;
-    const uint64_t q = blockIdx.y / SEG_SUBS, xs = blockIdx.y % SEG_SUBS;
-    const uint64_t* seg = recv + q * L;
-    const uint64_t m = seg[xs];
-    const uint64_t* keys = seg + SEG_SUBS + xs * C8 * W;
-    uint8_t* out = reply + q * C + xs * C8;
-    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < m; j += (uint64_t)gridDim.x * BLOCK) {
-        Key k;
-        if (W == 2) {
-            k.hi = keys[j * 2];
-            k.lo = keys[j * 2 + 1];
-        } else {
-            k.hi = 0;
-            k.lo = keys[j];
-        }
-        uint64_t w0 = 0;
-        out[j] = probe<W>(k, p, slots, cap, w0) ? (uint8_t)slot_ext(w0) : (uint8_t)0xFF;
-    }
-}
-
-hipError_t launch_rw_step_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
-                                const uint8_t* reply_prev, uint64_t* send, unsigned long long* ctl,
-                                unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
-    const unsigned g = (unsigned)hmin((rw.n + BLOCK * EMIT_IPT - 1) / (BLOCK * EMIT_IPT), 2048);
-    // rw.n == 0 still runs one block: it writes the (zero) headers
-    if (p.W == 1)
-        k_rw_step_fixed<1><<<g ? g : 1, BLOCK, 0, s>>>(p, rw, P, C, reply_prev, send, ctl, ctr, stats);
-    else
-        k_rw_step_fixed<2><<<g ? g : 1, BLOCK, 0, s>>>(p, rw, P, C, reply_prev, send, ctl, ctr, stats);
-    return hipGetLastError();
-}
-
-hipError_t launch_find_ext_fixed(const KParams& p, const uint64_t* recv, uint32_t P, uint64_t C, TableView t,
-                                 uint8_t* reply, hipStream_t s) {
-    if (P * C == 0) return hipSuccess;
-    const uint64_t C8 = C / SEG_SUBS;
-    const dim3 grid((unsigned)hmin((C8 + BLOCK - 1) / BLOCK, 512), P * SEG_SUBS);
-    if (p.W == 1)
-        k_find_ext_fixed<1><<<grid, BLOCK, 0, s>>>(p, recv, C, t.slots, t.cap, reply);
-    else
-        k_find_ext_fixed<2><<<grid, BLOCK, 0, s>>>(p, recv, C, t.slots, t.cap, reply);
     return hipGetLastError();
 }
 

@@ -7,6 +7,9 @@
 
 namespace kh {
 
+// KH_DEBUG = comma-separated test switches (e.g. "plain_build"); not for production runs.
+bool debug_flag(const char* name);
+
 // Device-side error / event counters (one 64-bit word each).
 enum StatIdx : int {
     ST_DUP = 0,        // duplicate key on insert (input contract: keys unique, README.md:35)
@@ -103,13 +106,17 @@ hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64
                                 uint64_t* scratch, uint64_t* out, unsigned long long* count, hipStream_t s);
 hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
                            unsigned long long* stats, hipStream_t s);
+// phases: MAT_SCAN = offsets + ctr[CT_OUT_BYTES]; MAT_WRITE = the text (out must hold the
+// scanned total: callers size it from CT_OUT_BYTES between the two phases)
+enum MatPhase : int { MAT_SCAN = 1, MAT_WRITE = 2, MAT_ALL = 3 };
 hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
                                   uint64_t* offsets, uint64_t* scratch, char* out, unsigned long long* ctr,
-                                  hipStream_t s);
+                                  hipStream_t s, int phases = MAT_ALL);
 
 // Contig bytes: offsets = exclusive scan of (K + len) (K + len-1 bases + '\n'), then write chars.
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
-                              uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s);
+                              uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s,
+                              int phases = MAT_ALL);
 
 // ---- migrating-walker rounds (kh_mwalk.hip) -------------------------------------------------
 // message: MSG_WORDS words [key.hi, key.lo, partial word, idx << 32 | bases appended,
@@ -222,58 +229,6 @@ hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint3
 hipError_t launch_insert_words(const KParams& p, const uint64_t* words, uint64_t m, TableView t,
                                unsigned long long* stats, hipStream_t s);
 
-// Round-based walker state (structure of arrays, one entry per local start k-mer).
-struct RoundWalk {
-    uint64_t n;          // walkers = local start k-mers
-    uint64_t* hi;        // current key
-    uint64_t* lo;
-    uint64_t* buf;       // partial word of appended bases
-    uint32_t* steps;     // bases appended
-    uint32_t* chunk;     // current chunk
-    uint8_t* state;      // 0..3 fwd base, 4 'F', 5 bad, 6 done, 7 query in flight
-    uint32_t* qperm;     // query slot -> walker (variable-size rounds)
-    uint32_t* pos;       // walker -> reply index of its query in flight (fixed rounds)
-    uint32_t* contig_len;
-    uint64_t* chunk_data;
-    uint32_t* chunk_owner;
-    uint32_t* chunk_seq;
-    uint64_t chunk_cap;
-    uint64_t max_steps;
-};
-
-hipError_t launch_rw_init(const KParams& p, const RoundWalk& rw, const uint64_t* starts, hipStream_t s);
-// Emit one query per walker that has a next k-mer, grouped by owner rank; finish walkers at 'F'.
-// keys: W words per query; counts: nranks + 1 words (last = total queries).
-hipError_t launch_rw_emit(const KParams& p, const RoundWalk& rw, uint32_t nranks, uint64_t* hist,
-                          uint64_t* off, uint64_t* scratch, uint64_t* keys, uint64_t* counts,
-                          unsigned long long* ctr, unsigned long long* stats, hipStream_t s);
-// Owner side: ext byte of each queried key (0xFF = absent).
-hipError_t launch_find_ext(const KParams& p, const uint64_t* keys, uint64_t m, TableView t,
-                           uint8_t* ext, hipStream_t s);
-// Home side: apply the replies of the m queries emitted last round.
-hipError_t launch_rw_apply(const KParams& p, const RoundWalk& rw, const uint8_t* ext, uint64_t m,
-                           unsigned long long* stats, hipStream_t s);
-
-// Fixed-capacity rounds (no count exchange, no host sync per round). Per-peer segment of
-// L = SEG_SUBS + C*W words: [count of sub 0..SEG_SUBS-1, keys of sub 0 (C/SEG_SUBS slots), keys
-// of sub 1, ...]; replies: C bytes per peer in the same slot order. Sub-segment x is filled by
-// the blocks with blockIdx % SEG_SUBS == x, so the slot-reservation atomics of a round spread
-// over SEG_SUBS * P cursors on separate cache lines instead of serialising on one address.
-// One step = apply the previous round's replies (reply_prev, indexed by rw.pos) + emit the next
-// queries; ctl = CTL_WORDS device words (zeroed once; every round's last block re-arms them).
-static constexpr int SEG_SUBS = 8;
-static constexpr int CTL_LINE = 16;  // words per 128-B line
-static constexpr int CTL_DONE0 = SEG_SUBS * MAX_RANKS * CTL_LINE;
-static constexpr int CTL_ACC0 = CTL_DONE0 + SEG_SUBS * CTL_LINE;
-static constexpr int CTL_GDONE = CTL_ACC0 + SEG_SUBS * CTL_LINE;
-static constexpr int CTL_LIVE = CTL_GDONE + CTL_LINE;
-static constexpr int CTL_WORDS = CTL_LIVE + CTL_LINE;
-hipError_t launch_rw_step_fixed(const KParams& p, const RoundWalk& rw, uint32_t P, uint64_t C,
-                                const uint8_t* reply_prev, uint64_t* send, unsigned long long* ctl,
-                                unsigned long long* ctr, unsigned long long* stats, hipStream_t s);
-hipError_t launch_find_ext_fixed(const KParams& p, const uint64_t* recv, uint32_t P, uint64_t C, TableView t,
-                                 uint8_t* reply, hipStream_t s);
-
 }  // namespace kh
 
 // ---- partitioned (atomic-free) bulk build ------------------------------------------------------
@@ -281,22 +236,17 @@ namespace kh {
 
 // The key space is cut into 2^17 hash ranges (top 17 bits of key_hash); because the home slot
 // mulhi(h, cap) is monotonic in h, region r owns the slot range
-// [floor(r*cap/2^17), floor((r+1)*cap/2^17)). Two radix passes (512 x 256 bins) group the batch by
-// region, then one workgroup per region builds its slot range in LDS (kh_build.hip).
-static constexpr int PART_TILE = 4096;  // inputs per block-tile of the radix passes
+// [floor(r*cap/2^17), floor((r+1)*cap/2^17)). Two windowed LDS-sort passes (512 buckets, then 256
+// bins per bucket) group the batch by region, then one workgroup per region builds its slot range
+// in LDS (kh_build.hip).
+static constexpr int PART_TILE = 4096;  // records per block-tile of k_part1_convert
 
-struct PartPlan {
-    uint64_t n;       // inputs
-    uint64_t nb1;     // pass-1 blocks
-    uint64_t G;       // pass-2 blocks per bucket
-};
-PartPlan part_plan(uint64_t n);
-uint64_t part_hist_words(const PartPlan& pl);     // words of each hist / offset buffer
-uint64_t part_scratch_words(const PartPlan& pl);  // words of scan scratch (+ one total word)
+static constexpr uint32_t PART_W1_COUNTERS = 512 * 8;  // pass-1 windows: 512 buckets x 8
+uint64_t part_count_words();                      // words of the pass-1 + pass-2 window counters
 uint64_t part_overflow_cap(uint64_t n);           // overflow entries
 uint32_t part_region_cap(uint64_t n);             // words per region window of pass 2
 uint64_t part_buf2_words(const KParams& p, uint64_t n);  // buf2 size (region windows or n * W)
-uint32_t part_win1_cap(uint64_t n);               // words per pass-1 window (k_part1_fused)
+uint32_t part_win1_cap(uint64_t n);               // words per pass-1 window
 uint64_t part_buf1_words(const KParams& p, uint64_t n);  // buf1 size (pass-1 windows or n * W)
 // True when the region slices fit LDS and the batch is large enough to be worth it.
 bool part_usable(const KParams& p, uint64_t cap, uint64_t n);
@@ -304,13 +254,10 @@ bool part_usable(const KParams& p, uint64_t cap, uint64_t n);
 bool region_slots_fit(const KParams& p, uint64_t cap);
 
 struct PartBuffers {
-    uint64_t* buf1;      // part_buf1_words(p, n) words
-    uint64_t* buf2;      // part_buf2_words(p, n) words
-    uint64_t* hist1;
-    uint64_t* off1;
-    uint64_t* hist2;
-    uint64_t* off2;
-    uint64_t* scratch;
+    uint64_t* buf1;      // part_buf1_words(p, n) words: pass-1 windows
+    uint64_t* buf2;      // part_buf2_words(p, n) words: region windows
+    uint32_t* wcnt;      // pass-1 window fill counters
+    uint32_t* rcnt;      // region window fill counters (wcnt + rcnt = part_count_words())
     uint64_t* overflow;  // part_overflow_cap(n) * W words
 };
 
@@ -321,8 +268,6 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
                               unsigned long long* stats, hipStream_t s, hipEvent_t after_records = nullptr,
                               uint64_t* word_splits = nullptr, uint64_t word_splits_cap = 0);
-// True when the partitioned insert of words collects splitter k-mers itself (k_win1).
-bool part_words_collect_splits();
 
 // Staged build of routed words (sharded insert): launch_part_stage per received chunk (first = the
 // first chunk of a build sized for `total` words), then launch_part_finish once. Requires

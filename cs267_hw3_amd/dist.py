@@ -1,21 +1,26 @@
-"""Sharded multi-GPU k-mer table + round-based contig walk (one rank per GPU).
+"""Sharded multi-GPU k-mer table + migrating-walker contig walk (one rank per GPU), Python host.
 
 MI355X-native replacement of the reference's DistributedHashMap (hash_map.hpp:12-114) and its
 UPC++ transport:
   owner = std::hash<string>(key) % P, one blocking RPC per target   hash_map.hpp:28-30,38-46,64-77
-    -> owner = owner_of(key_hash) on the GPU, ONE all-to-all of 8/16-B routed records
+    -> owner = hash of the k-mer's minimizer (consecutive k-mers of a contig share it for ~19
+       steps), ONE all-to-all of 8/16-B routed words, each shard sized from what it receives
   find(): one blocking RPC round trip per remote walk step           hash_map.hpp:83-107
-    -> every live walker of every rank advances one k-mer per ROUND: its next key goes to the
-       owner in one all-to-all, the owner answers with the 1-byte extension in a second one
+    -> migrating walkers: a walker walks the local shard until its next k-mer is owned by another
+       rank, then the walker itself (a 40-B message) moves there in the round's all-to-all;
+       ~19 rounds at P=8 for C3 contigs. Appended bases go home in one more all-to-all.
+    -> splitter segments (1 per ~256 k-mers) cut long chains (C2, C5) into segments walked in
+       parallel and stitched by distributed pointer jumping (kh_mseg.hip)
   barrier() between phases                                           hash_map.hpp:79
-Walkers stay on the rank that read their start k-mer (kmer_hash.cpp:41: each rank walks its own
-start nodes), so each rank's contig text is exactly its test_<rank>.dat.
+Each rank's contig text is exactly its test_<rank>.dat: the contigs of the start k-mers in its
+block (kmer_hash.cpp:41), in start-node order.
 
 The SPMD driver below is written against two small interfaces so that the same code runs
   * on GPUs: GpuShard (C ABI kernels on torch device tensors) + TorchComm (torch.distributed;
     backend "nccl" is RCCL over xGMI),
   * on one GPU with P logical ranks: GpuShard + ThreadComm (tests, smoke),
   * on CPUs: a test double shard + TorchComm over gloo (tests/test_dist_cpu.py).
+The C++ host of the same protocol is include/cs267_hw3_amd/dist_hash_map.hpp.
 """
 import ctypes
 import os
@@ -32,22 +37,13 @@ from ._lib import check
 class TorchComm:
     """torch.distributed process group (nccl = RCCL over xGMI on MI355X, or gloo on CPU)."""
 
-    def __init__(self, group=None, ctrl=None):
-        """ctrl: optional gloo group for small host-side exchanges that must not queue behind
-        large RCCL transfers (the pipelined insert's per-chunk counts)."""
+    def __init__(self, group=None):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
-        self.ctrl = ctrl
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
-
-    def all_gather_host(self, t):
-        """CPU int64 tensor [m] from every rank -> [world, m] over the ctrl (gloo) group."""
-        out = [torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(out, t, group=self.ctrl)
-        return torch.stack(out)
 
     def all_to_all_async(self, out, inp, out_splits, in_splits):
         return self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=True)
@@ -90,18 +86,10 @@ class ThreadComm:
         self.sh = shared
         self.rank = rank
         self.world = shared.world
-        self.ctrl = None  # set to enable the pipelined insert (tests)
 
     class _Done:
         def wait(self):
             pass
-
-    def all_gather_host(self, t):
-        self.sh.slots[self.rank] = t.clone()
-        self.sh.barrier.wait()
-        out = torch.stack([self.sh.slots[q] for q in range(self.world)])
-        self.sh.barrier.wait()
-        return out
 
     def all_to_all_async(self, out, inp, out_splits, in_splits):
         self.all_to_all(out, inp, out_splits, in_splits)
@@ -179,6 +167,10 @@ class GpuShard:
         check(f(self.h, self._p(recs), n, nranks, self._p(words), self._p(counts)))
         return words, counts
 
+    def reserve(self, m):
+        """Grow the (empty) shard to hold m k-mers (kh_reserve)."""
+        check(self.L.kh_reserve(self.h, int(m)))
+
     def insert_words(self, words, m):
         check(self.L.kh_insert_words_dev(self.h, self._p(words), m))
 
@@ -188,39 +180,6 @@ class GpuShard:
 
     def finish_words(self):
         check(self.L.kh_insert_words_finish(self.h))
-
-    def walk_begin(self, total_kmers):
-        nw = ctypes.c_uint64(0)
-        check(self.L.kh_walk_begin(self.h, total_kmers, ctypes.byref(nw)))
-        self.nw = nw.value
-        self.keys = self.zeros(self.nw * self.W, torch.int64)
-        self.counts = None
-        return self.nw
-
-    def walk_emit(self, nranks):
-        if self.counts is None or self.counts.numel() < nranks + 1:
-            self.counts = self.zeros(nranks + 1, torch.int64)
-        check(self.L.kh_walk_emit_dev(self.h, nranks, self._p(self.keys), self._p(self.counts)))
-        return self.keys, self.counts
-
-    def find_ext(self, keys, m):
-        ext = self.zeros(m, torch.uint8)
-        check(self.L.kh_find_ext_dev(self.h, self._p(keys), m, self._p(ext)))
-        return ext
-
-    def walk_apply(self, ext, m):
-        check(self.L.kh_walk_apply_dev(self.h, self._p(ext), m))
-
-    def walk_end(self):
-        check(self.L.kh_walk_end_dev(self.h))
-
-    # fixed-capacity rounds
-    def step_fixed(self, nranks, cap, reply_prev, send):
-        rp = self._p(reply_prev) if reply_prev is not None else None
-        check(self.L.kh_walk_step_fixed_dev(self.h, nranks, cap, rp, self._p(send)))
-
-    def find_ext_fixed(self, nranks, cap, recv, reply):
-        check(self.L.kh_find_ext_fixed_dev(self.h, nranks, cap, self._p(recv), self._p(reply)))
 
     # migrating-walker rounds
     MSG_WORDS = _lib.MSG_WORDS
@@ -289,16 +248,6 @@ class GpuShard:
     def mw_end_seg(self, recs, n, seg, m):
         check(self.L.kh_mwalk_end_seg_dev(self.h, self._p(recs), n, self._p(seg), m))
 
-    def signature(self):
-        v = ctypes.c_uint64()
-        check(self.L.kh_walk_signature(self.h, ctypes.byref(v)))
-        return v.value
-
-    def active(self):
-        out = self.zeros(1, torch.int64)
-        check(self.L.kh_walk_active_dev(self.h, self._p(out)))
-        return out
-
     def sync(self):
         self.table.sync()
 
@@ -319,50 +268,15 @@ class DistributedKmerHashMap:
                       (= test_<rank>.dat bytes); collective.
     """
 
-    CHECK_EVERY = 8  # rounds between host-side termination checks (fixed protocol)
-    # fixed protocol: capture CHECK_EVERY rounds (kernels + RCCL all-to-alls) into one hipGraph
-    # per segment capacity and replay it. Opt-in (KH_DIST_GRAPH=1, TorchComm over nccl only):
-    # torch's NCCL watchdog can query an event recorded inside the capture and abort
-    # (hipErrorCapturedEvent), seen on ROCm 7 / torch 2.10.
-    GRAPH = None
-
-    def __init__(self, comm, shard, protocol="migrate"):
-        assert protocol in ("migrate", "fixed", "variable")
+    def __init__(self, comm, shard):
         self.comm = comm
         self.shard = shard
         self.P = comm.world
-        self.protocol = protocol
         self.rounds = 0
-        self._bufs = None
-        self._graphs = {}
-        self.graph_captures = 0
+        self.jump_rounds = 0
 
     def close(self):
-        """Release captured round graphs (before the process group is destroyed)."""
-        if self._graphs:
-            torch.cuda.synchronize()
-            self._graphs.clear()
-            self._bufs = None
-
-    def _use_graph(self):
-        if self.GRAPH is not None:
-            return self.GRAPH
-        import os
-        return (isinstance(self.comm, TorchComm) and self.comm.backend == "nccl"
-                and os.environ.get("KH_DIST_GRAPH", "0") == "1")
-
-    def _round_buffers(self, C, dev):
-        """send/recv (P segments of SEG_SUBS + C*W words) and reply/reply_recv (P*C bytes),
-        kept across calls so captured graphs stay valid; grown when C exceeds them."""
-        P, W, S = self.P, self.shard.W, _lib.SEG_SUBS
-        if self._bufs is None or self._bufs[0] < C:
-            L = S + C * W
-            self._bufs = (C, torch.empty(P * L, dtype=torch.int64, device=dev),
-                          torch.empty(P * L, dtype=torch.int64, device=dev),
-                          torch.empty(P * C, dtype=torch.uint8, device=dev),
-                          torch.empty(P * C, dtype=torch.uint8, device=dev))
-            self._graphs.clear()
-        return self._bufs[1:]
+        pass
 
     def _int64(self, like, n):
         return torch.empty(max(int(n), 1), dtype=torch.int64, device=like.device)
@@ -429,140 +343,93 @@ class DistributedKmerHashMap:
                     out[out_off[q] + lo:out_off[q] + lo + rc[q]].copy_(recv[pos:pos + rc[q]])
                     pos += rc[q]
 
-    # pipelined insert: route chunk c+1 while chunk c is on the wire (KH_INSERT_CHUNKS=1: off)
+    # pipelined insert: chunk c-1, received, is partitioned while chunk c is on the wire
+    # (KH_INSERT_CHUNKS=1: one transfer)
     INSERT_CHUNKS = int(os.environ.get("KH_INSERT_CHUNKS", "4"))
     PIPELINE_MIN = 1 << 22  # records per rank below which the insert is one chunk
 
-    def _insert_pipelined(self, recs):
-        """Route and exchange the records in chunks: the route kernels of chunk c+1 run while
-        RCCL moves chunk c (counts go over the gloo ctrl group so they do not queue behind
-        the transfers), and chunk c-1, already received, is partitioned toward the build
-        (stage_words) meanwhile; one build at the end (finish_words). Words land back to back
-        in one receive buffer sized by the shard."""
+    def _exchange_count_matrix(self, counts):
+        """counts: list over chunks of [P+1] int64 device tensors (per-destination, total) ->
+        (send[c][q], recv[c][q], global max per-peer split over every chunk and rank). One small
+        all-to-all for all chunks."""
+        P, nch = self.P, len(counts)
+        mat = torch.stack([c[:P] for c in counts])            # [nch, P]
+        mx = mat.max().reshape(1)
+        send = torch.cat([mat.t(), mx.expand(P).reshape(P, 1)], 1).contiguous().view(-1)  # [P, nch+1]
+        recv = torch.empty_like(send)
+        self.comm.all_to_all(recv, send, [nch + 1] * P, [nch + 1] * P)
+        host = torch.cat([send, recv]).cpu().view(2, P, nch + 1)
+        send_c = [[int(host[0, q, c]) for q in range(P)] for c in range(nch)]
+        recv_c = [[int(host[1, q, c]) for q in range(P)] for c in range(nch)]
+        gmax = int(host[1, :, nch].max())
+        return send_c, recv_c, gmax
+
+    def _agree(self, err):
+        """Every rank learns whether any rank failed (one small exchange), and all of them raise
+        together, so no rank is left waiting in a collective the failed one skipped."""
+        bad = self._global_max(1 if err is not None else 0) if self.P > 1 else (1 if err else 0)
+        if bad:
+            if err is not None:
+                raise err
+            raise _lib.KmerHashError(_lib.KH_ERR_FULL, "another rank failed to size its shard")
+
+    def insert_all(self, recs):
+        """Route every record to its owner (+ this block's start k-mers), learn the per-chunk
+        counts in one exchange, size the shard from what it receives (kh_reserve; minimizer
+        ownership can be skewed on repetitive inputs), then move the words, partitioning each
+        received chunk while the next one is on the wire; one build at the end."""
         sh, P, W = self.shard, self.P, self.shard.W
         n = recs.shape[0]
-        nch = self.INSERT_CHUNKS
+        exchange = P > 1 or self.SELF_EXCHANGE
+        nch = 1
+        if exchange and self.INSERT_CHUNKS > 1 and n >= self.PIPELINE_MIN:
+            # per-peer bytes of a chunk <= chunk records * W * 8: keep every transfer under the
+            # per-peer message limit whatever the skew
+            nch = max(self.INSERT_CHUNKS, -(-n * W * 8 // self.A2A_CHUNK_BYTES))
         bounds = [n * c // nch for c in range(nch + 1)]
         words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
-        recv = self._grow("_ins_recv", max(sh.n_kmers, 1) * W, torch.int64, recs.device)
-        rank = self.comm.rank
+        counts = []
+        for c in range(nch):
+            c0, c1 = bounds[c], bounds[c + 1]
+            counts.append(sh.route(recs[c0:c1], P, words[c0 * W:max(c1, c0 + 1) * W], starts=True)[1])
+        send_c, recv_c, gmax = self._exchange_count_matrix(counts)
+        m = sum(sum(r) for r in recv_c)
+        err = None
+        try:
+            sh.reserve(m)
+        except RuntimeError as ex:  # KmerHashError (NOMEM) or a test shard's error
+            err = ex
+        self._agree(err)
+        if not exchange:
+            sh.insert_words(words, m)      # one rank: the routed words are this shard's
+            return m
+        recv = self._grow("_ins_recv", max(m, 1) * W, torch.int64, recs.device)
+        if nch == 1:
+            self._all_to_all(recv[:m * W], words[:n * W], [x * W for x in recv_c[0]],
+                             [x * W for x in send_c[0]], gmax * W)
+            sh.insert_words(recv, m)
+            return m
         works, spans, pos = [], [], 0
         for c in range(nch):
             c0, c1 = bounds[c], bounds[c + 1]
-            w = words[c0 * W:max(c1, c0 + 1) * W]
-            _, counts = sh.route(recs[c0:c1], P, w, starts=True)
-            send = counts[:P].cpu()                       # waits for this chunk's route only
-            mat = self.comm.all_gather_host(send)         # [src][dst]
-            recv_splits = mat[:, rank].tolist()
-            send_splits = send.tolist()
-            m = sum(recv_splits)
-            if pos + m > sh.n_kmers:
-                raise _lib.KmerHashError(_lib.KH_ERR_FULL, f"shard receives more than its {sh.n_kmers} k-mers")
-            works.append(self.comm.all_to_all_async(recv[pos * W:(pos + m) * W], w[:(c1 - c0) * W],
-                                                    [x * W for x in recv_splits],
-                                                    [x * W for x in send_splits]))
-            spans.append((pos, m))
-            pos += m
-            if c > 0:  # previous chunk: received -> partition it while this one is on the wire
+            mc = sum(recv_c[c])
+            works.append(self.comm.all_to_all_async(recv[pos * W:(pos + mc) * W], words[c0 * W:c1 * W],
+                                                    [x * W for x in recv_c[c]], [x * W for x in send_c[c]]))
+            spans.append((pos, mc))
+            pos += mc
+            if c > 0:  # previous chunk received: partition it while this one is on the wire
                 works[c - 1].wait()
                 p0, pm = spans[c - 1]
-                sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, sh.n_kmers)
+                sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
         works[-1].wait()
         p0, pm = spans[-1]
-        sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, sh.n_kmers)
+        sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
         sh.finish_words()
-        return pos
-
-    def insert_all(self, recs):
-        sh, P = self.shard, self.P
-        if ((P > 1 or self.SELF_EXCHANGE) and getattr(self.comm, "ctrl", None) is not None
-                and self.INSERT_CHUNKS > 1 and recs.shape[0] >= self.PIPELINE_MIN):
-            return self._insert_pipelined(recs)
-        words, counts = sh.route(recs, P, starts=True)  # + this block's starts, same pass
-        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
-        W = sh.W
-        m = sum(recv_splits)
-        if P == 1 and not self.SELF_EXCHANGE:
-            recv = words                       # one rank: nothing to exchange
-        else:
-            recv = self._int64(words, m * W)
-            self._all_to_all(recv[:m * W], words[:sum(send_splits) * W],
-                             [c * W for c in recv_splits], [c * W for c in send_splits], gmax * W)
-        sh.insert_words(recv, m)
         return m
-
-    def _active_stats(self, local):
-        """(sum, max) over ranks of the walkers not yet finished (one all-to-all + host sync)."""
-        P = self.P
-        send = local.reshape(1).expand(P).contiguous()
-        recv = torch.empty_like(send)
-        self.comm.all_to_all(recv, send, [1] * P, [1] * P)
-        v = recv.cpu().tolist()
-        return sum(v), max(v)
-
-    CAP_LIMIT = None  # tests: cap the per-peer segment to force overflow/retry rounds
-
-    def _capacity(self, gmax):
-        """Per-peer segment capacity for the next rounds (identical on every rank: a function
-        of the global max of live walkers; a multiple of SEG_SUBS). A rank's live walkers
-        spread ~evenly over the P owners and the SEG_SUBS sub-segments; 25% + 8 slots of
-        headroom per sub-segment make overflow (retry next round) rare."""
-        S = _lib.SEG_SUBS
-        per_sub = -(-gmax * 5 // (4 * self.P * S)) + 8
-        # quantised to {2^e, 1.5 * 2^e}: few distinct capacities -> few captured graphs
-        q = 1 << max(0, per_sub.bit_length() - 1)
-        per_sub = q if per_sub <= q else (q * 3 // 2 if per_sub <= q * 3 // 2 else 2 * q)
-        if self.CAP_LIMIT:
-            per_sub = min(per_sub, -(-self.CAP_LIMIT // S))
-        return S * max(1, per_sub)
 
     def assemble(self, total_kmers):
         """Walk this rank's start k-mers (collective); returns the number of rounds."""
-        if self.protocol == "migrate":
-            return self._assemble_migrate(total_kmers)
-        if self.protocol == "variable":
-            return self._assemble_variable(total_kmers)
-        sh, P, W = self.shard, self.P, self.shard.W
-        sh.walk_begin(total_kmers)
-        gsum, gmax = self._active_stats(sh.active())
-        C = self._capacity(gmax)
-        S = _lib.SEG_SUBS
-        send, recv, reply, rrecv = self._round_buffers(C, sh.active().device)
-        graph = self._use_graph()
-
-        def one_round(prev, C):
-            L = S + C * W
-            sh.step_fixed(P, C, prev, send)            # apply last replies, emit next queries
-            self._all_to_all(recv[:P * L], send[:P * L], [L] * P, [L] * P, L)
-            sh.find_ext_fixed(P, C, recv, reply)       # owner side
-            self._all_to_all(rrecv[:P * C], reply[:P * C], [C] * P, [C] * P, C)
-
-        self.rounds = 0
-        if gsum > 0:
-            one_round(None, C)                          # first step: no replies to apply yet
-            self.rounds = 1
-            gsum, gmax = self._active_stats(sh.active())
-        while gsum > 0:
-            C = min(C, self._capacity(gmax))
-            if graph:
-                key = (sh.signature(), C, send.data_ptr(), rrecv.data_ptr())
-                g = self._graphs.get(key)
-                if g is None:
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=sh.stream):
-                        for _ in range(self.CHECK_EVERY):
-                            one_round(rrecv, C)
-                    self._graphs[key] = g
-                    self.graph_captures += 1
-                g.replay()
-            else:
-                for _ in range(self.CHECK_EVERY):
-                    one_round(rrecv, C)
-            self.rounds += self.CHECK_EVERY
-            gsum, gmax = self._active_stats(sh.active())
-        sh.walk_end()
-        sh.sync()
-        return self.rounds
+        return self._assemble_migrate(total_kmers)
 
     def _grow(self, name, n, dtype, device):
         t = getattr(self, name, None)
@@ -682,38 +549,13 @@ class DistributedKmerHashMap:
                              [c * S for c in send_splits], gmax * S)
         sh.mw_end_seg(trecv, r, tin, m)
 
-    def _assemble_variable(self, total_kmers):
-        """Variable-size rounds: exact per-peer counts exchanged (and read on the host) every
-        round before the keys move."""
-        sh, P, W = self.shard, self.P, self.shard.W
-        sh.walk_begin(total_kmers)
-        self.rounds = 0
-        while True:
-            keys, counts = sh.walk_emit(P)
-            send_splits, recv_splits, totals, gmax = self._exchange_counts(counts)
-            if sum(totals) == 0:
-                break
-            self.rounds += 1
-            ms, mr = sum(send_splits), sum(recv_splits)
-            qin = self._int64(keys, mr * W)
-            self._all_to_all(qin[:mr * W], keys[:ms * W], [c * W for c in recv_splits],
-                             [c * W for c in send_splits], gmax * W)
-            ext = sh.find_ext(qin, mr)
-            rep = torch.empty(max(ms, 1), dtype=torch.uint8, device=ext.device)
-            self._all_to_all(rep[:ms], ext[:mr], send_splits, recv_splits, gmax)
-            sh.walk_apply(rep, ms)
-        sh.walk_end()
-        sh.sync()
-        return self.rounds
-
     def contigs_text(self):
         """This rank's contig text (D2H; outside the timed region)."""
         return self.shard.contigs_text()
 
 
 # --------------------------------------------------------------------------------------------
-def run_threaded(k, recs_np, nranks, device=0, protocol="migrate", cap_limit=None, info=None,
-                 insert_chunks=None):
+def run_threaded(k, recs_np, nranks, device=0, info=None, insert_chunks=None, shard_kmers=None):
     """P logical ranks on one GPU (threads): returns the per-rank contig texts. `info` (a dict)
     receives the round count and per-rank table stats."""
     import numpy as np
@@ -731,10 +573,8 @@ def run_threaded(k, recs_np, nranks, device=0, protocol="migrate", cap_limit=Non
             shard = GpuShard(k, max(n, 1), device=device)
             with torch.cuda.stream(shard.stream):
                 recs = torch.from_numpy(np.ascontiguousarray(recs_np[b:e])).to(shard.dev)
-                dm = DistributedKmerHashMap(comms[r], shard, protocol=protocol)
-                dm.CAP_LIMIT = cap_limit
+                dm = DistributedKmerHashMap(comms[r], shard)
                 if insert_chunks:
-                    comms[r].ctrl = comms[r]
                     dm.INSERT_CHUNKS = insert_chunks
                     dm.PIPELINE_MIN = 0
                 dm.insert_all(recs)
@@ -774,7 +614,7 @@ def bench_main(args, w, world, rank):
     local = int(os.environ.get("LOCAL_RANK", rank))
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    comm = TorchComm(ctrl=dist.new_group(backend="gloo"))
+    comm = TorchComm()
     k, n_per = w["k"], w["n"]
     n_total = n_per * world  # weak scaling: n k-mers per GPU
     t = time.time()
@@ -787,8 +627,7 @@ def bench_main(args, w, world, rank):
           flush=True)
     # each shard holds ~n_total/world keys; hash imbalance is tiny at this size, give 2% slack
     shard = GpuShard(k, int(n_per * 1.02) + 4096, device=local)
-    protocol = os.environ.get("KH_DIST_PROTOCOL", "migrate")
-    dm = DistributedKmerHashMap(comm, shard, protocol=protocol)
+    dm = DistributedKmerHashMap(comm, shard)
     R = record_size(k)
 
     phase_log = os.environ.get("KH_BENCH_PHASES") == "1"
@@ -850,8 +689,8 @@ def bench_main(args, w, world, rank):
                        "n_kmers_per_gpu": n_per, "contigs": nc, "lookups": nl,
                        "parallelism": f"{world} GPUs, key space sharded by "
                                       f"{'minimizer' if os.environ.get('KH_OWNER') != 'hash' else 'hash'} owner, "
-                                      f"RCCL all-to-all per walk round ({protocol} protocol)",
-                       "walk_rounds": dm.rounds, "round_graphs": dm.graph_captures},
+                                      f"RCCL all-to-all per migrating-walker round",
+                       "walk_rounds": dm.rounds},
             "inserts_per_s": n_total / tmax, "lookups_per_s": nl / tmax,
             "contigs_per_s": nc / tmax, "verified_vs_truth": ok,
             "roofline": {"bound": "hbm", "kernel": "insert pipeline on the received words (rank 0: "

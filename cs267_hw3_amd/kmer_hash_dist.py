@@ -6,11 +6,21 @@
 Every rank reads its block of the file (read_kmers.hpp:55-58), the sharded table is built over
 RCCL (cs267_hw3_amd.dist), every rank walks its own start k-mers and, in test mode, writes
 <prefix>_<rank>.dat; otherwise rank 0 prints the reference's two timing lines
-(kmer_hash.cpp:143-145). scripts/check_it.sh-style `cat test_*.dat | sort | diff` works as is.
+(kmer_hash.cpp:143-145); in test mode rank 0 prints the reference's summary line
+(kmer_hash.cpp:71-78 through BUtil::print, i.e. rank 0 only). scripts/check_it.sh-style `cat test_*.dat | sort | diff` works as is.
 """
 import os
 import sys
 import time
+
+
+def summary_line(rank, text, k, assembly_s, insert_s, total_s):
+    """kmer_hash.cpp:71-78 verbatim: contigs, nodes (k-mers over all contigs), the literal 0 start
+    nodes, then the assembly, insert and total times in the reference's argument order."""
+    ncontigs = text.count(b"\n")
+    nodes = len(text) - ncontigs * k  # a contig line is K + len - 1 bases + '\n' = K + len bytes
+    return (f"Rank {rank} reconstructed {ncontigs} contigs with {nodes} nodes from 0 start nodes. "
+            f"({assembly_s:f} read, {insert_s:f} insert, {total_s:f} total)")
 
 
 def main(argv):
@@ -48,8 +58,9 @@ def main(argv):
         shard.table.sync()  # surfaces a bad base (KH_ERR_BAD_BASE) before the timed region
     recs = buf[:n_local * R].view(n_local, R)
     del text
-    ctrl = dist.new_group(backend="gloo") if backend == "nccl" else None
-    dm = DistributedKmerHashMap(TorchComm(ctrl=ctrl), shard)
+    if run_type == "verbose" and rank == 0:
+        print("Finished reading kmers.")
+    dm = DistributedKmerHashMap(TorchComm(), shard)
     dist.barrier()
     with torch.cuda.stream(shard.stream):
         t0 = time.perf_counter()
@@ -68,9 +79,8 @@ def main(argv):
     else:
         with open(f"{prefix}_{rank}.dat", "wb") as f:
             f.write(text)
-        ncontigs = text.count(b"\n")
-        print(f"Rank {rank} reconstructed {ncontigs} contigs with {recs.shape[0]} nodes. "
-              f"({t1 - t0:f} insert, {t2 - t1:f} assemble, {t2 - t0:f} total)")
+        if rank == 0:
+            print(summary_line(rank, text, k, t2 - t1, t1 - t0, t2 - t0))
     dm.close()
     shard.table.close()
     dist.destroy_process_group()

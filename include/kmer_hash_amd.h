@@ -80,6 +80,9 @@ int kh_device_count(int* n);
 int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int device);
 int kh_destroy(kh_table* t);
 int kh_clear(kh_table* t);                       /* empty table + start list (async) */
+/* Grow an empty table (after create or clear) to hold n_kmers at the creation load factor; a
+ * no-op when it already does. The sharded path sizes each shard from the routed counts. */
+int kh_reserve(kh_table* t, uint64_t n_kmers);
 int kh_set_stream(kh_table* t, void* hip_stream); /* NULL = back to the table's own stream */
 int kh_sync(kh_table* t);                        /* wait for the stream; report device errors */
 uint64_t kh_capacity(const kh_table* t);
@@ -108,7 +111,7 @@ int kh_contigs_offsets(kh_table* t, uint64_t* host_offsets, uint64_t n); /* line
 
 /* ---- sharded multi-GPU path --------------------------------------------------------------------
  * One table per rank (GPU). The key space is split by an owner hash; the caller moves the buffers
- * between ranks (RCCL all-to-all over xGMI; cs267_hw3_amd/dist.py). Replaces the per-owner batched
+ * between ranks (RCCL all-to-all over xGMI; cs267_hw3_amd/csrc/kh_dist.cpp, cs267_hw3_amd/dist.py). Replaces the per-owner batched
  * insert RPCs (hash_map.hpp:38-46,64-77) and the per-step remote find RPCs (hash_map.hpp:94-100).
  * Routed records and query keys are kh_word_count(k) 64-bit words each. counts_out receives
  * nranks + 1 uint64 on the device: per-destination counts, then their total. All async. */
@@ -134,37 +137,7 @@ int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);
  * has been issued on the table's stream. */
 int kh_insert_words_stage_dev(kh_table* t, const void* dev_words, uint64_t m, uint64_t total_hint);
 int kh_insert_words_finish(kh_table* t);
-/* Round walk: begin (sync; sizes buffers; total_kmers = k-mers over all ranks, bounds contig
- * length), then per round emit -> exchange keys -> find_ext (owner) -> exchange replies -> apply,
- * until no rank emits; end materialises this rank's contig text (kh_contigs_text*). */
-int kh_walk_begin(kh_table* t, uint64_t total_kmers, uint64_t* n_walkers);
-int kh_walk_emit_dev(kh_table* t, int nranks, void* dev_keys_out, void* dev_counts_out);
-int kh_find_ext_dev(kh_table* t, const void* dev_keys, uint64_t m, void* dev_ext_out);
-int kh_walk_apply_dev(kh_table* t, const void* dev_ext, uint64_t m);
-int kh_walk_end_dev(kh_table* t);
-/* Fixed-capacity rounds (what cs267_hw3_amd/dist.py runs): every round exchanges one segment
- * per peer of L = KH_SEG_SUBS + cap*W int64 words and one of cap reply bytes, so no rank waits on
- * the host for counts. Segment = [count of sub-segment 0..KH_SEG_SUBS-1, then the keys of each
- * sub-segment, cap/KH_SEG_SUBS slots each]; replies use the same slot order (0xFF = absent). A
- * walker that does not fit its sub-segment retries next round. One step applies the replies of
- * the previous round (NULL before the first step) and emits the next queries:
- *   step(reply_prev, send) -> all-to-all(send -> recv, L words per peer)
- *   -> find_ext_fixed(recv -> reply) (owner) -> all-to-all(reply -> reply_prev, cap bytes per peer)
- * Stop when the global sum of kh_walk_active_dev is 0. cap: a multiple of KH_SEG_SUBS, the same
- * on every rank within a round (it may shrink between rounds); nranks * cap < 2^32. */
-#define KH_SEG_SUBS 8
-int kh_walk_step_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* dev_reply_prev,
-                           void* dev_send);
-int kh_find_ext_fixed_dev(kh_table* t, int nranks, uint64_t cap, const void* dev_recv,
-                          void* dev_reply);
-/* walkers unfinished after the last step (all walkers before the first) -> device word */
-int kh_walk_active_dev(kh_table* t, void* dev_u64_out);
-/* Hash of every device pointer / size the fixed-round launches bake in (for hosts that capture
- * rounds into a hipGraph after the first step: a graph is reusable while the signature, the
- * caller's buffers and cap are unchanged). */
-int kh_walk_signature(kh_table* t, uint64_t* sig);
-
-/* Migrating-walker rounds (what cs267_hw3_amd/dist.py runs by default). The table is sharded by
+/* Migrating-walker rounds. The table is sharded by
  * a hash of each k-mer's minimizer, so consecutive k-mers of a contig mostly share an owner; a
  * walker walks the local shard until its next k-mer is owned elsewhere and is then sent there:
  *   begin -> loop { round(in, n_in -> out grouped by destination, counts[P+1])

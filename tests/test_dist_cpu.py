@@ -21,8 +21,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="migrate", cap=None,
-               insert_chunks=None):
+def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, insert_chunks=None, max_kmers=None):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -35,17 +34,20 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="migr
                             world_size=world)
     k = MANIFEST[name]["k"]
     recs = kh.read_kmers(os.path.join(GOLDEN, f"{name}.txt"), k, world, rank)
-    ctrl = dist.new_group(backend="gloo") if insert_chunks else None
-    dm = DistributedKmerHashMap(TorchComm(ctrl=ctrl), FakeShard(k), protocol=protocol)
+    shard = FakeShard(k) if max_kmers is None else FakeShard(k, max_kmers=max_kmers if rank == 0 else 1 << 24)
+    dm = DistributedKmerHashMap(TorchComm(), shard)
     if insert_chunks:                      # pipelined insert: chunked route/exchange + staged build
         dm.INSERT_CHUNKS = insert_chunks
         dm.PIPELINE_MIN = 0
-    if cap:
-        dm.CAP_LIMIT = cap                 # force segment overflow -> retry rounds
-        dm.CHECK_EVERY = 3
     if chunk_bytes:
         dm.A2A_CHUNK_BYTES = chunk_bytes   # force the chunked all-to-all path
-    dm.insert_all(torch.from_numpy(recs))
+    try:
+        dm.insert_all(torch.from_numpy(recs))
+    except Exception as ex:                # every rank must fail together (no rank left waiting)
+        with open(os.path.join(outdir, f"err_{rank}"), "w") as f:
+            f.write(str(ex))
+        dist.destroy_process_group()
+        return
     rounds = dm.assemble(MANIFEST[name]["n"])
     with open(os.path.join(outdir, f"test_{rank}.dat"), "wb") as f:
         f.write(dm.contigs_text())
@@ -55,17 +57,11 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, protocol="migr
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world,chunk,protocol,cap", [
-    ("mixed19", 2, None, "migrate", None), ("small51", 2, None, "migrate", None),
-    ("singles51", 2, None, "migrate", None), ("small51", 3, None, "migrate", None),
-    ("small51", 3, 64, "migrate", None), ("mixed19", 3, 1000, "migrate", None),
-    ("mixed19", 2, None, "fixed", None), ("small51", 2, None, "fixed", None),
-    ("singles51", 2, None, "fixed", None), ("small51", 3, None, "fixed", None),
-    ("small51", 3, 64, "fixed", None), ("small51", 3, None, "fixed", 2),
-    ("mixed19", 2, None, "fixed", 5), ("mixed19", 2, 1000, "variable", None),
-    ("small51", 3, 64, "variable", None), ("singles51", 2, None, "variable", None)])
-def test_sharded_driver_gloo(tmp_path, name, world, chunk, protocol, cap):
-    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), chunk, protocol, cap),
+@pytest.mark.parametrize("name,world,chunk", [
+    ("mixed19", 2, None), ("small51", 2, None), ("singles51", 2, None), ("small51", 3, None),
+    ("small51", 3, 64), ("mixed19", 3, 1000), ("small51", 4, None)])
+def test_sharded_driver_gloo(tmp_path, name, world, chunk):
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), chunk),
                        nprocs=world, join=True, start_method="spawn")
     import cs267_hw3_amd as kh
     m = MANIFEST[name]
@@ -85,10 +81,10 @@ def test_sharded_driver_gloo(tmp_path, name, world, chunk, protocol, cap):
 
 @pytest.mark.parametrize("name,world,chunks", [("small51", 2, 3), ("mixed19", 3, 4), ("singles51", 2, 2)])
 def test_sharded_pipelined_insert_gloo(tmp_path, name, world, chunks):
-    """Pipelined insert over gloo: chunk counts over the ctrl group, async all-to-alls, each
-    received chunk staged while the next is in flight, one build at the end."""
-    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), None, "migrate", None,
-                                         chunks), nprocs=world, join=True, start_method="spawn")
+    """Pipelined insert over gloo: every chunk routed, the count matrix exchanged once, async
+    all-to-alls, each received chunk staged while the next is in flight, one build at the end."""
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), None, chunks),
+                       nprocs=world, join=True, start_method="spawn")
     import cs267_hw3_amd as kh
     m = MANIFEST[name]
     g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"],
@@ -96,3 +92,14 @@ def test_sharded_pipelined_insert_gloo(tmp_path, name, world, chunks):
     for r in range(world):
         b, e = g.block(world, r)
         assert open(tmp_path / f"test_{r}.dat", "rb").read() == g.truth(b, e)
+
+
+def test_sharded_shard_full_fails_on_every_rank(tmp_path):
+    """A shard that cannot hold what it is routed (rank 0 here) makes EVERY rank raise after the
+    count exchange, instead of leaving the others blocked in the next collective."""
+    world = 2
+    mp.start_processes(_rank_main, args=(world, _free_port(), "small51", str(tmp_path), None, None, 3),
+                       nprocs=world, join=True, start_method="spawn")
+    errs = [open(tmp_path / f"err_{r}").read() for r in range(world)]
+    assert "cannot hold" in errs[0]
+    assert "another rank" in errs[1]

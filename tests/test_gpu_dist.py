@@ -1,5 +1,5 @@
-"""GPU: the sharded path's kernels (route / insert words / round walker emit-find-apply) with P
-logical ranks on one GPU (ThreadComm). Each rank's text == ground truth of its block; the union
+"""GPU: the sharded path's kernels (route / insert words / migrating walker rounds / splitter
+segments) with P logical ranks on one GPU (ThreadComm). Each rank's text == ground truth of its block; the union
 == the reference-harness output / the oracle."""
 import json
 import os
@@ -21,16 +21,13 @@ def check_ranks(g, texts, P):
         assert got == g.truth(b, e), f"rank {r}"
 
 
-@pytest.mark.parametrize("protocol,cap", [("migrate", None), ("fixed", None), ("fixed", 3),
-                                          ("variable", None)])
 @pytest.mark.parametrize("name", ["mixed19", "small51", "singles51", "k30", "k60", "tiny19"])
-@pytest.mark.parametrize("P", [1, 2, 3, 4])
-def test_sharded_golden(name, P, protocol, cap):
-    """cap=3 forces per-peer segment overflow: walkers that do not fit retry next round."""
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+def test_sharded_golden(name, P):
     from cs267_hw3_amd.dist import run_threaded
     m = MANIFEST[name]
     recs = kh.pack_text(m["k"], open(os.path.join(GOLDEN, f"{name}.txt"), "rb").read())
-    texts = run_threaded(m["k"], recs, P, protocol=protocol, cap_limit=cap)
+    texts = run_threaded(m["k"], recs, P)
     g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"],
                           seed=m["seed"])
     check_ranks(g, texts, P)
@@ -38,24 +35,22 @@ def test_sharded_golden(name, P, protocol, cap):
     assert sorted(b"".join(texts).splitlines()) == sorted(want.splitlines())
 
 
-@pytest.mark.parametrize("protocol", ["migrate", "fixed", "variable"])
 @pytest.mark.parametrize("k,n,P", [(51, 2_000_000, 8), (19, 1_000_000, 4)])
-def test_sharded_generated(k, n, P, protocol):
+def test_sharded_generated(k, n, P):
     from cs267_hw3_amd.dist import run_threaded
     g = kh.SyntheticKmers(k, n, 8, 400, 10, seed=k + P)
-    texts = run_threaded(k, g.records(), P, protocol=protocol)
+    texts = run_threaded(k, g.records(), P)
     check_ranks(g, texts, P)
 
 
-@pytest.mark.parametrize("protocol", ["migrate", "fixed", "variable"])
-def test_sharded_missing_kmer_raises(protocol):
+def test_sharded_missing_kmer_raises():
     from cs267_hw3_amd.dist import run_threaded
     m = MANIFEST["tiny19"]
     recs = kh.pack_text(19, open(os.path.join(GOLDEN, "tiny19.txt"), "rb").read())
     P = (19 + 3) // 4
     interior = np.where((recs[:, P] != ord("F")) & (recs[:, P + 1] != ord("F")))[0][5]
     with pytest.raises(kh.KmerHashError):
-        run_threaded(19, np.delete(recs, interior, axis=0), 2, protocol=protocol)
+        run_threaded(19, np.delete(recs, interior, axis=0), 2)
 
 
 @pytest.mark.parametrize("mode", ["cas", "part"])
@@ -94,18 +89,17 @@ def test_sharded_long_contigs_migrate():
         check_ranks(g, run_threaded(19, g.records(), P), P)
 
 
-@pytest.mark.parametrize("protocol", ["migrate", "fixed", "variable"])
-def test_sharded_hash_owner(monkeypatch, protocol):
+def test_sharded_hash_owner(monkeypatch):
     """SURVEY §8(e)'s owner (hash bits) instead of the minimizer owner: same outputs."""
     from cs267_hw3_amd.dist import run_threaded
     monkeypatch.setenv("KH_OWNER", "hash")
     g = kh.SyntheticKmers(51, 500_000, 8, 200, 10, seed=123)
-    check_ranks(g, run_threaded(51, g.records(), 4, protocol=protocol), 4)
+    check_ranks(g, run_threaded(51, g.records(), 4), 4)
 
 
 @pytest.mark.parametrize("chunks", [2, 5])
 def test_sharded_pipelined_insert(chunks):
-    """Chunked route + exchange of the insert (counts over the ctrl group), P=4 logical ranks."""
+    """Chunked route + one count exchange + chunked transfers of the insert, P=4 logical ranks."""
     from cs267_hw3_amd.dist import run_threaded
     g = kh.SyntheticKmers(51, 6_000_000, 8, 200, 10, seed=321)
     check_ranks(g, run_threaded(51, g.records(), 4, insert_chunks=chunks), 4)
