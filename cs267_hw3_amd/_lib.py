@@ -56,6 +56,7 @@ _SIGS = {
     "kh_destroy": (ctypes.c_int, [c_vp]),
     "kh_clear": (ctypes.c_int, [c_vp]),
     "kh_reserve": (ctypes.c_int, [c_vp, c_u64]),
+    "kh_key_owner": (ctypes.c_int, [c_vp, c_u8p, ctypes.c_int]),
     "kh_set_stream": (ctypes.c_int, [c_vp, c_vp]),
     "kh_sync": (ctypes.c_int, [c_vp]),
     "kh_capacity": (c_u64, [c_vp]),

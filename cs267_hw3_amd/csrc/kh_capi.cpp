@@ -744,6 +744,12 @@ int kh_memcpy_dtoh(void* dst, const void* src, uint64_t bytes) {
 }
 
 // ---- sharded multi-GPU path -------------------------------------------------------------------
+int kh_key_owner(const kh_table* t, const uint8_t* packed_key, int nranks) {
+    if (!t || !packed_key) return fail(KH_ERR_ARG, "null argument");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
+    return (int)kh::owner_key(kh::key_from_packed(packed_key, t->kp), t->kp, (uint32_t)nranks);
+}
+
 int kh_word_count(int k) { return (k >= 1 && k <= KH_K_MAX) ? kh::make_params(k).W : KH_ERR_ARG; }
 
 namespace {

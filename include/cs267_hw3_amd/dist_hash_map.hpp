@@ -1,0 +1,457 @@
+// dist_hash_map.hpp — the sharded table behind DistributedHashMap(size, rank, world) for world > 1
+// (hash_map.hpp:12-114 + kmer_hash.cpp:21-55 of the reference), C++ host over the C ABI.
+//
+// One rank per GPU (or P logical ranks on one GPU for tests), SPMD: every rank calls the same
+// collective methods in the same order. The reference's transport (UPC++ RPCs: one batched insert
+// RPC per owner, hash_map.hpp:38-46,64-77; one blocking find RPC per remote walk step,
+// hash_map.hpp:94-100) becomes bulk exchanges through a kh::Comm (comm.hpp / rccl_comm.hpp):
+//
+//   insert_all  route every record to its owner on the GPU (kh_route_starts_dev; the block's start
+//               k-mers are collected in the same pass, kmer_hash.cpp:27-31) -> one count all-gather
+//               -> each shard sized from what it receives (kh_reserve) -> all-to-all of the routed
+//               words in chunks, each received chunk partitioned while the next is on the wire
+//               (kh_insert_words_stage_dev), one region build at the end (kh_insert_words_finish)
+//   assemble    migrating walkers (kh_mwalk_*): a walker walks the local shard until its next
+//               k-mer is owned elsewhere, then moves there in the round's all-to-all; the bases
+//               go home in one more all-to-all; splitter segments (long chains) are stitched by
+//               distributed pointer jumping. Each rank ends with its test_<rank>.dat bytes.
+//   find        the owner's table answers (in-process peers; the RPC of hash_map.hpp:94-100)
+//
+// The same protocol has a Python host in cs267_hw3_amd/dist.py (torch.distributed).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../kmer_hash_amd.h"
+#include "comm.hpp"
+
+namespace kh {
+
+inline void abi_check(int rc) {
+    if (rc != KH_OK) throw std::runtime_error(kh_last_error());
+}
+
+// Grow-only device buffer (25 % headroom when it grows).
+class DevBuf {
+public:
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void* ensure(size_t bytes) {
+        if (bytes <= cap_ && p_) return p_;
+        release();
+        const size_t want = bytes + bytes / 4 + 256;
+        hip_check(hipMalloc(&p_, want), "hipMalloc");
+        cap_ = want;
+        return p_;
+    }
+    int64_t* words(size_t n) { return static_cast<int64_t*>(ensure(n * 8)); }
+    void* get() const { return p_; }
+    void release() {
+        if (p_) (void)hipFree(p_);
+        p_ = nullptr;
+        cap_ = 0;
+    }
+
+private:
+    void* p_ = nullptr;
+    size_t cap_ = 0;
+};
+
+class ShardedTable;
+
+// The ranks this process drives (one thread each), set by the launcher before the threads start,
+// like upcxx::init(): DistributedHashMap(size, rank, world) looks its rank up here.
+struct RankContext {
+    Comm* comm = nullptr;
+    int device = 0;
+    const void* peer_group = nullptr;  // in-process peers (owner-side finds); null: none
+};
+inline std::vector<RankContext>& rank_contexts() {
+    static std::vector<RankContext> v;
+    return v;
+}
+
+// In-process peers of a communicator group (threads of one process), for owner-side finds.
+class PeerRegistry {
+public:
+    static PeerRegistry& get() {
+        static PeerRegistry r;
+        return r;
+    }
+    void add(const void* group, int world, int rank, ShardedTable* t) {
+        std::lock_guard<std::mutex> g(m_);
+        auto& v = peers_[group];
+        if ((int)v.size() < world) v.resize(world, nullptr);
+        v[rank] = t;
+    }
+    void remove(const void* group, int rank) {
+        std::lock_guard<std::mutex> g(m_);
+        auto it = peers_.find(group);
+        if (it == peers_.end()) return;
+        it->second[rank] = nullptr;
+        if (std::all_of(it->second.begin(), it->second.end(), [](ShardedTable* x) { return !x; })) peers_.erase(it);
+    }
+    ShardedTable* peer(const void* group, int rank) {
+        std::lock_guard<std::mutex> g(m_);
+        auto it = peers_.find(group);
+        return it == peers_.end() || rank >= (int)it->second.size() ? nullptr : it->second[rank];
+    }
+
+private:
+    std::mutex m_;
+    std::map<const void*, std::vector<ShardedTable*>> peers_;
+};
+
+class ShardedTable {
+public:
+    // n_kmers_hint: k-mers this shard is expected to hold (it grows to what it is routed)
+    ShardedTable(int k, uint64_t n_kmers_hint, Comm& comm, int device, const void* peer_group = nullptr)
+        : k_(k), comm_(comm), P_(comm.size()), rank_(comm.rank()), device_(device), group_(peer_group) {
+        hip_check(hipSetDevice(device), "hipSetDevice");
+        abi_check(kh_create(&t_, k, n_kmers_hint ? n_kmers_hint : 1, 0.5, device));
+        hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+        hip_check(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking), "hipStreamCreate");
+        abi_check(kh_set_stream(t_, stream_));
+        W_ = kh_word_count(k);
+        R_ = kh_record_size(k);
+        counts_.words(P_ + 1);
+        if (group_) PeerRegistry::get().add(group_, P_, rank_, this);
+    }
+    ~ShardedTable() {
+        if (group_) PeerRegistry::get().remove(group_, rank_);
+        (void)hipSetDevice(device_);
+        if (t_) kh_destroy(t_);
+        for (auto* b : {&words_, &recv_, &counts_, &a_, &b_, &tout_, &trecv_, &lout_, &lin_, &qout_, &qin_, &rep_,
+                        &rin_, &sout_, &sin_, &recs_})
+            b->release();
+        for (auto e : events_) (void)hipEventDestroy(e);
+        if (stream_) (void)hipStreamDestroy(stream_);
+        if (xstream_) (void)hipStreamDestroy(xstream_);
+    }
+    ShardedTable(const ShardedTable&) = delete;
+    ShardedTable& operator=(const ShardedTable&) = delete;
+
+    kh_table* handle() { return t_; }
+    hipStream_t stream() { return stream_; }
+    int rank() const { return rank_; }
+    int world() const { return P_; }
+    int rounds() const { return rounds_; }
+    int jump_rounds() const { return jump_rounds_; }
+    std::mutex& mutex() { return m_; }
+
+    void clear() {
+        hip_check(hipSetDevice(device_), "hipSetDevice");
+        abi_check(kh_clear(t_));
+    }
+
+    // hash_map.hpp:55-80 insert_all (+ kmer_hash.cpp:27-31 start nodes) for this rank's block of
+    // records (host kmer_pair array, R bytes each). Collective. Returns the k-mers this shard got.
+    uint64_t insert_all(const void* host_recs, uint64_t n) {
+        hip_check(hipSetDevice(device_), "hipSetDevice");
+        void* d = recs_.ensure(n * R_ + 16);
+        if (n) hip_check(hipMemcpyAsync(d, host_recs, n * R_, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync");
+        return insert_all_dev(d, n);
+    }
+
+    // Same with the records already in device memory (16-B aligned). Collective.
+    uint64_t insert_all_dev(const void* dev_recs, uint64_t n) {
+        hip_check(hipSetDevice(device_), "hipSetDevice");
+        const uint64_t P = (uint64_t)P_;
+        uint64_t nch = 1;
+        if (P > 1 && n >= kPipelineMin) {
+            // per-peer bytes of a chunk <= chunk records * W * 8: every message stays under the
+            // transport's per-peer limit whatever the skew
+            const uint64_t lim = (512ull << 20);
+            nch = std::max<uint64_t>(kInsertChunks, (n * W_ * 8 + lim - 1) / lim);
+        }
+        std::vector<uint64_t> bounds(nch + 1);
+        for (uint64_t c = 0; c <= nch; ++c) bounds[c] = n * c / nch;
+        int64_t* words = words_.words(std::max<uint64_t>(n, 1) * W_);
+        int64_t* cnt = counts_.words(nch * (P + 1));
+        const uint8_t* recs = static_cast<const uint8_t*>(dev_recs);
+        for (uint64_t c = 0; c < nch; ++c)
+            abi_check(kh_route_starts_dev(t_, recs + bounds[c] * R_, bounds[c + 1] - bounds[c], P_,
+                                          words + bounds[c] * W_, cnt + c * (P + 1)));
+        // every rank learns the whole [src][chunk][dst] count matrix in one all-gather
+        std::vector<uint64_t> mine(nch * (P + 1)), all(P * nch * (P + 1));
+        hip_check(hipMemcpyAsync(mine.data(), cnt, mine.size() * 8, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync");
+        hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        abi_check(kh_sync(t_));
+        comm_.allgather(mine.data(), mine.size(), all.data(), stream_);
+        auto M = [&](uint64_t src, uint64_t c, uint64_t dst) { return all[(src * nch + c) * (P + 1) + dst]; };
+        uint64_t m = 0, gmax = 0;
+        for (uint64_t q = 0; q < P; ++q)
+            for (uint64_t c = 0; c < nch; ++c) {
+                m += M(q, c, rank_);
+                for (uint64_t d = 0; d < P; ++d) gmax = std::max(gmax, M(q, c, d));
+            }
+        // size the shard from what it receives; every rank fails together if any rank cannot
+        const int rc = kh_reserve(t_, m);
+        const std::string err = rc == KH_OK ? "" : kh_last_error();
+        agree(rc != KH_OK, err);
+        if (P == 1) {  // one rank: the routed words are this shard's
+            abi_check(kh_insert_words_dev(t_, words, m));
+            return m;
+        }
+        int64_t* recv = recv_.words(std::max<uint64_t>(m, 1) * W_);
+        std::vector<uint64_t> sc(P), sd(P), rcn(P), rd(P);
+        auto plan = [&](uint64_t c, uint64_t pos) {  // chunk c's counts/displacements, in words
+            uint64_t so = bounds[c] * W_, ro = pos * W_;
+            for (uint64_t q = 0; q < P; ++q) {
+                sc[q] = M(rank_, c, q) * W_;
+                sd[q] = so;
+                so += sc[q];
+                rcn[q] = M(q, c, rank_) * W_;
+                rd[q] = ro;
+                ro += rcn[q];
+            }
+        };
+        if (nch == 1) {
+            plan(0, 0);
+            comm_.alltoallv(words, sc.data(), sd.data(), recv, rcn.data(), rd.data(), gmax * W_, stream_);
+            abi_check(kh_insert_words_dev(t_, recv, m));
+            return m;
+        }
+        // chunk c moves on the exchange stream while chunk c-1, received, is partitioned on the
+        // table's stream; one build at the end
+        ensure_events(nch + 1);
+        hip_check(hipEventRecord(events_[nch], stream_), "hipEventRecord");  // routed words ready
+        hip_check(hipStreamWaitEvent(xstream_, events_[nch], 0), "hipStreamWaitEvent");
+        uint64_t pos = 0, prev_pos = 0, prev_m = 0;
+        for (uint64_t c = 0; c < nch; ++c) {
+            uint64_t mc = 0;
+            for (uint64_t q = 0; q < P; ++q) mc += M(q, c, rank_);
+            plan(c, pos);
+            comm_.alltoallv(words, sc.data(), sd.data(), recv, rcn.data(), rd.data(), gmax * W_, xstream_);
+            hip_check(hipEventRecord(events_[c], xstream_), "hipEventRecord");
+            if (c > 0) stage(recv, prev_pos, prev_m, m, events_[c - 1]);
+            prev_pos = pos;
+            prev_m = mc;
+            pos += mc;
+        }
+        stage(recv, prev_pos, prev_m, m, events_[nch - 1]);
+        abi_check(kh_insert_words_finish(t_));
+        return m;
+    }
+
+    // kmer_hash.cpp:38-55 assemble_contigs for this rank's start k-mers, every rank at once.
+    // total_kmers bounds contig length (cycle detection). Collective. Returns walk rounds.
+    int assemble(uint64_t total_kmers) {
+        hip_check(hipSetDevice(device_), "hipSetDevice");
+        constexpr uint64_t M = KH_MSG_WORDS, T = KH_TEXT_REC_WORDS;
+        uint64_t n_in = 0;
+        abi_check(kh_mwalk_begin(t_, P_, rank_, total_kmers, &n_in));
+        const uint64_t n_walkers = n_in;
+        const int64_t* in = nullptr;
+        DevBuf* out = &a_;
+        DevBuf* nxt = &b_;
+        rounds_ = 0;
+        Exchange ex;
+        for (;;) {
+            int64_t* o = out->words(std::max<uint64_t>(n_in, 1) * M);
+            abi_check(kh_mwalk_round_dev(t_, in, n_in, o, counts_.words(P_ + 1)));
+            exchange_counts(ex);  // syncs: the round has consumed `in`
+            ++rounds_;
+            if (ex.total_all == 0) break;
+            if (P_ == 1) {
+                in = o;  // nothing to move: the next round reads this round's output
+                std::swap(out, nxt);
+            } else {
+                int64_t* r = nxt->words(std::max<uint64_t>(ex.recv_total, 1) * M);
+                move(o, r, ex, M);
+                in = r;
+            }
+            n_in = ex.recv_total;
+        }
+        uint64_t nrec = 0;
+        abi_check(kh_mwalk_text_count(t_, &nrec));
+        int64_t* tout = tout_.words(std::max<uint64_t>(nrec, 1) * T);
+        abi_check(kh_mwalk_text_dev(t_, tout, counts_.words(P_ + 1)));
+        exchange_counts(ex);
+        const uint64_t r = ex.recv_total;
+        int64_t* trecv = tout;
+        if (P_ > 1) {
+            trecv = trecv_.words(std::max<uint64_t>(r, 1) * T);
+            move(tout, trecv, ex, T);
+        }
+        uint64_t nseg = 0;
+        abi_check(kh_mwalk_segments(t_, &nseg));
+        // every rank takes the same branch (a rank without splitters still links and answers)
+        if (global_max(nseg))
+            segments_end(trecv, r, n_walkers);
+        else
+            abi_check(kh_mwalk_end_dev(t_, trecv, r));
+        abi_check(kh_sync(t_));
+        return rounds_;
+    }
+
+    // This rank's contig text (= test_<rank>.dat bytes) of the last assemble.
+    std::string contigs_text() {
+        hip_check(hipSetDevice(device_), "hipSetDevice");
+        const char* d = nullptr;
+        uint64_t bytes = 0;
+        abi_check(kh_contigs_text_dev(t_, &d, &bytes));
+        std::string s(bytes, '\0');
+        if (bytes) hip_check(hipMemcpy(&s[0], d, bytes, hipMemcpyDeviceToHost), "hipMemcpy");
+        return s;
+    }
+
+    // Single-key find (hash_map.hpp:83-107): the owner's table answers. Keys this rank owns are
+    // looked up here; others go to the owning rank's table when it lives in this process (the
+    // ranks are threads); a one-process-per-GPU run has no RPC channel and throws.
+    bool find(const uint8_t* packed_key, uint8_t* rec_out) {
+        const int owner = kh_key_owner(t_, packed_key, P_);
+        if (owner < 0) abi_check(owner);
+        ShardedTable* o = owner == rank_ ? this : (group_ ? PeerRegistry::get().peer(group_, owner) : nullptr);
+        if (!o) throw std::runtime_error("DistributedHashMap::find: the owner rank is not in this process");
+        std::lock_guard<std::mutex> g(o->m_);
+        hip_check(hipSetDevice(o->device_), "hipSetDevice");
+        uint8_t found = 0;
+        abi_check(kh_find(o->t_, packed_key, 1, rec_out, &found));
+        return found != 0;
+    }
+
+    void barrier() { comm_.barrier(); }
+
+    static constexpr uint64_t kInsertChunks = 4;
+    static constexpr uint64_t kPipelineMin = 1ull << 22;  // records per rank below: one transfer
+
+private:
+    struct Exchange {
+        std::vector<uint64_t> send, recv;  // per peer, in items
+        uint64_t send_total = 0, recv_total = 0, total_all = 0, gmax = 0;
+    };
+
+    // counts_ holds [P+1] device words (per destination, total) -> every rank's view
+    void exchange_counts(Exchange& ex) {
+        const uint64_t P = (uint64_t)P_;
+        std::vector<uint64_t> mine(P + 1), all(P * (P + 1));
+        hip_check(hipMemcpyAsync(mine.data(), counts_.get(), (P + 1) * 8, hipMemcpyDeviceToHost, stream_),
+                  "hipMemcpyAsync");
+        hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        abi_check(kh_sync(t_));
+        comm_.allgather(mine.data(), P + 1, all.data(), stream_);
+        ex.send.assign(mine.begin(), mine.begin() + P);
+        ex.recv.resize(P);
+        ex.send_total = ex.recv_total = ex.total_all = ex.gmax = 0;
+        for (uint64_t q = 0; q < P; ++q) {
+            ex.recv[q] = all[q * (P + 1) + rank_];
+            ex.send_total += ex.send[q];
+            ex.recv_total += ex.recv[q];
+            ex.total_all += all[q * (P + 1) + P];
+            for (uint64_t d = 0; d < P; ++d) ex.gmax = std::max(ex.gmax, all[q * (P + 1) + d]);
+        }
+    }
+
+    // items of `width` words grouped by destination (ex.send) -> received (ex.recv); reverse:
+    // the replies of a query exchange go back the way the queries came
+    void move(const int64_t* send, int64_t* recv, const Exchange& ex, uint64_t width, bool reverse = false) {
+        const uint64_t P = (uint64_t)P_;
+        const std::vector<uint64_t>& s = reverse ? ex.recv : ex.send;
+        const std::vector<uint64_t>& r = reverse ? ex.send : ex.recv;
+        std::vector<uint64_t> sc(P), sd(P), rc(P), rd(P);
+        uint64_t so = 0, ro = 0;
+        for (uint64_t q = 0; q < P; ++q) {
+            sc[q] = s[q] * width;
+            sd[q] = so;
+            so += sc[q];
+            rc[q] = r[q] * width;
+            rd[q] = ro;
+            ro += rc[q];
+        }
+        comm_.alltoallv(send, sc.data(), sd.data(), recv, rc.data(), rd.data(), ex.gmax * width, stream_);
+    }
+
+    uint64_t global_max(uint64_t x) {
+        if (P_ == 1) return x;
+        std::vector<uint64_t> all(P_);
+        comm_.allgather(&x, 1, all.data(), stream_);
+        return *std::max_element(all.begin(), all.end());
+    }
+
+    void agree(bool failed, const std::string& err) {
+        if (global_max(failed ? 1 : 0) == 0) return;
+        throw std::runtime_error(failed ? err : "another rank failed to size its shard");
+    }
+
+    void stage(const int64_t* recv, uint64_t pos, uint64_t m, uint64_t total, hipEvent_t arrived) {
+        hip_check(hipStreamWaitEvent(stream_, arrived, 0), "hipStreamWaitEvent");
+        abi_check(kh_insert_words_stage_dev(t_, recv + pos * W_, m, total));
+    }
+
+    void ensure_events(size_t n) {
+        while (events_.size() < n) {
+            hipEvent_t e;
+            hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+            events_.push_back(e);
+        }
+    }
+
+    // Splitter segments: link each segment to its successor's owner, pointer-jump to the contig
+    // heads, send the segments' text to the contig origins, materialise.
+    void segments_end(const int64_t* trecv, uint64_t r, uint64_t nseg) {
+        constexpr uint64_t L = KH_LINK_WORDS, J = KH_JUMP_REPLY_WORDS, S = KH_SEG_REC_WORDS;
+        const bool local = P_ == 1;
+        Exchange ex;
+        int64_t* lout = lout_.words(std::max<uint64_t>(nseg, 1) * L);
+        abi_check(kh_mwalk_link_dev(t_, trecv, r, lout, counts_.words(P_ + 1)));
+        exchange_counts(ex);
+        int64_t* lin = lout;
+        if (!local) {
+            lin = lin_.words(std::max<uint64_t>(ex.recv_total, 1) * L);
+            move(lout, lin, ex, L);
+        }
+        abi_check(kh_mwalk_pred_dev(t_, lin, ex.recv_total));
+        jump_rounds_ = 0;
+        int64_t* qout = qout_.words(std::max<uint64_t>(nseg, 1));
+        for (;;) {
+            abi_check(kh_mwalk_jump_emit_dev(t_, qout, counts_.words(P_ + 1)));
+            exchange_counts(ex);
+            if (ex.total_all == 0) break;
+            ++jump_rounds_;
+            int64_t* qin = qout;
+            if (!local) {
+                qin = qin_.words(std::max<uint64_t>(ex.recv_total, 1));
+                move(qout, qin, ex, 1);
+            }
+            int64_t* rep = rep_.words(std::max<uint64_t>(ex.recv_total, 1) * J);
+            abi_check(kh_mwalk_jump_answer_dev(t_, qin, ex.recv_total, rep));
+            int64_t* rin = rep;
+            if (!local) {
+                rin = rin_.words(std::max<uint64_t>(ex.send_total, 1) * J);
+                move(rep, rin, ex, J, /*reverse=*/true);
+            }
+            abi_check(kh_mwalk_jump_apply_dev(t_, rin, ex.send_total, nullptr));
+        }
+        int64_t* tout = sout_.words(std::max<uint64_t>(r + nseg, 1) * S);
+        abi_check(kh_mwalk_retag_dev(t_, trecv, r, tout, counts_.words(P_ + 1)));
+        exchange_counts(ex);
+        int64_t* tin = tout;
+        if (!local) {
+            tin = sin_.words(std::max<uint64_t>(ex.recv_total, 1) * S);
+            move(tout, tin, ex, S);
+        }
+        abi_check(kh_mwalk_end_seg_dev(t_, trecv, r, tin, ex.recv_total));
+    }
+
+    int k_;
+    Comm& comm_;
+    int P_, rank_, device_;
+    const void* group_;
+    kh_table* t_ = nullptr;
+    hipStream_t stream_ = nullptr, xstream_ = nullptr;
+    uint64_t W_ = 2, R_ = 15;
+    int rounds_ = 0, jump_rounds_ = 0;
+    std::mutex m_;
+    std::vector<hipEvent_t> events_;
+    DevBuf words_, recv_, counts_, a_, b_, tout_, trecv_, lout_, lin_, qout_, qin_, rep_, rin_, sout_, sin_, recs_;
+};
+
+}  // namespace kh

@@ -8,14 +8,17 @@
 //   bool find(const pkmer_t&, kmer_pair&); size_t size() const           (README.md:95,99)
 //
 // GPU additions: assemble() walks every start k-mer collected by the inserts on the device and
-// returns the test_<rank>.dat bytes (kmer_hash.cpp:38-68 in one call).
+// returns the test_<rank>.dat bytes (kmer_hash.cpp:38-68 in one call). Compile with
+// -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include and link -lkmerhash_amd -lamdhip64.
 // Single-key insert() calls are buffered on the host and flushed as one batch before the next
 // find()/size()/assemble(), so starter-style loops stay correct without a device call per k-mer.
 #pragma once
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "dist_hash_map.hpp"
 #include "kmer_t.hpp"
 
 namespace kh_detail {
@@ -26,16 +29,21 @@ inline void check(int rc) {
 
 class HashMap {
 public:
-    // size = number of slots (the stock driver passes 2 * n_kmers, kmer_hash.cpp:109)
-    explicit HashMap(size_t size, int device = 0) : size_(size) {
-        kh_detail::check(kh_create(&t_, KMER_LEN, size / 2 ? size / 2 : 1, 0.5, device));
+    // Stock starter semantics (README.md:95): the table holds up to `size` k-mers and insert()
+    // returns false ("HashMap is full") beyond that. The GPU table behind it has 2 * size slots
+    // (load 0.5).
+    explicit HashMap(size_t size, int device = 0) : HashMap(size, size, device) {}
+    // Table allocated for n_kmers (<= size); a bulk insert_all into the empty table grows it
+    // (DistributedHashMap at world_size 1: size = 2 * k-mers, kmer_hash.cpp:108-109).
+    HashMap(size_t size, uint64_t n_kmers, int device) : size_(size), n_kmers_(n_kmers ? n_kmers : 1) {
+        kh_detail::check(kh_create(&t_, KMER_LEN, n_kmers_, 0.5, device));
     }
     ~HashMap() { kh_destroy(t_); }
     HashMap(const HashMap&) = delete;
     HashMap& operator=(const HashMap&) = delete;
 
     bool insert(const kmer_pair& kmer) {
-        if (inserted_ + pending_.size() >= size_ / 2) return false;  // "HashMap is full!"
+        if (inserted_ + pending_.size() >= size_) return false;  // "HashMap is full!"
         pending_.push_back(kmer);
         return true;
     }
@@ -49,6 +57,7 @@ public:
 
     void insert_all(const std::vector<kmer_pair>& items) {
         flush();
+        if (inserted_ == 0) grow(items.size());
         kh_detail::check(kh_insert(t_, reinterpret_cast<const uint8_t*>(items.data()), items.size()));
         inserted_ += items.size();
     }
@@ -64,35 +73,83 @@ public:
     kh_table* handle() { return t_; }
 
 private:
+    void grow(uint64_t n) {
+        if (n <= n_kmers_) return;
+        kh_detail::check(kh_reserve(t_, n));
+        n_kmers_ = n;
+    }
     void flush() {
         if (pending_.empty()) return;
+        if (inserted_ == 0) grow(pending_.size());
         kh_detail::check(kh_insert(t_, reinterpret_cast<const uint8_t*>(pending_.data()), pending_.size()));
         inserted_ += pending_.size();
         pending_.clear();
     }
     kh_table* t_ = nullptr;
     size_t size_ = 0, inserted_ = 0;
+    uint64_t n_kmers_ = 1;
     std::vector<kmer_pair> pending_;
 };
 
+// DistributedHashMap (hash_map.hpp:12-114). world_size == 1: one GPU table (HashMap above).
+// world_size > 1: one shard per rank (kh::ShardedTable, dist_hash_map.hpp) over the rank's
+// kh::Comm, found in kh::rank_contexts() — the launcher fills it before starting one thread per
+// rank, as upcxx::init() would (tools/kmer_hash.cpp) — or passed explicitly.
 class DistributedHashMap {
 public:
-    // One GPU per rank. In this header world_size must be 1 (one process, one GPU); the sharded
-    // multi-GPU table lives in cs267_hw3_amd.dist (torch.distributed over RCCL).
-    DistributedHashMap(size_t table_size, int rank_id, int world_size, int device = 0)
-        : map_(table_size ? table_size : 2, device), rank_(rank_id), world_(world_size) {
-        if (world_size != 1)
-            throw std::runtime_error("DistributedHashMap (C++ header): world_size must be 1; use "
-                                     "cs267_hw3_amd.dist for the multi-GPU sharded table");
+    DistributedHashMap(size_t table_size, int rank_id, int world_size, int device = -1)
+        : size_(table_size ? table_size : 2), rank_(rank_id), world_(world_size) {
+        if (world_size == 1) {
+            map_.reset(new HashMap(size_, size_ / 2, device < 0 ? 0 : device));
+            return;
+        }
+        auto& ctx = kh::rank_contexts();
+        if ((int)ctx.size() != world_size || rank_id < 0 || rank_id >= world_size || !ctx[rank_id].comm)
+            throw std::runtime_error("DistributedHashMap: world_size > 1 needs kh::rank_contexts() set up by "
+                                     "the launcher (one kh::Comm per rank)");
+        make_shard(*ctx[rank_id].comm, device < 0 ? ctx[rank_id].device : device, ctx[rank_id].peer_group);
     }
-    void insert_all(const std::vector<kmer_pair>& items) { map_.insert_all(items); }
-    bool find(const std::string& key, kmer_pair& result) { return map_.find(pkmer_t(key), result); }
-    bool find(const pkmer_t& key, kmer_pair& result) { return map_.find(key, result); }
-    void process_requests() {}
-    std::string assemble() { return map_.assemble(); }
-    kh_table* handle() { return map_.handle(); }
+    DistributedHashMap(size_t table_size, kh::Comm& comm, int device, const void* peer_group = nullptr)
+        : size_(table_size ? table_size : 2), rank_(comm.rank()), world_(comm.size()) {
+        make_shard(comm, device, peer_group);
+    }
+
+    // hash_map.hpp:55-80 (collective at world_size > 1; ends like the reference's barrier)
+    void insert_all(const std::vector<kmer_pair>& items) {
+        if (map_) return map_->insert_all(items);
+        shard_->insert_all(items.data(), items.size());
+    }
+    // hash_map.hpp:83-107: the owner's table answers (one device round trip per call)
+    bool find(const pkmer_t& key, kmer_pair& result) {
+        if (map_) return map_->find(key, result);
+        return shard_->find(key.data, reinterpret_cast<uint8_t*>(&result));
+    }
+    bool find(const std::string& key, kmer_pair& result) { return find(pkmer_t(key), result); }
+    void process_requests() {}  // hash_map.hpp:110-113: nothing is left pending between calls
+
+    // kmer_hash.cpp:38-68 in one call: walk every start k-mer collected by insert_all on the
+    // device and return this rank's test_<rank>.dat bytes (collective at world_size > 1).
+    std::string assemble() {
+        if (map_) return map_->assemble();
+        shard_->assemble(size_ / 2);  // the reference sizes the table at 2 x the k-mer count
+        return shard_->contigs_text();
+    }
+    void barrier() {
+        if (shard_) shard_->barrier();
+    }
+    kh_table* handle() { return map_ ? map_->handle() : shard_->handle(); }
+    kh::ShardedTable* shard() { return shard_.get(); }
+    int rank() const { return rank_; }
+    int world() const { return world_; }
 
 private:
-    HashMap map_;
+    void make_shard(kh::Comm& comm, int device, const void* peer_group) {
+        // expected share of the k-mers (size_ / 2 in all); the shard grows to what it receives
+        const uint64_t hint = size_ / 2 / (uint64_t)world_ + 1024;
+        shard_.reset(new kh::ShardedTable(KMER_LEN, hint, comm, device, peer_group));
+    }
+    size_t size_;
     int rank_, world_;
+    std::unique_ptr<HashMap> map_;
+    std::unique_ptr<kh::ShardedTable> shard_;
 };

@@ -116,6 +116,9 @@ int kh_contigs_offsets(kh_table* t, uint64_t* host_offsets, uint64_t n); /* line
  * Routed records and query keys are kh_word_count(k) 64-bit words each. counts_out receives
  * nranks + 1 uint64 on the device: per-destination counts, then their total. All async. */
 int kh_word_count(int k);
+/* Rank (0..nranks-1) owning a pkmer_t key under the table's sharding (the route and the walk use
+ * the same function); < 0 on a bad argument. Replaces hash_map.hpp:28-30 get_target_rank. */
+int kh_key_owner(const kh_table* t, const uint8_t* packed_key, int nranks);
 int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n); /* local start k-mers */
 /* read_kmers.hpp:62-76 on the GPU: len bytes of fixed-width "KMER BF\n" lines (k+4 bytes each)
  * in device memory -> *n_out = len / (k+4) kmer_pair records at dev_recs (16-byte aligned; NULL:

@@ -1,0 +1,172 @@
+// C++ tests of the drop-in headers (include/cs267_hw3_amd/*.hpp), driven by tests/test_cpp_api.py.
+//   test_hash_map_<K> stock   <kmer_file>                 HashMap(size): insert/find/size/full
+//   test_hash_map_<K> refloop <kmer_file> <P> <prefix>    the reference's own initialize_kmers +
+//        assemble_contigs + output_results (kmer_hash.cpp:21-68) over DistributedHashMap, P ranks
+//        as threads on GPU 0 (kh::ThreadComm; P = 1: the single-GPU table), one find() per step
+//   test_hash_map_<K> rccl1   <kmer_file> <prefix>        DistributedHashMap over a one-rank RCCL
+//        communicator (sharded code path, RCCL all-gathers) -> <prefix>_0.dat
+// Exit status 0 = pass; a failed check prints it and exits 1.
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <list>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cs267_hw3_amd/hash_map.hpp"
+#include "cs267_hw3_amd/rccl_comm.hpp"
+#include "cs267_hw3_amd/read_kmers.hpp"
+
+#define CHECK(c)                                                                 \
+    do {                                                                         \
+        if (!(c)) {                                                              \
+            fprintf(stderr, "CHECK failed: %s (%s:%d)\n", #c, __FILE__, __LINE__); \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+namespace {
+
+// README.md:95,99 stock surface: every k-mer inserted one by one, found again; absent keys are
+// not found; size() is the constructor's; a full table refuses inserts.
+int stock(const std::string& fname) {
+    std::vector<kmer_pair> kmers = read_kmers(fname);
+    const size_t n = kmers.size();
+    HashMap hm(n * 2);
+    CHECK(hm.size() == n * 2);
+    for (const auto& k : kmers) CHECK(hm.insert(k));
+    for (const auto& k : kmers) {
+        kmer_pair got;
+        CHECK(hm.find(k.kmer, got));
+        CHECK(got == k);
+    }
+    // absent keys: the next k-mer of each contig end ('F' forward) is not in the set
+    int absent = 0;
+    for (const auto& k : kmers)
+        if (k.forwardExt() == 'F') {
+            kmer_pair got;
+            std::string s = k.kmer_str().substr(1) + "A";
+            bool present = false;
+            for (const auto& o : kmers) present |= o.kmer_str() == s;
+            if (!present) {
+                CHECK(!hm.find(pkmer_t(s), got));
+                ++absent;
+            }
+            if (absent > 20) break;
+        }
+    CHECK(absent > 0);
+    // "HashMap is full": a table of n slots takes exactly n k-mers
+    HashMap small(n / 2);
+    size_t ok = 0;
+    for (const auto& k : kmers) ok += small.insert(k);
+    CHECK(ok == n / 2);
+    for (size_t i = 0; i < n / 2; ++i) {
+        kmer_pair got;
+        CHECK(small.find(kmers[i].kmer, got) && got == kmers[i]);
+    }
+    kmer_pair got;
+    CHECK(!small.find(kmers[n - 1].kmer, got));
+    // assemble() on the stock table == one line per start k-mer
+    std::string text = hm.assemble();
+    size_t starts = 0, lines = 0;
+    for (const auto& k : kmers) starts += k.backwardExt() == 'F';
+    for (char c : text) lines += c == '\n';
+    CHECK(lines == starts);
+    printf("stock ok: %zu k-mers, %d absent probes, %zu contigs\n", n, absent, lines);
+    return 0;
+}
+
+// kmer_hash.cpp:21-68, verbatim in structure (find per step), for one rank
+void ref_rank(const std::string& fname, int rank, int world, const std::string& prefix, size_t n_kmers) {
+    DistributedHashMap hashmap(n_kmers * 2, rank, world, 0);
+    std::vector<kmer_pair> kmers = read_kmers(fname, world, rank);
+    hashmap.barrier();
+    // initialize_kmers
+    std::vector<kmer_pair> start_nodes;
+    hashmap.insert_all(kmers);
+    for (const auto& kmer : kmers)
+        if (kmer.backwardExt() == 'F') start_nodes.push_back(kmer);
+    hashmap.barrier();
+    // assemble_contigs
+    std::list<std::list<kmer_pair>> contigs;
+    for (const auto& start_kmer : start_nodes) {
+        std::list<kmer_pair> contig;
+        contig.push_back(start_kmer);
+        while (contig.back().forwardExt() != 'F') {
+            kmer_pair found;
+            bool success = hashmap.find(contig.back().next_kmer().get(), found);
+            if (!success) throw std::runtime_error("Error: k-mer not found in Distributed HashMap.");
+            contig.push_back(found);
+        }
+        contigs.push_back(contig);
+    }
+    hashmap.barrier();  // every rank's finds are answered before any table goes away
+    // output_results
+    std::ofstream fout(prefix + "_" + std::to_string(rank) + ".dat");
+    for (const auto& contig : contigs) fout << extract_contig(contig) << std::endl;
+}
+
+int refloop(const std::string& fname, int world, const std::string& prefix) {
+    const size_t n = line_count(fname);
+    if (world == 1) {
+        ref_rank(fname, 0, 1, prefix, n);
+        return 0;
+    }
+    kh::ThreadComm::Group group(world);
+    auto& ctx = kh::rank_contexts();
+    ctx.assign(world, kh::RankContext{});
+    for (int r = 0; r < world; ++r) ctx[r] = kh::RankContext{group.comm(r), 0, &group};
+    std::vector<std::thread> th;
+    int failed = 0;
+    for (int r = 0; r < world; ++r)
+        th.emplace_back([&, r] {
+            try {
+                ref_rank(fname, r, world, prefix, n);
+            } catch (const std::exception& ex) {
+                fprintf(stderr, "rank %d: %s\n", r, ex.what());
+                failed = 1;
+                group.abort();
+            }
+        });
+    for (auto& t : th) t.join();
+    return failed;
+}
+
+int rccl1(const std::string& fname, const std::string& prefix) {
+    auto comms = kh::RcclComm::init_all({0});
+    const size_t n = line_count(fname);
+    DistributedHashMap hashmap(n * 2, *comms[0], 0, comms.data());
+    CHECK(hashmap.shard() != nullptr);
+    hashmap.insert_all(read_kmers(fname));
+    std::string text = hashmap.assemble();
+    std::ofstream(prefix + "_0.dat", std::ios::binary).write(text.data(), (std::streamsize)text.size());
+    // a single-key find through the sharded surface
+    std::vector<kmer_pair> kmers = read_kmers(fname);
+    kmer_pair got;
+    CHECK(hashmap.find(kmers[0].kmer_str(), got) && got == kmers[0]);
+    printf("rccl1 ok: %zu bytes, %d rounds\n", text.size(), hashmap.shard()->rounds());
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        fprintf(stderr, "usage: %s stock|refloop|rccl1 <kmer_file> ...\n", argv[0]);
+        return 2;
+    }
+    const std::string mode = argv[1], fname = argv[2];
+    try {
+        if (mode == "stock") return stock(fname);
+        if (mode == "refloop" && argc >= 5) return refloop(fname, atoi(argv[3]), argv[4]);
+        if (mode == "rccl1" && argc >= 4) return rccl1(fname, argv[3]);
+    } catch (const std::exception& ex) {
+        fprintf(stderr, "%s\n", ex.what());
+        return 1;
+    }
+    fprintf(stderr, "bad arguments\n");
+    return 2;
+}

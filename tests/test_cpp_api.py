@@ -1,0 +1,96 @@
+"""The C++ host surface (include/cs267_hw3_amd/*.hpp) on the GPU:
+  * the stock single-key HashMap (README.md:95,99): insert / find / size / full,
+  * the reference's own initialize_kmers + assemble_contigs + output_results loop
+    (kmer_hash.cpp:21-68, one DistributedHashMap::find per step) at P = 1, 2, 3, 8 ranks,
+  * the multi-rank DistributedHashMap through the drop-in driver (KH_RANKS=P ranks as threads on
+    one GPU, kh::ThreadComm) and over a one-rank RCCL communicator,
+  * the driver's stdout contract (kmer_hash.cpp:71-78, 143-145).
+Each rank's <prefix>_<rank>.dat == the ground truth of its block (read_kmers.hpp:55-58) and the
+sorted union == the reference-harness solution (scripts/check_it.sh semantics)."""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+import cs267_hw3_amd as kh
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+pytestmark = pytest.mark.gpu
+
+
+def _exe(kind, k):
+    return os.path.join(ROOT, "tools", f"kmer_hash_{k}") if kind == "driver" else \
+        os.path.join(ROOT, "tests", "cpp", f"test_hash_map_{k}")
+
+
+def _check_ranks(tmp_path, name, P, prefix="out"):
+    m = MANIFEST[name]
+    g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"], seed=m["seed"])
+    parts = []
+    for r in range(P):
+        got = open(tmp_path / f"{prefix}_{r}.dat", "rb").read()
+        b, e = g.block(P, r)
+        assert got == g.truth(b, e), f"rank {r}"
+        parts.append(got)
+    want = open(os.path.join(GOLDEN, f"{name}_test_0.dat"), "rb").read()
+    assert sorted(b"".join(parts).splitlines()) == sorted(want.splitlines())
+
+
+@pytest.mark.parametrize("name,k", [("tiny19", 19), ("small51", 51)])
+def test_stock_hashmap_surface(name, k):
+    r = subprocess.run([_exe("test", k), "stock", os.path.join(GOLDEN, f"{name}.txt")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "stock ok" in r.stdout
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 8])
+@pytest.mark.parametrize("name,k", [("tiny19", 19), ("small51", 51)])
+def test_reference_find_loop(tmp_path, name, k, P):
+    """kmer_hash.cpp:38-55 as written: one find() per walk step, answered by the owner's table."""
+    r = subprocess.run([_exe("test", k), "refloop", os.path.join(GOLDEN, f"{name}.txt"), str(P), "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    _check_ranks(tmp_path, name, P)
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("name,k", [("mixed19", 19), ("small51", 51), ("singles51", 51), ("k60", 60)])
+def test_driver_multirank_threads(tmp_path, name, k, P):
+    if not os.path.exists(_exe("driver", k)):
+        pytest.skip(f"driver for k={k} not built")
+    env = dict(os.environ, KH_RANKS=str(P), KH_COMM="thread")
+    r = subprocess.run([_exe("driver", k), os.path.join(GOLDEN, f"{name}.txt"), "test", "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    _check_ranks(tmp_path, name, P)
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1                       # BUtil::print: rank 0 only
+    assert re.fullmatch(r"Rank 0 reconstructed \d+ contigs with \d+ nodes from 0 start nodes\. "
+                        r"\(\d+\.\d{6} read, \d+\.\d{6} insert, \d+\.\d{6} total\)", lines[0])
+
+
+@pytest.mark.parametrize("name,k", [("small51", 51), ("mixed19", 19)])
+def test_sharded_over_rccl_one_rank(tmp_path, name, k):
+    r = subprocess.run([_exe("test", k), "rccl1", os.path.join(GOLDEN, f"{name}.txt"), "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert open(tmp_path / "out_0.dat", "rb").read() == \
+        open(os.path.join(GOLDEN, f"{name}_test_0.dat"), "rb").read()
+
+
+def test_driver_summary_line(tmp_path):
+    """kmer_hash.cpp:71-78: contigs = lines of test_0.dat, nodes = k-mers over all contigs."""
+    name, k = "small51", 51
+    r = subprocess.run([_exe("driver", k), os.path.join(GOLDEN, f"{name}.txt"), "test", "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    text = open(tmp_path / "out_0.dat", "rb").read()
+    nc = text.count(b"\n")
+    m = re.fullmatch(r"Rank 0 reconstructed (\d+) contigs with (\d+) nodes from 0 start nodes\. "
+                     r"\((\S+) read, (\S+) insert, (\S+) total\)", r.stdout.strip())
+    assert m and int(m.group(1)) == nc and int(m.group(2)) == MANIFEST[name]["n"]
