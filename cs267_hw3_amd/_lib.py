@@ -110,6 +110,7 @@ _SIGS = {
     "kh_gen_destroy": (ctypes.c_int, [c_vp]),
     "kh_gen_num_contigs": (c_u64, [c_vp]),
     "kh_gen_records": (ctypes.c_int, [c_vp, c_u64, c_u64, c_vp]),
+    "kh_gen_records_dev": (ctypes.c_int, [c_vp, c_u64, c_u64, c_vp, c_vp]),
     "kh_gen_truth": (ctypes.c_int, [c_vp, c_u64, c_u64, c_vp, c_u64, ctypes.POINTER(c_u64)]),
 }
 

@@ -548,6 +548,7 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
     uint64_t a[IPT], b[IPT];
     if (COLLECT && threadIdx.x == 0) *scount = 0;
     load_words_tb<W, TB, TILE>(words, b0, min(b0 + TILE, n), b0 < n ? b0 : 0, a, b);
+    if (COLLECT) lds_barrier();  // the splitter counter is zero before any wave counts
     for (int tt = 0; tt < T1; ++tt) {
         const uint64_t base = b0 + (uint64_t)tt * TILE;
         if (base >= n) break;  // uniform

@@ -841,6 +841,7 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* _
     __shared__ uint32_t h[MAX_RANKS];
     __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
     for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    __syncthreads();  // counters zeroed before any wave counts (records of <= 16 B take no barrier below)
     const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
     for (uint32_t j = 0; j < ROUTE_TILE / BLOCK; ++j) {
         const uint64_t sub = b0 + (uint64_t)j * BLOCK;
@@ -871,6 +872,7 @@ __global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p, const uint8_
     __shared__ uint32_t h[MAX_RANKS];
     __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
     for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    __syncthreads();  // counters zeroed before any wave counts (records of <= 16 B take no barrier below)
     const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
     for (uint32_t j = 0; j < ROUTE_TILE / BLOCK; ++j) {
         const uint64_t sub = b0 + (uint64_t)j * BLOCK;

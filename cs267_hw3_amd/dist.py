@@ -386,7 +386,8 @@ class DistributedKmerHashMap:
             # per-peer bytes of a chunk <= chunk records * W * 8: keep every transfer under the
             # per-peer message limit whatever the skew
             nch = max(self.INSERT_CHUNKS, -(-n * W * 8 // self.A2A_CHUNK_BYTES))
-        bounds = [n * c // nch for c in range(nch + 1)]
+        # chunk starts at multiples of 16 records: every chunk's records stay 16-B aligned
+        bounds = [min(n, (n * c // nch) & ~15) for c in range(nch)] + [n]
         words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
         counts = []
         for c in range(nch):
@@ -555,33 +556,47 @@ class DistributedKmerHashMap:
 
 
 # --------------------------------------------------------------------------------------------
-def run_threaded(k, recs_np, nranks, device=0, info=None, insert_chunks=None, shard_kmers=None):
-    """P logical ranks on one GPU (threads): returns the per-rank contig texts. `info` (a dict)
-    receives the round count and per-rank table stats."""
+def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard_kmers=None,
+                 check=None):
+    """P logical ranks on one GPU (threads): returns the per-rank contig texts. recs: a host
+    record array, or a SyntheticKmers whose blocks each rank generates on the GPU (C4-size
+    inputs). Shards start at shard_kmers (default n / P) and grow to what they are routed.
+    check(rank, text) (optional) consumes each rank's text instead of returning it (large runs).
+    `info` (a dict) receives the round count and per-rank table stats."""
     import numpy as np
     comms = ThreadComm.group(nranks)
-    n = recs_np.shape[0]
+    gen = recs if hasattr(recs, "records_dev") else None
+    n = gen.n if gen is not None else recs.shape[0]
     split = (n + nranks - 1) // nranks
     out = [None] * nranks
     errs = []
+    start = shard_kmers if shard_kmers else max(n // nranks, 1)
 
     def body(r):
         try:
             torch.cuda.set_device(device)
             b = min(r * split, n)
             e = min(b + split, n)
-            shard = GpuShard(k, max(n, 1), device=device)
+            shard = GpuShard(k, start, device=device)
             with torch.cuda.stream(shard.stream):
-                recs = torch.from_numpy(np.ascontiguousarray(recs_np[b:e])).to(shard.dev)
+                if gen is not None:
+                    mine = gen.records_dev(b, e, device=device, stream=shard.stream)
+                else:
+                    mine = torch.from_numpy(np.ascontiguousarray(recs[b:e])).to(shard.dev)
                 dm = DistributedKmerHashMap(comms[r], shard)
                 if insert_chunks:
                     dm.INSERT_CHUNKS = insert_chunks
                     dm.PIPELINE_MIN = 0
-                dm.insert_all(recs)
+                dm.insert_all(mine)
                 shard.sync()
+                del mine
                 comms[r].barrier()
                 dm.assemble(n)
-                out[r] = dm.contigs_text()
+                text = dm.contigs_text()
+                if check is not None:
+                    check(r, text)
+                else:
+                    out[r] = text
                 if info is not None:
                     info.setdefault("rounds", dm.rounds)
                     info.setdefault("stats", {})[r] = shard.stats()

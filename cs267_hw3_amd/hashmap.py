@@ -249,6 +249,19 @@ class SyntheticKmers:
         check(self._L.kh_gen_records(self._h, begin, end, _ptr(out)))
         return out
 
+    def records_dev(self, begin=0, end=None, device=None, stream=None):
+        """Records [begin, end) generated on the GPU into a uint8 torch tensor [m, R] (16-B
+        aligned); stream: a torch stream (default: the current one)."""
+        import torch
+        end = self.n if end is None else end
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        with torch.cuda.device(dev):
+            out = torch.empty(max(end - begin, 1) * self.R + 16, dtype=torch.uint8, device=dev)
+            s = stream if stream is not None else torch.cuda.current_stream(dev)
+            check(self._L.kh_gen_records_dev(self._h, begin, end, ctypes.c_void_p(out.data_ptr()),
+                                             ctypes.c_void_p(s.cuda_stream)))
+        return out[:(end - begin) * self.R].view(end - begin, self.R)
+
     def truth(self, begin=0, end=None):
         end = self.n if end is None else end
         nb = ctypes.c_uint64(0)

@@ -172,7 +172,9 @@ public:
             nch = std::max<uint64_t>(kInsertChunks, (n * W_ * 8 + lim - 1) / lim);
         }
         std::vector<uint64_t> bounds(nch + 1);
-        for (uint64_t c = 0; c <= nch; ++c) bounds[c] = n * c / nch;
+        // chunk starts at multiples of 16 records: every chunk's records stay 16-B aligned
+        for (uint64_t c = 0; c < nch; ++c) bounds[c] = std::min<uint64_t>(n, (n * c / nch) & ~15ull);
+        bounds[nch] = n;
         int64_t* words = words_.words(std::max<uint64_t>(n, 1) * W_);
         int64_t* cnt = counts_.words(nch * (P + 1));
         const uint8_t* recs = static_cast<const uint8_t*>(dev_recs);

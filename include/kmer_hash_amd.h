@@ -220,6 +220,10 @@ uint64_t kh_gen_num_contigs(const kh_gen* g);
 /* records at output positions [pos_begin, pos_end) in kmer_pair layout (block split of
  * read_kmers.hpp:55-58 = positions [r*ceil(n/P), ...)) */
 int kh_gen_records(const kh_gen* g, uint64_t pos_begin, uint64_t pos_end, uint8_t* out);
+/* the same records produced by the GPU into device memory (R bytes each, contiguous) on a HIP
+ * stream (NULL = default stream): a 200M-record C3 set in milliseconds instead of seconds of host
+ * work and a PCIe upload. Async; the generator must outlive the work. */
+int kh_gen_records_dev(kh_gen* g, uint64_t pos_begin, uint64_t pos_end, void* dev_out, void* hip_stream);
 /* ground-truth contig text of the contigs whose start k-mer lies in [pos_begin, pos_end), in
  * start-node order (= expected test_<rank>.dat bytes); bytes_out gets the size. out may be NULL
  * to query the size. */

@@ -5,7 +5,11 @@
 //        as threads on GPU 0 (kh::ThreadComm; P = 1: the single-GPU table), one find() per step
 //   test_hash_map_<K> rccl1   <kmer_file> <prefix>        DistributedHashMap over a one-rank RCCL
 //        communicator (sharded code path, RCCL all-gathers) -> <prefix>_0.dat
+//   test_hash_map_<K> gen     <n> <P> <len_min> <len_max> kh::ShardedTable at P ranks (threads, one
+//        GPU) on n generated k-mers (records made in HBM by kh_gen_records_dev); large enough per
+//        rank for the chunked, overlapped insert; each rank's text == its block's ground truth
 // Exit status 0 = pass; a failed check prints it and exits 1.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -151,6 +155,54 @@ int rccl1(const std::string& fname, const std::string& prefix) {
     return 0;
 }
 
+// read_kmers.hpp:55-58 block split
+void block(uint64_t n, int P, int r, uint64_t& b, uint64_t& e) {
+    const uint64_t split = (n + P - 1) / P;
+    b = std::min<uint64_t>(split * r, n);
+    e = std::min<uint64_t>(b + split, n);
+}
+
+int gen(uint64_t n, int P, uint32_t lmin, uint32_t lmax) {
+    kh_gen* g = nullptr;
+    kh::abi_check(kh_gen_create(&g, KMER_LEN, n, lmin, lmax, 10, 4242, 1, 0));
+    kh::ThreadComm::Group group(P);
+    std::vector<std::thread> th;
+    std::vector<int> ok(P, 0);
+    std::vector<int> rounds(P, 0);
+    for (int r = 0; r < P; ++r)
+        th.emplace_back([&, r] {
+            try {
+                kh::hip_check(hipSetDevice(0), "hipSetDevice");
+                uint64_t b, e;
+                block(n, P, r, b, e);
+                kh::ShardedTable st(KMER_LEN, n / P + 1, *group.comm(r), 0, &group);
+                kh::DevBuf recs;
+                void* d = recs.ensure((e - b) * kh_record_size(KMER_LEN) + 16);
+                kh::abi_check(kh_gen_records_dev(g, b, e, d, st.stream()));
+                st.insert_all_dev(d, e - b);
+                rounds[r] = st.assemble(n);
+                const std::string text = st.contigs_text();
+                uint64_t bytes = 0;
+                kh::abi_check(kh_gen_truth(g, b, e, nullptr, 0, &bytes));
+                std::string want(bytes, '\0');
+                kh::abi_check(kh_gen_truth(g, b, e, &want[0], bytes, &bytes));
+                ok[r] = text == want;
+            } catch (const std::exception& ex) {
+                fprintf(stderr, "rank %d: %s\n", r, ex.what());
+                group.abort();
+            }
+        });
+    for (auto& t : th) t.join();
+    kh_gen_destroy(g);
+    for (int r = 0; r < P; ++r)
+        if (!ok[r]) {
+            fprintf(stderr, "rank %d differs from the truth of its block\n", r);
+            return 1;
+        }
+    printf("gen ok: n=%llu P=%d rounds=%d\n", (unsigned long long)n, P, rounds[0]);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -160,6 +212,8 @@ int main(int argc, char** argv) {
     }
     const std::string mode = argv[1], fname = argv[2];
     try {
+        if (mode == "gen" && argc >= 6)
+            return gen(strtoull(argv[2], nullptr, 10), atoi(argv[3]), (uint32_t)atoi(argv[4]), (uint32_t)atoi(argv[5]));
         if (mode == "stock") return stock(fname);
         if (mode == "refloop" && argc >= 5) return refloop(fname, atoi(argv[3]), argv[4]);
         if (mode == "rccl1" && argc >= 4) return rccl1(fname, argv[3]);

@@ -94,3 +94,14 @@ def test_driver_summary_line(tmp_path):
     m = re.fullmatch(r"Rank 0 reconstructed (\d+) contigs with (\d+) nodes from 0 start nodes\. "
                      r"\((\S+) read, (\S+) insert, (\S+) total\)", r.stdout.strip())
     assert m and int(m.group(1)) == nc and int(m.group(2)) == MANIFEST[name]["n"]
+
+
+@pytest.mark.parametrize("k,n,P,lmin,lmax", [(51, 64_000_000, 8, 8, 200), (51, 12_000_000, 3, 200, 1374),
+                                             (19, 20_000_000, 5, 8, 400)])
+def test_sharded_table_generated(k, n, P, lmin, lmax):
+    """kh::ShardedTable at P ranks on generated data: per rank >= 4M records, so the insert takes
+    the chunked path (transfers on the exchange stream, staged partitioning on the table's)."""
+    r = subprocess.run([_exe("test", k), "gen", str(n), str(P), str(lmin), str(lmax)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gen ok" in r.stdout

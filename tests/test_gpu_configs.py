@@ -1,0 +1,107 @@
+"""Every BASELINE.json config at the size it names, on the GPU:
+
+  C2  k=19, 10M k-mers, one GPU                 -> test_gpu_parity.py (generator truth, 10M)
+  C3  k=51, 200M k-mers, one GPU, load 0.5      -> byte-compared to the generator's ground truth;
+      a C3-shape 20M sample byte-compared to the oracle (oracle/kmer_oracle.c, ~7 s)
+  C4  k=51, 1B k-mers sharded over 8 ranks      -> 8 logical ranks on one GPU (ThreadComm): each
+      rank's text == the truth of its block (read_kmers.hpp:55-58); the exchange protocol is the
+      one RCCL runs at 8 GPUs, only the transport differs
+  C5  k=51, 200M skewed k-mers over 8 ranks     -> same, with the C5 generator (8 chains of 10^6
+      k-mers, every start k-mer first: rank 0 owns every walker)
+
+Inputs are generated on the GPU (kh_gen_records_dev) so a 1B set takes seconds; the truth is
+built on the host by the same generator (kh_gen_truth) and compared per rank.
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+import cs267_hw3_amd as kh
+
+pytestmark = pytest.mark.gpu
+
+C3 = dict(k=51, len_min=8, len_max=200, single=0, seed=51)
+C5 = dict(k=51, len_min=2, len_max=16, single=0, seed=5199, n_long=8, long_len=1_000_000, front_starts=True)
+
+
+def _gen(cfg, n):
+    c = dict(cfg)
+    return kh.SyntheticKmers(c.pop("k"), n, c.pop("len_min"), c.pop("len_max"), c.pop("single"),
+                             seed=c.pop("seed"), **c)
+
+
+def _single_gpu(g, n):
+    """One table, records generated in HBM, one insert + assemble; returns the contig text."""
+    with kh.KmerHashTable(g.k, n, 0.5) as t:
+        s = torch.cuda.Stream()
+        t.set_stream(s.cuda_stream)
+        recs = g.records_dev(stream=s)
+        t.insert_dev(recs.data_ptr(), n)
+        t.sync()
+        del recs
+        t.assemble()
+        st = t.stats()
+        assert st["n_dup"] == 0 and st["n_full"] == 0 and st["n_missing"] == 0
+        return t.contigs_text(), st
+
+
+def test_device_generator_matches_host():
+    """kh_gen_records_dev == kh_gen_records (plain and C5 orders, unaligned ranges)."""
+    import numpy as np
+    for cfg, n in ((C3, 3_000_000), (C5, 1_500_000), (dict(C3, k=19, seed=19, len_min=200, len_max=1374), 2_000_000)):
+        g = _gen(dict(cfg, long_len=100_000) if "long_len" in cfg else cfg, n)
+        for b, e in ((0, n), (12345, 1_234_567), (n - 77, n)):
+            got = g.records_dev(b, e).cpu().numpy()
+            assert np.array_equal(got, g.records(b, e))
+
+
+def test_c3_full_size_vs_truth():
+    """BASELINE configs[2] at full size: 200M k-mers, k=51, load 0.5."""
+    n = 200_000_000
+    g = _gen(C3, n)
+    text, st = _single_gpu(g, n)
+    assert st["n_contigs"] == g.num_contigs
+    assert text == g.truth()
+
+
+def test_c3_shape_20m_vs_oracle():
+    """The oracle (serial stock open addressing + the reference walk) on a 20M C3-shape set."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_bind as ob
+    n = 20_000_000
+    g = _gen(C3, n)
+    rc, want, nc, _, _, _ = ob.assemble(51, g.records())
+    assert rc == 0
+    text, st = _single_gpu(g, n)
+    assert st["n_contigs"] == nc
+    assert text == want
+
+
+def _sharded(g, P, **kw):
+    from cs267_hw3_amd.dist import run_threaded
+    bad = []
+
+    def check(r, text):
+        b, e = g.block(P, r)
+        if text != g.truth(b, e):
+            bad.append(r)
+
+    info = {}
+    run_threaded(g.k, g, P, check=check, info=info, **kw)
+    assert not bad, f"ranks {bad} differ from the truth of their blocks"
+    return info
+
+
+def test_c4_1b_kmers_8_ranks():
+    """BASELINE configs[3]: 1B k-mers, k=51, sharded over 8 ranks (logical, one GPU)."""
+    n = 1_000_000_000
+    info = _sharded(_gen(C3, n), 8)
+    assert sum(s["n_inserted"] for s in info["stats"].values()) == n
+
+
+def test_c5_skewed_200m_8_ranks():
+    """BASELINE configs[4]: the skewed set at 200M over 8 ranks (logical, one GPU)."""
+    info = _sharded(_gen(C5, 200_000_000), 8)
+    assert sum(s["n_inserted"] for s in info["stats"].values()) == 200_000_000
