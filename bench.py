@@ -44,33 +44,66 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(w, sample_n):
-    """Oracle (plain-C serial stock-semantics restatement) on a bounded sample of the workload,
-    this host, 1 core."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_bind as ob
-    import cs267_hw3_amd as kh
-    g = kh.SyntheticKmers(w["k"], sample_n, w["len_min"], w["len_max"], w["single"],
-                          seed=w["seed"], **w.get("gen", {}))
-    recs = g.records()
-    rc, text, nc, nl, ti, tw = ob.assemble(w["k"], recs)
-    if rc != 0:
-        raise RuntimeError(f"oracle failed rc={rc}")
-    ok = text == g.truth()
-    ops = (sample_n + nl) / (ti + tw)
-    cpu = "unknown"
+def host_cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": ops, "unit": "ops/s", "cores": 1, "kind": "port",
-            "sample": f"{sample_n} k-mers of the same generator/config (k={w['k']}, seed "
-                      f"{w['seed']}), {nc} contigs; insert {ti:.2f}s + walk {tw:.2f}s; "
-                      f"oracle/kmer_oracle.c serial stock semantics (djb2, linear probing, "
-                      f"load 0.5); output == ground truth: {ok}; host CPU: {cpu}"}
+    return "unknown"
+
+
+def host_threads():
+    """Threads for the parallel CPU baseline: this process's CPU share (OMP_NUM_THREADS on the GPU
+    box, else the affinity mask) — os.cpu_count() reports the whole machine there."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(avail, int(env))) if env and env.isdigit() else avail
+
+
+def cpu_baseline(w, host_recs, truth, sample_n):
+    """CPU restatements of the reference path on this host (oracle/, test infrastructure):
+    (1) the thread-parallel DistributedHashMap restatement (oracle/kmer_oracle_par.c: threads =
+        ranks, block split, owner-batched insert_all, each rank walks its own start nodes) on the
+        FULL workload, all cores of this process's share -> `value`;
+    (2) the serial stock-semantics oracle (oracle/kmer_oracle.c, 1 core) on a bounded sample of
+        the same generator/config -> `serial`.
+    Both time the reference's boundary (records packed in host memory -> contigs in host memory,
+    kmer_hash.cpp:129-137), file I/O excluded."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    import cs267_hw3_amd as kh
+    k, n = w["k"], len(host_recs)
+    P = host_threads()
+    rc, text, nc, nl, ti, tw = ob.assemble_par(k, host_recs, P)
+    if rc != 0:
+        raise RuntimeError(f"parallel oracle failed rc={rc}")
+    ok_par = text == truth
+    del text
+    par_ops = (n + nl) / (ti + tw)
+    serial = None
+    if sample_n:
+        g = kh.SyntheticKmers(k, sample_n, w["len_min"], w["len_max"], w["single"],
+                              seed=w["seed"], **w.get("gen", {}))
+        rc, text, snc, snl, sti, stw = ob.assemble(k, g.records())
+        if rc != 0:
+            raise RuntimeError(f"oracle failed rc={rc}")
+        serial = {"value": (sample_n + snl) / (sti + stw), "unit": "ops/s", "cores": 1, "kind": "port",
+                  "sample": f"{sample_n} k-mers of the same generator/config, {snc} contigs; insert "
+                            f"{sti:.2f}s + walk {stw:.2f}s; oracle/kmer_oracle.c serial stock semantics "
+                            f"(djb2, linear probing, load 0.5); output == ground truth: {text == g.truth()}"}
+    return {"value": par_ops, "unit": "ops/s", "cores": P, "kind": "port",
+            "nproc": os.cpu_count(), "host_cpu": host_cpu_model(),
+            "sample": f"the full workload: {n} k-mers, {nc} contigs; {P} threads as {P} ranks "
+                      f"(oracle/kmer_oracle_par.c: block split read_kmers.hpp:55-58, owner-batched "
+                      f"insert_all hash_map.hpp:55-80 into stock open-addressing shards at load 0.5, "
+                      f"each rank walks its own start nodes kmer_hash.cpp:38-55); insert {ti:.2f}s + "
+                      f"walk {tw:.2f}s; output == ground truth: {ok_par}",
+            "serial": serial}
 
 
 def load_traffic(workload, n_per_gpu):
@@ -86,6 +119,42 @@ def load_traffic(workload, n_per_gpu):
     return e, os.path.relpath(path, ROOT)
 
 
+def end_to_end(table, host, n, nl, truth, steps):
+    """The reference's timed boundary (kmer_hash.cpp:129-137): records packed in host memory ->
+    contigs in host memory. One step = kh_insert of the host records (H2D from pinned memory +
+    the insert pipeline), assemble, D2H of the contig text into pinned memory."""
+    import ctypes
+    import numpy as np
+    import torch
+    import cs267_hw3_amd as kh
+    L = kh._lib.lib()
+    pin = torch.empty(host.nbytes, dtype=torch.uint8, pin_memory=True)
+    pin.numpy()[:] = host.reshape(-1).view(np.uint8)
+    tb = len(truth)
+    tpin = torch.empty(tb + 64, dtype=torch.uint8, pin_memory=True)
+    nb = ctypes.c_uint64(0)
+    nco = ctypes.c_uint64(0)
+
+    def step():
+        table.clear()
+        kh._lib.check(L.kh_insert(table._h, ctypes.c_void_p(pin.data_ptr()), n))
+        kh._lib.check(L.kh_assemble(table._h, ctypes.byref(nco), ctypes.byref(nb)))
+        kh._lib.check(L.kh_contigs_text(table._h, ctypes.c_void_p(tpin.data_ptr()), tb + 64))
+
+    step()
+    times = []
+    for _ in range(steps):
+        t = time.perf_counter()
+        step()
+        times.append((time.perf_counter() - t) * 1e3)
+    ok = nb.value == tb and bytes(tpin.numpy()[:tb]) == truth
+    med = sorted(times)[len(times) // 2]
+    return {"value": (n + nl) / (med / 1e3), "unit": "ops/s", "ms_per_step_median": med, "step_ms": times,
+            "h2d_bytes": int(host.nbytes), "d2h_bytes": tb, "verified_vs_truth": ok,
+            "note": "reference boundary (kmer_hash.cpp:129-137): kh_insert from pinned host records "
+                    "(H2D + insert), kh_assemble, kh_contigs_text D2H into pinned host memory"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,7 +163,10 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--n", type=int, default=0, help="override k-mers per GPU")
     ap.add_argument("--cpu-sample", type=int, default=20_000_000,
-                    help="k-mers for the CPU baseline sample (0 = skip)")
+                    help="k-mers for the serial CPU baseline sample (0 = skip the serial leg)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--e2e-steps", type=int, default=3,
+                    help="steps of the reference-boundary (host records -> host contigs) figure")
     ap.add_argument("--no-verify", action="store_true")
     args = ap.parse_args()
 
@@ -135,20 +207,24 @@ def main():
     for _ in range(args.warmup):
         step()
     table.sync()
-    phases = []
+    phases, step_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        phases.append(step())
+        ts = time.perf_counter()
+        phases.append(step())           # step() ends with a stream sync: per-step wall time
+        step_ms.append((time.perf_counter() - ts) * 1e3)
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1e3 / args.steps
     s = phases[-1]
     nc, nl = s["n_contigs"], s["n_lookups"]
     assert s["n_inserted"] == n and nl == n - nc, s
+    truth = g.truth()
     ok = None
     if not args.no_verify:
-        ok = table.contigs_text() == g.truth()
+        ok = table.contigs_text() == truth
         if not ok:
             raise SystemExit("bench: contig text differs from the generator ground truth")
+    e2e = end_to_end(table, host, n, nl, truth, args.e2e_steps) if args.e2e_steps else None
     ops = n + nl
     value = ops / (ms / 1e3)
     avg = lambda key: sum(p[key] for p in phases) / len(phases)  # noqa: E731
@@ -182,14 +258,15 @@ def main():
         insert_pipe["traffic_GBs"] = insert_pipe["traffic"] / (ins_ms / 1e3) / 1e9
         insert_pipe["traffic_frac"] = insert_pipe["traffic_GBs"] / HBM_PEAK_GBS
     cpu = None
-    if args.cpu_sample:
+    if not args.no_cpu:
         t = time.time()
-        cpu = cpu_baseline(w, min(args.cpu_sample, n))
+        cpu = cpu_baseline(w, host, truth, min(args.cpu_sample, n))
         log(f"cpu baseline took {time.time() - t:.1f}s")
     out = {
         "metric": "k-mer inserts+lookups/sec (k=51)" if k == 51 else f"k-mer inserts+lookups/sec (k={k})",
         "value": value, "unit": "ops/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": ms,
+        "ms_per_step_median": sorted(step_ms)[len(step_ms) // 2], "step_ms": step_ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": value / BEST_PUBLISHED_OPS, "dtype": "u64", "data": "synthetic",
         "config": {"workload": w["desc"], "k": k, "n_kmers_per_gpu": n, "contigs": nc,
                    "lookups": nl, "parallelism": "1 GPU", "load_factor": 0.5,
@@ -200,7 +277,7 @@ def main():
         "phases_ms": {"insert_total": avg("ms_insert"), "k_insert": ins_ms, "k_walk": walk_ms,
                       "materialize": avg("ms_materialize")},
         "verified_vs_truth": ok,
-        "roofline": roof, "insert_pipeline": insert_pipe, "cpu_baseline": cpu,
+        "roofline": roof, "insert_pipeline": insert_pipe, "end_to_end": e2e, "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
     table.close()

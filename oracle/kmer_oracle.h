@@ -42,6 +42,13 @@ int ko_assemble(int K, const uint8_t* recs, size_t n, char** out, size_t* out_le
                 size_t* n_contigs, size_t* n_lookups, double* t_insert, double* t_walk);
 void ko_free(void* p);
 
+/* Thread-parallel restatement of the DistributedHashMap path (kmer_oracle_par.c): P threads as
+ * P ranks, block split (read_kmers.hpp:55-58), owner-batched insert_all (hash_map.hpp:55-80),
+ * each rank walks its own start nodes (kmer_hash.cpp:38-55). Output = the ranks' test_<r>.dat
+ * concatenated in rank order (== ko_assemble's text). Same return codes (+ -5 bad P). */
+int ko_assemble_par(int K, const uint8_t* recs, size_t n, int P, char** out, size_t* out_len,
+                    size_t* n_contigs, size_t* n_lookups, double* t_insert, double* t_walk);
+
 /* Stock table, exposed for find()/insert() unit parity. */
 typedef struct ko_table ko_table;
 ko_table* ko_table_new(int K, size_t size);

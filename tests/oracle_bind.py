@@ -38,6 +38,11 @@ def lib():
                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
         o.ko_assemble.restype = ctypes.c_int
+        o.ko_assemble_par.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(vp),
+                                      ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double)]
+        o.ko_assemble_par.restype = ctypes.c_int
         o.ko_free.argtypes = [vp]
         o.ko_table_new.argtypes = [ctypes.c_int, ctypes.c_size_t]
         o.ko_table_new.restype = vp
@@ -92,6 +97,23 @@ def assemble(k, recs):
     ti, tw = ctypes.c_double(), ctypes.c_double()
     rc = lib().ko_assemble(k, _p(recs), n, ctypes.byref(out), ctypes.byref(ln), ctypes.byref(nc),
                            ctypes.byref(nl), ctypes.byref(ti), ctypes.byref(tw))
+    text = b""
+    if rc == 0:
+        text = ctypes.string_at(out, ln.value)
+        lib().ko_free(out)
+    return rc, text, nc.value, nl.value, ti.value, tw.value
+
+
+def assemble_par(k, recs, threads):
+    """Thread-parallel DistributedHashMap restatement (threads = ranks) -> same tuple as assemble;
+    the text is the ranks' outputs concatenated in rank order."""
+    recs = np.ascontiguousarray(recs, np.uint8)
+    n = recs.shape[0] if recs.ndim == 2 else recs.size // ((k + 3) // 4 + 2)
+    out = ctypes.c_void_p()
+    ln, nc, nl = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    ti, tw = ctypes.c_double(), ctypes.c_double()
+    rc = lib().ko_assemble_par(k, _p(recs), n, threads, ctypes.byref(out), ctypes.byref(ln),
+                               ctypes.byref(nc), ctypes.byref(nl), ctypes.byref(ti), ctypes.byref(tw))
     text = b""
     if rc == 0:
         text = ctypes.string_at(out, ln.value)

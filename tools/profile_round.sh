@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${1:-run}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 --no-verify ${BARGS:-}"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu --e2e-steps 0 --no-verify ${BARGS:-}"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$OUT/trace -- $B > $OUT/trace.log 2>&1
 python3 tools/kstats.py $OUT/trace > $OUT/kernel_stats.txt
 for c in FETCH_SIZE WRITE_SIZE TCC_EA0_ATOMIC_sum; do
