@@ -2,7 +2,8 @@
 //
 // Replaces one-CAS-per-key global inserts (bound at ~20 G random CAS/s on MI355X, measured by
 // tools/membench) with streaming passes:
-//   pass 1   group the batch by the top 9 bits of key_hash (512 buckets x S1 windows); records
+//   pass 1   group the batch by the top 9 bits of the placement hash (512 buckets x S1 windows;
+//            place: region = a hash of the k-mer's minimizer window, kh_codec.hpp); records
 //            are parsed by the pass itself (k_win1_rec) or converted to words first
 //            (k_part1_convert, other k), routed words go straight in (k_win1)
 //   pass 2   then by the next 8 bits, within each pass-1 bucket, into 2^17 region windows (k_win2)
@@ -14,6 +15,11 @@
 //   overflow keys whose probe run leaves their slice take the global CAS path afterwards, so
 //            every key satisfies the linear-probing invariant "all slots from home to position
 //            are occupied"
+//   chains   with the region's keys in LDS, every k-mer whose successor (next_kmer) shares its
+//            minimizer (provable from j*: the minimizer window survives the shift and the new
+//            window orders above it) looks the successor up in LDS; each chain head (no linked
+//            predecessor) gets a head record {tail key + ext, links} and its slot the record index,
+//            so the walker crosses a run of ~20 k-mers (K=51) with two requests instead of ~20
 // Placement differs from the CAS path; find()/the walk depend only on the invariant, so outputs
 // are identical (tests run both paths).
 #include <hip/hip_runtime.h>
@@ -24,13 +30,16 @@
 
 #include "kh_device.hpp"
 
+#include <cstdio>
+
 namespace kh {
 
 static constexpr int PB = 256;                    // threads per block of the small kernels
-static constexpr int B1 = 9, B2 = 8;              // radix bits per pass
+static constexpr int B1 = 9, B2 = 8;              // radix bits per pass (pass 2: up to B2, p.rbits - B1)
 static constexpr int NB1 = 1 << B1, NB2 = 1 << B2;
-static constexpr int RBITS = B1 + B2;             // region = top 17 hash bits
-static constexpr uint32_t NREG = 1u << RBITS;
+static constexpr uint32_t NREG_MAX = 1u << (B1 + B2);
+static_assert(B1 == REGION_BITS_MIN && B1 + B2 == REGION_BITS_MAX, "regions of the placement hash");
+__host__ __device__ inline uint32_t nreg(const KParams& p) { return 1u << p.rbits; }
 static constexpr int BUILD_THREADS = 512;
 static constexpr int T1 = 2;                      // consecutive tiles per pass-1 block
 static constexpr uint32_t S1 = 8;                 // pass-1 windows (atomic counters) per bucket
@@ -53,18 +62,24 @@ static uint64_t win_G(uint64_t n) {
     return (tiles_per_bucket + 1) / 2;
 }
 
-uint64_t part_count_words() { return (NW1 + NREG) / 2; }
+uint64_t part_count_words() { return (NW1 + NREG_MAX) / 2; }
 
 uint64_t part_overflow_cap(uint64_t n) { return n / 4 + 65536; }
 
-uint32_t part_region_cap(uint64_t n) {
-    const double mu = (double)n / NREG;
-    return (uint32_t)(mu + 10.0 * sqrt(mu) + 16.0);
+// Window capacities. Regions are picked by minimizer, so a region's load is a sum of runs of
+// ~19 k-mers (compound Poisson: variance = mu * E[S^2]/E[S] ~ 30 mu at K=51, M=16: C3 sd 210 for
+// mu 1526, simulated): the region windows hold mu + 7 sigma; pass-1 windows see 1/S1 of a bucket
+// (sigma^2 = mu1 (1 + 30/S1)). A full window spills to the overflow list (global CAS inserts),
+// never loses a key.
+static constexpr double CLUMP = 30.0;
+uint32_t part_region_cap(const KParams& p, uint64_t n) {
+    const double mu = (double)n / nreg(p);
+    return (uint32_t)(mu + 7.0 * sqrt(CLUMP * mu) + 16.0);
 }
 
 uint32_t part_win1_cap(uint64_t n) {
     const double mu = (double)n / NW1;
-    return (uint32_t)(mu + 10.0 * sqrt(mu) + 64.0);
+    return (uint32_t)(mu + 10.0 * sqrt(mu * (1.0 + CLUMP / S1)) + 64.0);
 }
 
 uint64_t part_buf1_words(const KParams& p, uint64_t n) {
@@ -73,24 +88,32 @@ uint64_t part_buf1_words(const KParams& p, uint64_t n) {
 }
 
 uint64_t part_buf2_words(const KParams& p, uint64_t n) {
-    const uint64_t w = (uint64_t)NREG * part_region_cap(n);
+    const uint64_t w = (uint64_t)nreg(p) * part_region_cap(p, n);
     return (w > n ? w : n) * p.W;
 }
 
-static uint64_t region_max_slots(uint64_t cap) { return cap / NREG + 1; }
+static uint64_t region_max_slots(const KParams& p, uint64_t cap) { return cap / nreg(p) + 1; }
+// build LDS: the slice, plus one 16-bit successor per slot when chains are built
+static uint64_t build_lds(const KParams& p, uint64_t cap, bool chains) {
+    // chains: a 16-bit successor per slot + the head list (<= slots/8 + 32 entries, part_head_cap)
+    const uint64_t sm = region_max_slots(p, cap);
+    return sm * 8ull * p.W + (chains ? sm * 2 + (sm / 8 + 32) * 2 : 0) + 16;
+}
 
-bool region_slots_fit(const KParams& p, uint64_t cap) {
-    return region_max_slots(cap) <= LDS_BYTES / (8ull * p.W);
+bool region_slots_fit(const KParams& p, uint64_t cap) { return build_lds(p, cap, false) <= LDS_BYTES; }
+
+// head records per region: room for chains of >= 8 slots (C3: 413 for ~75 heads); 0 = no chains
+uint32_t part_head_cap(const KParams& p, uint64_t cap) {
+    if (!p.chain || build_lds(p, cap, true) > LDS_BYTES || region_max_slots(p, cap) >= 0xFFFF) return 0;
+    const uint64_t lim = (1ull << (SCRATCH_BIT - p.idx_lo)) - 1;
+    const uint64_t h = region_max_slots(p, cap) / 8 + 32;
+    return (uint32_t)(h < lim ? h : lim);
 }
 
 bool part_usable(const KParams& p, uint64_t cap, uint64_t n) {
-    return n >= (1ull << 20) && region_slots_fit(p, cap) && cap >= (uint64_t)NREG * 8;
+    return n >= (1ull << 20) && region_slots_fit(p, cap) && cap >= (uint64_t)nreg(p) * 8;
 }
 
-template <int W>
-__device__ __forceinline__ uint64_t words_hash(uint64_t w0, uint64_t w1, const KParams& p) {
-    return key_hash(slot_key(w0, w1, p));
-}
 
 // ---- record -> word conversion (k other than 51 / 19) ---------------------------------------------
 // Parse the reference records once, one per thread per 256-record sub-tile (the next sub-tile's
@@ -99,10 +122,11 @@ __device__ __forceinline__ uint64_t words_hash(uint64_t w0, uint64_t w1, const K
 template <int PK>
 __device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, int pad, Key& k, uint32_t& ext);
 
-template <int W, int PK = 0>
-__global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* __restrict__ recs,
+template <int W, int PK = 0, int KT = 0>
+__global__ __launch_bounds__(PB) void k_part1_convert(KParams p_in, const uint8_t* __restrict__ recs,
                                                       uint64_t n, uint64_t* words_out,
                                                       uint64_t* start_mask, uint64_t* split_mask) {
+    const KParams p = specialize<KT>(p_in);
     __shared__ __attribute__((aligned(16))) uint8_t stage[2][PB * 17 + 16];
     const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
     const uint64_t b1 = min(b0 + (uint64_t)T1 * PART_TILE, n);
@@ -146,13 +170,14 @@ __global__ __launch_bounds__(PB) void k_part1_convert(KParams p, const uint8_t* 
         const uint64_t bal = __ballot(is_start);
         const uint64_t wb = sub + (threadIdx.x & ~63u);
         if ((threadIdx.x & 63) == 0 && wb < b1 && start_mask) start_mask[wb >> 6] = bal;
-        const uint64_t hk = key_hash(k);
         if (split_mask) {
-            const uint64_t sb = __ballot(valid && !is_start && is_splitter(hk, p));
+            const uint64_t sb = __ballot(valid && !is_start && is_splitter(key_hash32(k), p));
             if ((threadIdx.x & 63) == 0 && wb < b1) split_mask[wb >> 6] = sb;
         }
         if (valid) {
-            const uint64_t w0 = slot_w0(k, ext, p), i = sub + threadIdx.x;
+            // the word carries its minimizer window j* (pass 1 reads the region from it)
+            const uint64_t w0 = part_word0(slot_w0(k, ext, p), mini_scan(k, p), p);
+            const uint64_t i = sub + threadIdx.x;
             if (W == 2) {
                 *reinterpret_cast<ulonglong2*>(words_out + i * 2) = make_ulonglong2(w0, k.lo);
             } else {
@@ -175,10 +200,13 @@ __device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, in
 }
 
 // ---- build ------------------------------------------------------------------------------------
-// LDS insert with linear probing inside the slice; false = the run left the slice.
+// LDS insert with linear probing inside the slice: the slot (>= 0), LDS_DUP (key present) or
+// LDS_OUT (the run left the slice).
+static constexpr int LDS_DUP = -1, LDS_OUT = -2;
 template <int W>
-__device__ __forceinline__ bool lds_insert(unsigned long long* lt, uint32_t S, uint64_t loc, uint64_t w0,
-                                           uint64_t w1, unsigned long long* stats) {
+__device__ __forceinline__ int lds_insert(const KParams& p, unsigned long long* lt, uint32_t S, uint64_t loc,
+                                          uint64_t w0, uint64_t w1, unsigned long long* stats) {
+    const uint64_t want0 = slot_keybits(w0, p);
     uint32_t spins = 0;
     while (loc < S) {
         const unsigned long long old = atomicCAS(&lt[W * loc], (unsigned long long)EMPTY, w0);
@@ -186,30 +214,136 @@ __device__ __forceinline__ bool lds_insert(unsigned long long* lt, uint32_t S, u
             if (W == 2)
                 __hip_atomic_store(&lt[2 * loc + 1], (unsigned long long)w1, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-            return true;
+            return (int)loc;
         }
-        if ((old >> 6) == (w0 >> 6)) {
+        if (slot_keybits(old, p) == want0) {
             if (W == 1) {
                 atomicAdd(&stats[ST_DUP], 1ull);
-                return true;
+                return LDS_DUP;
             }
             const unsigned long long o1 =
                 __hip_atomic_load(&lt[2 * loc + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (o1 == EMPTY) {  // the claiming lane has not stored word1 yet: retry this slot
                 if (++spins > (1u << 24)) {
                     atomicAdd(&stats[ST_SPIN], 1ull);
-                    return true;
+                    return LDS_DUP;
                 }
                 continue;
             }
             if (o1 == w1) {
                 atomicAdd(&stats[ST_DUP], 1ull);
-                return true;
+                return LDS_DUP;
             }
         }
         ++loc;
     }
-    return false;
+    return LDS_OUT;
+}
+
+// KH_DEBUG=build_prof: per-phase shader-clock cycles of the prefetching build (thread 0 of every
+// block, summed), printed after each build. Off: one uniform branch per phase.
+__device__ unsigned long long g_build_prof[8];
+#define BPROF(i)                                                                       \
+    do {                                                                               \
+        if (prof && threadIdx.x == 0) {                                                \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
+            atomicAdd(&g_build_prof[i], t_ - pt_);                                     \
+            pt_ = t_;                                                                  \
+        }                                                                              \
+    } while (0)
+
+// ---- chains ------------------------------------------------------------------------------------
+// After a region's keys are in LDS (lt: S slots): link every k-mer x to its successor y =
+// next_kmer(x) when y provably shares x's minimizer (x's minimizer window j* is not the one that
+// drops out, and the window y appends orders strictly above it: then y's minimizer value is x's,
+// y is in this region) and y is in this slice; y is not linked into when it is a splitter (the
+// walker must stop before those). A link is only ever made to the key next_kmer(x) itself, so a
+// chain record is exact whatever the regions are. Heads (a successor, no predecessor) of this
+// region get a record {tail word0 with the link count in the index field, tail word1} and their
+// slot the record index + 1. succ: S 16-bit entries; hcnt: the region's record counter (zeroed).
+static constexpr uint16_t NO_SUCC = 0xFFFFu;
+// The slot of x's successor in this slice, or NO_SUCC. With mtop (x is a word of this region's
+// window carrying the top bits of its minimizer order) the test needs no window extraction and
+// y's home is this region's; a tie in the top bits counts as "no link" (never a wrong link).
+template <int W, bool MTOP>
+__device__ __forceinline__ uint16_t chain_link(const KParams& p, const unsigned long long* lt, uint32_t S,
+                                               uint64_t lo, uint64_t cap, uint64_t w0, uint64_t w1) {
+    const uint32_t f = ext_fwd(slot_ext(w0));
+    const uint32_t j = slot_jstar(w0);
+    if (f > 3u || (int)j >= p.K - p.M) return NO_SUCC;
+    const Key x = slot_key(w0, w1, p);
+    const Key y = key_next(x, f, p);
+    uint32_t mw = 0;
+    if (MTOP) {
+        if (order_top(win_order(win_bits(y, 0, p)), p) <= slot_hidx(w0, p)) return NO_SUCC;
+    } else {
+        mw = win_bits(x, (int)j, p);
+        if (win_order(win_bits(y, 0, p)) <= win_order(mw)) return NO_SUCC;
+    }
+    const uint32_t hy = key_hash32(y);
+    if (is_splitter(hy, p)) return NO_SUCC;
+    const uint64_t home = MTOP ? home_in(lo, lo + S, hy) : home_of(place_w(mw, y, p), cap, p);
+    if (home < lo || home >= lo + S) return NO_SUCC;
+    const uint64_t want0 = W == 1 ? y.lo : y.hi;
+    for (uint32_t t = (uint32_t)(home - lo); t < S; ++t) {
+        const uint64_t v0 = lt[W * t];
+        if (v0 == EMPTY) break;
+        if (slot_keybits(v0, p) == want0 && (W == 1 || lt[W * t + 1] == y.lo)) return (uint16_t)t;
+    }
+    return NO_SUCC;
+}
+
+// Head records of the listed heads (hlist[0, min(*hcnt, hcap))): walk each chain to its tail.
+template <int W, int TB>
+__device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long* lt, const uint16_t* succ,
+                                            const uint16_t* hlist, uint32_t r, bool fresh, uint64_t* headrec,
+                                            uint32_t hcap, const uint32_t* hcnt) {
+    const uint32_t nh = min(*hcnt, hcap);
+    for (uint32_t id = threadIdx.x; id < nh; id += TB) {
+        const uint32_t i = hlist[id];
+        const uint64_t w0 = lt[W * i];
+        if (!fresh) {
+            // the walker reads a record at the region of the key it looked up: in a slice reloaded
+            // from the table only keys of this region may own one (others may have spilled in)
+            const Key hk = slot_key(w0, W == 2 ? lt[W * i + 1] : 0ull, p);
+            if (mini_region(mini_window(hk, mini_scan(hk, p), p), p) != r) continue;
+        }
+        uint32_t t = succ[i], links = 1;
+        while (succ[t] != NO_SUCC && links < 63u) {
+            t = succ[t];
+            ++links;
+        }
+        const uint64_t tw0 = lt[W * t], tw1 = W == 2 ? lt[W * t + 1] : 0ull;
+        *reinterpret_cast<ulonglong2*>(headrec + ((uint64_t)r * hcap + id) * 2) =
+            make_ulonglong2(with_hidx(slot_clean(tw0, p), links, p), tw1);
+        lt[W * i] = with_hidx(w0, id + 1, p);
+    }
+}
+
+template <int W, int TB>
+__device__ __forceinline__ void region_chains(const KParams& p, unsigned long long* lt, uint16_t* succ,
+                                              uint16_t* hlist, uint32_t S, uint64_t lo, uint64_t cap, uint32_t r,
+                                              bool fresh, uint64_t* headrec, uint32_t hcap, uint32_t* hcnt) {
+    for (uint32_t i = threadIdx.x; i < S; i += TB) {
+        const uint64_t w0 = lt[W * i];
+        uint16_t nx = NO_SUCC;
+        if (w0 != EMPTY) {
+            nx = chain_link<W, false>(p, lt, S, lo, cap, w0, W == 2 ? lt[W * i + 1] : 0ull);
+            if (nx != NO_SUCC) atomicOr(&lt[W * nx], 1ull << SCRATCH_BIT);  // nx has a predecessor
+        }
+        succ[i] = nx;
+    }
+    lds_barrier();
+    // heads (a successor, no predecessor) -> a dense list: the chain walks keep whole waves busy
+    for (uint32_t i = threadIdx.x; i < S; i += TB) {
+        if (succ[i] != NO_SUCC && !((lt[W * i] >> SCRATCH_BIT) & 1ull)) {
+            const uint32_t id = atomicAdd(hcnt, 1u);
+            if (id < hcap) hlist[id] = (uint16_t)i;
+        }
+    }
+    lds_barrier();
+    chain_heads<W, TB>(p, lt, succ, hlist, r, fresh, headrec, hcap, hcnt);
+    lds_barrier();
 }
 
 // Build from the region windows, one region per block at a time (windows larger than the
@@ -220,20 +354,31 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
                                                               uint64_t* ovf, uint64_t ovf_cap,
                                                               unsigned long long* ctr,
                                                               unsigned long long* stats,
-                                                              uint32_t RC, const uint32_t* rcnt) {
+                                                              uint32_t RC, const uint32_t* rcnt,
+                                                              uint64_t* headrec, uint32_t hcap, uint32_t smax) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
-    for (uint32_t r = blockIdx.x; r < NREG; r += gridDim.x) {
-        const uint64_t lo = mulhi64((uint64_t)r << (64 - RBITS), cap);
-        const uint64_t hi = (r + 1 < NREG) ? mulhi64((uint64_t)(r + 1) << (64 - RBITS), cap) : cap;
+    uint16_t* succ = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
+    uint16_t* hlist = succ + smax;
+    __shared__ uint32_t hcnt;
+    const uint32_t NR = nreg(p);
+    for (uint32_t r = blockIdx.x; r < NR; r += gridDim.x) {
+        if (threadIdx.x == 0) hcnt = 0;
+        const uint64_t lo = mulhi64((uint64_t)r << (64 - p.rbits), cap);
+        const uint64_t hi = (r + 1 < NR) ? mulhi64((uint64_t)(r + 1) << (64 - p.rbits), cap) : cap;
         const uint32_t S = (uint32_t)(hi - lo);
         if (W == 2) {
             ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
             const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
-                l2[i] = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                ulonglong2 v = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
+                if (v.x != EMPTY) v.x = slot_clean(v.x, p);  // earlier chain bits are rebuilt
+                l2[i] = v;
+            }
         } else {
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
-                lt[i] = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                const unsigned long long v = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
+                lt[i] = v == EMPTY ? v : slot_clean(v, p);
+            }
         }
         __syncthreads();
         const uint64_t b = (uint64_t)r * RC, e = b + min(rcnt[r], RC);
@@ -246,8 +391,9 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
             } else {
                 w0 = buf2[j];
             }
-            const uint64_t home = home_slot(words_hash<W>(w0, w1, p), cap);
-            if (!lds_insert<W>(lt, S, home - lo, w0, w1, stats)) {
+            // every word of region r's window is a key of region r; the slot keeps key, ext and j*
+            const uint64_t home = home_in(lo, hi, key_hash32(slot_key(w0, w1, p)));
+            if (lds_insert<W>(p, lt, S, home - lo, slot_clean(w0, p), w1, stats) == LDS_OUT) {
                 const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
                 if (idx < ovf_cap) {
                     ovf[idx * W] = w0;
@@ -258,6 +404,7 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
             }
         }
         __syncthreads();
+        if (hcap) region_chains<W, BUILD_THREADS>(p, lt, succ, hlist, S, lo, cap, r, table_empty != 0, headrec, hcap, &hcnt);
         if (W == 2) {
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
             const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
@@ -273,18 +420,25 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
 // to IPT words of the region it inserts and issues the loads of its words of the next region
 // before the LDS inserts and the slice write-out, and region hand-offs use LDS-only barriers,
 // so a block's window loads, LDS work and slice stores overlap.
-template <int W, int IPT>
-__global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p, const uint64_t* __restrict__ buf2,
+template <int W, int IPT, int KT>
+__global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p_in, const uint64_t* __restrict__ buf2,
                                                                  uint64_t* slots, uint64_t cap, int table_empty,
                                                                  uint64_t* ovf, uint64_t ovf_cap,
                                                                  unsigned long long* ctr,
                                                                  unsigned long long* stats, uint32_t RC,
-                                                                 const uint32_t* __restrict__ rcnt) {
+                                                                 const uint32_t* __restrict__ rcnt,
+                                                                 uint64_t* headrec, uint32_t hcap, uint32_t smax,
+                                                                 int prof) {
+    const KParams p = specialize<KT>(p_in);
     extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
+    uint16_t* succ = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
+    uint16_t* hlist = succ + smax;
+    __shared__ uint32_t hcnt;
+    unsigned long long pt_ = prof ? __builtin_amdgcn_s_memtime() : 0ull;
     uint64_t a[IPT], b[IPT];
     auto load = [&](uint32_t r, uint64_t (&x)[IPT], uint64_t (&y)[IPT]) {
-        const uint32_t m = r < NREG ? min(rcnt[r], RC) : 0u;
-        const uint64_t base = (uint64_t)(r < NREG ? r : 0) * RC;
+        const uint32_t m = r < nreg(p) ? min(rcnt[r], RC) : 0u;
+        const uint64_t base = (uint64_t)(r < nreg(p) ? r : 0) * RC;
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             const uint32_t i = threadIdx.x + (uint32_t)j * BUILD_THREADS;
@@ -303,30 +457,43 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p, cons
     };
     uint32_t r = blockIdx.x;
     load(r, a, b);
-    for (; r < NREG; r += gridDim.x) {
-        const uint64_t lo = mulhi64((uint64_t)r << (64 - RBITS), cap);
-        const uint64_t hi = (r + 1 < NREG) ? mulhi64((uint64_t)(r + 1) << (64 - RBITS), cap) : cap;
+    const uint32_t NR = nreg(p);
+    for (; r < NR; r += gridDim.x) {
+        const uint64_t lo = mulhi64((uint64_t)r << (64 - p.rbits), cap);
+        const uint64_t hi = (r + 1 < NR) ? mulhi64((uint64_t)(r + 1) << (64 - p.rbits), cap) : cap;
         const uint32_t S = (uint32_t)(hi - lo);
+        if (threadIdx.x == 0) hcnt = 0;
         if (W == 2) {
             ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
             const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
-                l2[i] = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                ulonglong2 v = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
+                if (v.x != EMPTY) v.x = slot_clean(v.x, p);  // earlier chain bits are rebuilt
+                l2[i] = v;
+            }
         } else {
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS)
-                lt[i] = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                const unsigned long long v = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
+                lt[i] = v == EMPTY ? v : slot_clean(v, p);
+            }
         }
         if (table_empty)
             lds_barrier();
         else
             __syncthreads();
+        BPROF(0);
         uint64_t na[IPT], nb[IPT];
         load(r + gridDim.x, na, nb);  // next region's words in flight during this one
+        int pos[IPT];  // LDS slot of each word inserted here (chains walk from these)
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
+            pos[j] = LDS_DUP;
             if (a[j] == EMPTY) continue;
-            const uint64_t home = home_slot(words_hash<W>(a[j], b[j], p), cap);
-            if (!lds_insert<W>(lt, S, home - lo, a[j], b[j], stats)) {
+            // every word of region r's window is a key of region r; the slot keeps key, ext and j*
+            // (the order bits stay in the register copy for the link test)
+            const uint64_t home = home_in(lo, hi, key_hash32(slot_key(a[j], b[j], p)));
+            pos[j] = lds_insert<W>(p, lt, S, home - lo, slot_clean(a[j], p), b[j], stats);
+            if (pos[j] == LDS_OUT) {
                 const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
                 if (idx < ovf_cap) {
                     ovf[idx * W] = a[j];
@@ -337,6 +504,33 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p, cons
             }
         }
         lds_barrier();
+        BPROF(1);
+        if (hcap && !table_empty) {
+            region_chains<W, BUILD_THREADS>(p, lt, succ, hlist, S, lo, cap, r, false, headrec, hcap, &hcnt);
+        } else if (hcap) {
+            // fresh slice: its keys are exactly this thread's words, so links are computed from
+            // registers (no pass over empty slots) and every key knows its slot
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                if (pos[j] < 0) continue;
+                const uint16_t nx = chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j]);
+                succ[pos[j]] = nx;
+                if (nx != NO_SUCC) atomicOr(&lt[W * nx], 1ull << SCRATCH_BIT);
+            }
+            lds_barrier();
+            BPROF(2);
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                if (pos[j] < 0 || succ[pos[j]] == NO_SUCC || ((lt[W * pos[j]] >> SCRATCH_BIT) & 1ull)) continue;
+                const uint32_t id = atomicAdd(&hcnt, 1u);
+                if (id < hcap) hlist[id] = (uint16_t)pos[j];
+            }
+            lds_barrier();
+            BPROF(3);
+            chain_heads<W, BUILD_THREADS>(p, lt, succ, hlist, r, true, headrec, hcap, &hcnt);
+            lds_barrier();
+            BPROF(4);
+        }
         if (W == 2) {
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
             const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
@@ -345,6 +539,7 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p, cons
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) slots[lo + i] = lt[i];
         }
         lds_barrier();
+        BPROF(5);
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             a[j] = na[j];
@@ -359,18 +554,35 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
                                  uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats, uint32_t RC,
                                  const uint32_t* rcnt, size_t lds, hipStream_t s) {
     const int te = table_empty ? 1 : 0;
+    const uint32_t smax = (uint32_t)region_max_slots(p, t.cap);
+    const uint32_t hcap = B.headrec ? B.hcap : 0u;
+    const int prof = debug_flag("build_prof") ? 1 : 0;
+    if (prof) {
+        static const unsigned long long zero[8] = {0};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_build_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, s);
+    }
     if (debug_flag("plain_build"))  // tests: the large-window kernel at small sizes
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap, ctr,
-                                                         stats, RC, rcnt);
+                                                         stats, RC, rcnt, B.headrec, hcap, smax);
     else if (RC <= 4u * BUILD_THREADS)
-        k_part_build_pf<W, 4><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
-                                                               ctr, stats, RC, rcnt);
+        with_kt<W>(p.K, [&](auto kt) { k_part_build_pf<W, 4, decltype(kt)::value><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
+                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
+    else if (RC <= 6u * BUILD_THREADS)
+        with_kt<W>(p.K, [&](auto kt) { k_part_build_pf<W, 6, decltype(kt)::value><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
+                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else if (RC <= 12u * BUILD_THREADS)
-        k_part_build_pf<W, 12><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
-                                                                ctr, stats, RC, rcnt);
+        with_kt<W>(p.K, [&](auto kt) { k_part_build_pf<W, 12, decltype(kt)::value><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
+                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap, ctr,
-                                                         stats, RC, rcnt);
+                                                         stats, RC, rcnt, B.headrec, hcap, smax);
+    if (prof) {
+        unsigned long long v[8];
+        (void)hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_build_prof), sizeof v, 0, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        fprintf(stderr, "build_prof (s_memtime, summed over blocks): slice-init %llu insert %llu link %llu "
+                        "heads %llu walk+rec %llu write %llu\n", v[0], v[1], v[2], v[3], v[4], v[5]);
+    }
 }
 
 template <int W>
@@ -380,7 +592,9 @@ __global__ __launch_bounds__(PB) void k_insert_overflow(KParams p, const uint64_
     const uint64_t m = min((uint64_t)ctr[CT_OVF], ovf_cap);
     for (uint64_t i = (uint64_t)blockIdx.x * PB + threadIdx.x; i < m; i += (uint64_t)gridDim.x * PB) {
         const uint64_t w0 = ovf[i * W], w1 = (W == 2) ? ovf[i * W + 1] : 0;
-        insert_one<W>(slot_key(w0, w1, p), slot_ext(w0), p, slots, cap, stats);
+        // overflow words come from the partition passes: their j* gives the placement hash
+        insert_one<W>(slot_key(w0, w1, p), slot_clean(w0, p), home_of(word_place(w0, w1, p), cap, p), p, slots, cap,
+                      stats);
     }
 }
 
@@ -524,12 +738,13 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
 }
 
 // pass 1 on words: bucket = top 9 hash bits, S1 windows per bucket (window blockIdx % S1)
-template <int W, int TB, bool COLLECT, int TILE>
-__global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restrict__ words, uint64_t n,
+template <int W, int TB, bool COLLECT, int TILE, int KT>
+__global__ __launch_bounds__(TB) void k_win1(KParams p_in, const uint64_t* __restrict__ words, uint64_t n,
                                              uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1, uint64_t* ovf,
                                              uint64_t ovf_cap, unsigned long long* ctr,
-                                             unsigned long long* stats, uint64_t* splits = nullptr,
-                                             uint64_t splits_cap = 0) {
+                                             unsigned long long* stats, uint64_t* splits, uint64_t splits_cap,
+                                             int jstar_in) {
+    const KParams p = specialize<KT>(p_in);
     constexpr int IPT = TILE / TB;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
@@ -555,10 +770,14 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
         uint32_t bin[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
-            const uint64_t h = words_hash<W>(a[j], b[j], p);
-            bin[j] = (uint32_t)(h >> (64 - B1));
+            // minimizer -> region (bucket = its top B1 bits); the word carries j* onward
+            const Key kk = slot_key(a[j], b[j], p);
+            // words of k_part1_convert carry j*; routed words do not
+            const uint32_t mn = jstar_in ? slot_jstar(a[j]) : mini_scan(kk, p);
+            bin[j] = mini_region(mini_window(kk, mn, p), p) >> (p.rbits - B1);
+            const bool live = a[j] != EMPTY;
             // splitter k-mers this shard owns (they head migrating-walk segments, kh_mseg.hip)
-            if (COLLECT && a[j] != EMPTY && ext_bwd(slot_ext(a[j])) != EXT_F && is_splitter(h, p)) {
+            if (COLLECT && live && ext_bwd(slot_ext(a[j])) != EXT_F && is_splitter(key_hash32(kk), p)) {
                 const uint32_t pos = atomicAdd(scount, 1u);
                 if (pos < WIN_SPLIT_LCAP) {
                     sbuf[pos * W] = a[j];
@@ -571,6 +790,7 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p, const uint64_t* __restri
                     }
                 }
             }
+            if (live && !jstar_in) a[j] = part_word0(slot_clean(a[j], p), mn, p);
         }
         const uint64_t nbase = base + TILE;
         sort_reserve_write<W, TB, NB1, TILE>(
@@ -677,20 +897,20 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __res
                 const uint32_t sh = (o & 7u) * 8u;
                 if (valid) parse_record_regs_t<PK>(funnel64(w0, w1, sh), funnel64(w1, w2, sh), p.pad, k, ext);
             }
-            const uint64_t hk = key_hash(k);
+            const uint32_t mn = mini_scan(k, p);
             if (s0 < n) {  // uniform: one start / splitter word per 64 consecutive records
                 const bool is_start = valid && ext_bwd(ext) == EXT_F;
                 const uint64_t bal = __ballot(is_start);
-                const uint64_t sb = __ballot(valid && !is_start && is_splitter(hk, p));
+                const uint64_t sb = split_mask ? __ballot(valid && !is_start && is_splitter(key_hash32(k), p)) : 0;
                 const uint64_t wb = s0 + (threadIdx.x & ~63u);
                 if ((threadIdx.x & 63) == 0 && wb < n) {
                     if (start_mask) start_mask[wb >> 6] = bal;
                     if (split_mask) split_mask[wb >> 6] = sb;
                 }
             }
-            a[j] = valid ? slot_w0(k, ext, p) : EMPTY;
+            a[j] = valid ? part_word0(slot_w0(k, ext, p), mn, p) : EMPTY;
             b[j] = (valid && W == 2) ? k.lo : 0;
-            bin[j] = (uint32_t)(hk >> (64 - B1));
+            bin[j] = mini_region(mini_window(k, mn, p), p) >> (p.rbits - B1);
         }
         const uint64_t nt = t + gridDim.x, nbase = nt * TILE;
         sort_reserve_write<W, TB, NB1, TILE>(
@@ -702,12 +922,13 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __res
 }
 
 // pass 2: next 8 hash bits within bucket bk, into the region windows (RC words each)
-template <int W, int TB, int TILE>
-__global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restrict__ buf1, uint64_t G,
+template <int W, int TB, int TILE, int KT>
+__global__ __launch_bounds__(TB) void k_win2(KParams p_in, const uint64_t* __restrict__ buf1, uint64_t G,
                                              uint32_t RC, uint32_t* rcnt,
                                              uint64_t* buf2, uint64_t* ovf, uint64_t ovf_cap,
                                              unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
                                              const uint32_t* wcnt) {
+    const KParams p = specialize<KT>(p_in);
     constexpr int IPT = TILE / TB;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
@@ -717,6 +938,7 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restri
     uint32_t* gpos = start + NB1;
     __shared__ uint32_t wsum[TB / 64];  // static: one block per CU (see k_win1)
     const uint32_t bk = blockIdx.x / (uint32_t)G, g = blockIdx.x % (uint32_t)G;
+    const uint32_t b2 = (uint32_t)(p.rbits - B1);  // pass-2 bits: regions per bucket = 2^b2
     // the bucket's S1 pass-1 windows read as one virtual range [0, e)
     uint32_t pre[S1 + 1];
     pre[0] = 0;
@@ -732,11 +954,11 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p, const uint64_t* __restri
         uint32_t bin[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
-            bin[j] = (uint32_t)(words_hash<W>(a[j], b[j], p) >> (64 - RBITS)) & (NB2 - 1);
+            bin[j] = mini_region(word_mini_window(a[j], b[j], p), p) & ((1u << b2) - 1u);
         sort_reserve_write<W, TB, NB2, TILE>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
-            [&](uint32_t q) { return &rcnt[(bk << B2) | q]; },
-            [&](uint32_t q) { return (uint64_t)((bk << B2) | q) * RC; }, RC, buf2, ovf, ovf_cap, ctr, stats,
+            [&](uint32_t q) { return &rcnt[(bk << b2) | q]; },
+            [&](uint32_t q) { return (uint64_t)((bk << b2) | q) * RC; }, RC, buf2, ovf, ovf_cap, ctr, stats,
             [&]() { load(t + G * TILE); });
     }
 }
@@ -753,19 +975,24 @@ static constexpr size_t WIN_LDS = sort_lds(WIN_TILE);
 template <int W>
 static hipError_t win1_launch(const KParams& p, const uint64_t* words, uint64_t n, uint32_t CAP1, uint32_t* wcnt,
                               const PartBuffers& B, uint64_t ovf_cap, unsigned long long* ctr,
-                              unsigned long long* stats, hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap) {
+                              unsigned long long* stats, hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap,
+                              bool jstar_in = false) {
     const unsigned nb = (unsigned)win_blocks1(n);
-    hipError_t e;
-    if (wsplits) {
-        if ((e = allow_lds(k_win1<W, 512, true, WIN_TILE>, WIN_LDS)) != hipSuccess) return e;
-        k_win1<W, 512, true, WIN_TILE><<<nb, 512, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow, ovf_cap,
-                                                                ctr, stats, wsplits, wsplits_cap);
-    } else {
-        if ((e = allow_lds(k_win1<W, 512, false, WIN_TILE>, WIN_LDS)) != hipSuccess) return e;
-        k_win1<W, 512, false, WIN_TILE><<<nb, 512, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
-                                                                 ovf_cap, ctr, stats);
-    }
-    return hipSuccess;
+    const int ji = (jstar_in && p.chain) ? 1 : 0;
+    return with_kt<W>(p.K, [&](auto kt) {
+        constexpr int KT = decltype(kt)::value;
+        hipError_t e;
+        if (wsplits) {
+            if ((e = allow_lds(k_win1<W, 512, true, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
+            k_win1<W, 512, true, WIN_TILE, KT><<<nb, 512, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
+                                                                        ovf_cap, ctr, stats, wsplits, wsplits_cap, ji);
+        } else {
+            if ((e = allow_lds(k_win1<W, 512, false, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
+            k_win1<W, 512, false, WIN_TILE, KT><<<nb, 512, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
+                                                                         ovf_cap, ctr, stats, nullptr, 0, ji);
+        }
+        return hipSuccess;
+    });
 }
 
 
@@ -794,22 +1021,32 @@ static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n
                               uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
                               const uint32_t* wcnt, hipStream_t s) {
     const uint64_t G = win_G(n);
-    hipError_t e;
-    if ((e = allow_lds(k_win2<W, 512, WIN_TILE>, WIN_LDS)) != hipSuccess) return e;
-    k_win2<W, 512, WIN_TILE><<<(unsigned)(NB1 * G), 512, WIN_LDS, s>>>(p, B.buf1, G, RC, rcnt, B.buf2, B.overflow,
-                                                                      ovf_cap, ctr, stats, CAP1, wcnt);
-    return hipSuccess;
+    return with_kt<W>(p.K, [&](auto kt) {
+        constexpr int KT = decltype(kt)::value;
+        hipError_t e;
+        if ((e = allow_lds(k_win2<W, 512, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
+        k_win2<W, 512, WIN_TILE, KT><<<(unsigned)(NB1 * G), 512, WIN_LDS, s>>>(p, B.buf1, G, RC, rcnt, B.buf2,
+                                                                              B.overflow, ovf_cap, ctr, stats, CAP1,
+                                                                              wcnt);
+        return hipSuccess;
+    });
 }
 
 template <int W>
 static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bool table_empty, const PartBuffers& B,
                                unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
     hipError_t e;
-    const size_t lds = (size_t)region_max_slots(t.cap) * W * 8;
+    const size_t lds = (size_t)build_lds(p, t.cap, B.headrec && B.hcap);
     if ((e = allow_lds(k_part_build<W>, lds)) != hipSuccess) return e;
-    if ((e = allow_lds(k_part_build_pf<W, 4>, lds)) != hipSuccess) return e;
-    if ((e = allow_lds(k_part_build_pf<W, 12>, lds)) != hipSuccess) return e;
-    const uint32_t RC = part_region_cap(total);
+    if ((e = with_kt<W>(p.K, [&](auto kt) {
+             constexpr int KT = decltype(kt)::value;
+             hipError_t x;
+             if ((x = allow_lds(k_part_build_pf<W, 4, KT>, lds)) != hipSuccess) return x;
+             if ((x = allow_lds(k_part_build_pf<W, 6, KT>, lds)) != hipSuccess) return x;
+             return allow_lds(k_part_build_pf<W, 12, KT>, lds);
+         })) != hipSuccess)
+        return e;
+    const uint32_t RC = part_region_cap(p, total);
     launch_build_windows<W>(p, B, t, table_empty, part_overflow_cap(total), ctr, stats, RC,
                             reinterpret_cast<const uint32_t*>(B.rcnt), lds, s);
     k_insert_overflow<W><<<1024, PB, 0, s>>>(p, B.overflow, part_overflow_cap(total), ctr, t.slots, t.cap, stats);
@@ -825,13 +1062,13 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
                               uint64_t wsplits_cap = 0) {
     hipError_t e;
     const uint64_t ovf_cap = part_overflow_cap(n);
-    const uint32_t CAP1 = part_win1_cap(n), RC = part_region_cap(n);
+    const uint32_t CAP1 = part_win1_cap(n), RC = part_region_cap(p, n);
     uint32_t* wcnt = B.wcnt;
     uint32_t* rcnt = B.rcnt;
     if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(rcnt, 0, (size_t)NREG * 4, s)) != hipSuccess) return e;
-    const bool rec_pass = REC && ((p.P == 13 && W == 2) || (p.P == 5 && W == 1));
+    if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
+    const bool rec_pass = REC && ((p.P == 13 && W == 2) || (p.P == 5 && W == 1)) && debug_flag("p1rec");
     if (rec_pass) {
         if ((e = win1_rec_launch<W>(p, recs, n, CAP1, wcnt, B, start_mask, split_mask, ovf_cap, ctr, stats, s)) !=
             hipSuccess)
@@ -839,11 +1076,20 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     } else {
         if (REC) {  // records -> words (input order) in buf2, which pass 2 only writes after pass 1
             const unsigned nb = (unsigned)((n + (uint64_t)T1 * PART_TILE - 1) / ((uint64_t)T1 * PART_TILE));
-            k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+            if (W == 2 && p.K == 51)  // compile-time shape: aligned 8-B LDS reads, constant masks
+                k_part1_convert<W, 13, 51><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+            else if (W == 1 && p.K == 19)
+                k_part1_convert<W, 5, 19><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+            else if (p.P == 13)
+                k_part1_convert<W, 13><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+            else if (p.P == 5)
+                k_part1_convert<W, 5><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+            else
+                k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
             words = B.buf2;
         }
         if ((e = win1_launch<W>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, REC ? nullptr : wsplits,
-                                wsplits_cap)) != hipSuccess)
+                                wsplits_cap, REC)) != hipSuccess)
             return e;
     }
     // start / splitter bits are complete: the caller's compaction may start
@@ -862,10 +1108,10 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     hipError_t e;
     if (first) {
         if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(B.rcnt, 0, (size_t)NREG * 4, s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
     }
     if (m == 0) return hipSuccess;
-    const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(total);
+    const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(p, total);
     if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = win1_launch<W>(p, words, m, CAP1, B.wcnt, B, part_overflow_cap(total), ctr, stats, s, wsplits,
                             wsplits_cap)) != hipSuccess)

@@ -98,6 +98,8 @@ struct kh_table {
     DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text;
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
+    DevBuf headrec;                           // chain head records (region build -> walker)
+    uint32_t hcap = 0;                        // head records per region (0 = no chains)
     bool last_insert_part = false;
     bool staging = false, stage_part = false, stage_fresh = false;  // kh_insert_words_stage_dev build
     uint64_t stage_total = 0, stage_n = 0;
@@ -221,6 +223,12 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     b.wcnt = t->pb_cnt.as<uint32_t>();
     b.rcnt = b.wcnt + kh::PART_W1_COUNTERS;
     b.overflow = t->pb_ovf.as<uint64_t>();
+    // chain head records: sized by the table (regions x records per region), kept across builds
+    const uint32_t hcap = kh::debug_flag("no_chains") ? 0u : kh::part_head_cap(t->kp, t->cap);
+    if (hcap && (rc = t->headrec.ensure((uint64_t)hcap * (1ull << t->kp.rbits) * 16))) return rc;
+    t->hcap = hcap;
+    b.headrec = hcap ? t->headrec.as<uint64_t>() : nullptr;
+    b.hcap = hcap;
     return KH_OK;
 }
 
@@ -240,6 +248,7 @@ void size_table(kh_table* t, uint64_t n_kmers) {
     t->cap = (uint64_t)c;
     if ((double)t->cap < c) t->cap++;
     if (t->cap < 2) t->cap = 2;
+    kh::set_region_bits(t->kp, t->cap);
 }
 
 }  // namespace
@@ -316,7 +325,7 @@ int kh_destroy(kh_table* t) {
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
-                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf};
+                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec};
     for (auto* b : bufs) b->release();
     if (t->side) (void)hipStreamSynchronize(t->side);
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_conv,
@@ -564,6 +573,8 @@ int kh_assemble_dev(kh_table* t) {
     wb.chunk_seq = t->chunk_seq.as<uint32_t>();
     wb.chunk_cap = chunk_cap;
     wb.max_steps = n;
+    wb.headrec = t->headrec.as<uint64_t>();
+    wb.hcap = t->headrec.p ? t->hcap : 0u;
     kh::SegBuffers sb{};
     if (kp.split_bits) {
         // walkers may stop before a splitter k-mer even when none was collected (then the link

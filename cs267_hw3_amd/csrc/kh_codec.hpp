@@ -20,6 +20,10 @@
 //   ext = bwd_code | fwd_code << 3, codes A0 C1 G2 T3 F4, 5 = not an A/C/G/T/F byte.
 //   Live slots never hold all-ones words (ext <= 45 < 63 and lo < 2^62), so all-ones is the
 //   EMPTY sentinel for both words.
+//   Bits of word0 above the key (when the K leaves room, KParams::chain): bits 58-63 = the
+//   minimizer window j* (set by the partition passes, see place_hash), bits [idx_lo, 57) = the
+//   chain head-record index + 1 (set by the region build, 0 = none), bit 57 = scratch of the build.
+//   Every key comparison masks them (slot_keybits).
 #pragma once
 #include <stdint.h>
 
@@ -47,16 +51,28 @@ struct KParams {
     int W;          // slot words (1 or 2)
     uint64_t hi_mask;   // mask for hi after a shift (2K-62 bits, 0 when K <= 31)
     uint64_t v_mask;    // W=1: mask of V (2K bits)
-    int M;              // minimizer length (bases) of the sharded owner function
+    int M;              // minimizer length (bases): placement region and sharded owner
     int owner_mode;     // sharded owner: 0 = minimizer hash (default), 1 = low key_hash bits
-    int split_bits;     // walk splitters: k-mers with (key_hash & (2^split_bits - 1)) == 0 and a
+    int split_bits;     // walk splitters: k-mers with (key_hash32 & (2^split_bits - 1)) == 0 and a
                         // predecessor start extra walkers (0 = off); see kh_kernels.hip k_walk
+    uint64_t kmask;     // key bits of (word0 >> 6): hi_mask (W=2) or v_mask (W=1)
+    int chain;          // word0 has room for j* and a head-record index (chain links, kh_build.hip)
+    int idx_lo;         // first bit of the head-record index field in word0 (field = [idx_lo, 57))
+    int rbits;          // placement regions = 2^rbits (9..17, by table size: set_region_bits)
 };
 
-// Minimizer length for owner_key: consecutive k-mers of a contig share their minimizer for
-// ~(K-M+2)/2 steps on random sequence, so a walk stays on one rank for that long; 4^M distinct
-// values keep the shards balanced.
-inline int minimizer_len(int K) { return K >= 31 ? 15 : K >= 20 ? 12 : K >= 10 ? 10 : K; }
+// Minimizer length: consecutive k-mers of a contig share their minimizer for ~(K-M+2)/2 steps on
+// random sequence (K=51, M=16: 18.6 k-mers), so a contig's k-mers come in runs that share a
+// placement region (and a rank). M must make minimizer *windows* rare in the data: a region's
+// load is a sum over the minimizer windows mapped to it, and a window that recurs (a 12-mer
+// occurs ~18x in C3's 296M bases) brings all its runs along: C3 region loads (mean 1526 per
+// 3052-slot slice) have sd 642 and spill 0.8M keys at M=12, sd 210 and none at M=16
+// (simulated at full size).
+inline int minimizer_len(int K) { return K >= 31 ? 16 : K >= 20 ? 14 : K >= 14 ? 12 : K; }
+static constexpr int JSTAR_SHIFT = 58;   // word0 bits 58-63: minimizer window index j*
+static constexpr int SCRATCH_BIT = 57;   // word0 bit 57: build scratch (has a local predecessor)
+static constexpr int REGION_BITS_MIN = 9, REGION_BITS_MAX = 17;  // placement regions: 2^rbits
+static constexpr uint64_t REGION_SLOTS = 3072;  // target slots per region (one LDS slice)
 
 inline KParams make_params(int K) {
     KParams p;
@@ -71,7 +87,46 @@ inline KParams make_params(int K) {
     p.M = minimizer_len(K);
     p.split_bits = 0;
     p.owner_mode = 0;
+    p.kmask = p.W == 2 ? p.hi_mask : p.v_mask;
+    p.idx_lo = 6 + (p.W == 2 ? (hib > 0 ? hib : 0) : 2 * K);
+    // chain links need j* (6 bits, K-M+1 <= 49 windows) and an index field of >= 8 bits
+    p.chain = (SCRATCH_BIT - p.idx_lo >= 8) && K >= 14 ? 1 : 0;
+    p.rbits = REGION_BITS_MAX;
     return p;
+}
+
+// Compile-time copy of the shape fields for the bench shapes (KT = 51 or 19; 0 = as given):
+// kernels templated on KT call the codec through this copy, so K, W, masks and field positions
+// fold into constants (runtime fields: split_bits, rbits, owner_mode).
+template <int KT>
+KH_HD KParams specialize(const KParams& p) {
+    if constexpr (KT == 0) {
+        return p;
+    } else {
+        KParams q = p;
+        q.K = KT;
+        q.P = (KT + 3) / 4;
+        q.R = q.P + 2;
+        q.pad = 4 * q.P - KT;
+        q.W = KT <= KMAX_W1 ? 1 : 2;
+        q.hi_mask = 2 * KT - 62 > 0 ? ((1ull << (2 * KT - 62)) - 1) : 0ull;
+        q.v_mask = 2 * KT >= 64 ? ~0ull : ((1ull << (2 * KT)) - 1);
+        q.M = KT >= 31 ? 16 : KT >= 20 ? 14 : KT >= 14 ? 12 : KT;
+        q.kmask = q.W == 2 ? q.hi_mask : q.v_mask;
+        q.idx_lo = 6 + (q.W == 2 ? (2 * KT - 62 > 0 ? 2 * KT - 62 : 0) : 2 * KT);
+        q.chain = (57 - q.idx_lo >= 8) && KT >= 14 ? 1 : 0;
+        return q;
+    }
+}
+// the specialization a table's K gets (0 = generic)
+inline int kt_of(int K) { return K == 51 ? 51 : K == 19 ? 19 : 0; }
+
+// Regions of ~REGION_SLOTS slots: a region's load is a sum of minimizer runs (~20 k-mers), so
+// small slices would overflow (at 38 slots per region a quarter of the keys did); 2^9..2^17.
+inline void set_region_bits(KParams& p, uint64_t cap) {
+    int b = REGION_BITS_MIN;
+    while (b < REGION_BITS_MAX && (cap >> b) > REGION_SLOTS) ++b;
+    p.rbits = b;
 }
 
 KH_HD uint32_t base_code(uint8_t c) {
@@ -178,27 +233,118 @@ KH_HD uint32_t mix32(uint32_t x) {
     return x;
 }
 
-// Owner rank of a k-mer in the sharded table: a hash of its minimizer (the M-mer of smallest
-// mix32 value among its K-M+1 windows), not of the whole key. Placement never changes the
-// output (the reference's owner is std::hash<string> % P, hash_map.hpp:28-30); this one keeps
-// runs of consecutive k-mers on one rank so a walker migrates only at minimizer changes.
+// 32-bit key hash (3 x mix32): the in-region home slot and the splitter test. Cheaper than
+// key_hash's two 64-bit fmix rounds; placement never changes outputs.
+KH_HD uint32_t key_hash32(Key k) {
+    uint32_t h = (uint32_t)k.lo * 0x9E3779B1u + (uint32_t)(k.lo >> 32);
+    h = (h ^ (h >> 15)) * 0x85EBCA77u + ((uint32_t)k.hi ^ (uint32_t)(k.hi >> 32));
+    h = (h ^ (h >> 13)) * 0xC2B2AE3Du;
+    return h ^ (h >> 16);
+}
+
+// ---- minimizer ---------------------------------------------------------------------------------
+// Window j (0 = the last M bases, K-M = the first M) = bits [2j, 2j + 2M) of V. Its order key is
+// (w[23:0] * C + (w >> 8)) mod 2^32 (one v_mad_u32_u24), top 26 bits; the minimizer is the
+// window of smallest order, ties to the smallest j (j*). Packed result: order26 << 6 | j*. The
+// region and the owner rank hash the minimizer window's *content* (2M bits), never its order
+// (26 bits: distinct windows share values).
+static constexpr uint32_t MINI_C = 0x9E3779u;
+KH_HD uint32_t win_order(uint32_t w) { return ((w & 0xFFFFFFu) * MINI_C + (w >> 8)) >> 6; }
+
+KH_HD uint32_t win_bits(Key k, int j, const KParams& p) {
+    const int b = 2 * j;  // V = hi * 2^62 + lo
+    const uint64_t t = b < 62 ? (k.lo >> b) | (k.hi << (62 - b)) : k.hi >> (b - 62);
+    return (uint32_t)t & (uint32_t)((1ull << (2 * p.M)) - 1);
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// V as four 32-bit words; every window is one alignbit at a constant shift (unrolled). K and M
+// known at compile time (the bench shapes) drop the per-window bounds branch and mask.
+template <int K, int M>
+__device__ __forceinline__ uint32_t mini_scan_t(Key k) {
+    const uint32_t v[5] = {(uint32_t)k.lo, (uint32_t)(k.lo >> 32) | (uint32_t)(k.hi << 30), (uint32_t)(k.hi >> 2),
+                           (uint32_t)(k.hi >> 34), 0u};
+    constexpr uint32_t mmask = (uint32_t)((1ull << (2 * M)) - 1);
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j <= K - M; ++j) {
+        const int b = 2 * j;
+        const uint32_t w = (b & 31) ? __builtin_amdgcn_alignbit(v[(b >> 5) + 1], v[b >> 5], b & 31) : v[b >> 5];
+        const uint32_t o = (win_order(w & mmask) << 6) | (uint32_t)j;
+        best = o < best ? o : best;
+    }
+    return best;
+}
+#endif
+
+KH_HD uint32_t mini_scan(Key k, const KParams& p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (p.K == 51 && p.M == 16) return mini_scan_t<51, 16>(k);  // uniform branches
+    if (p.K == 19 && p.M == 12) return mini_scan_t<19, 12>(k);
+    const uint32_t v[5] = {(uint32_t)k.lo, (uint32_t)(k.lo >> 32) | (uint32_t)(k.hi << 30), (uint32_t)(k.hi >> 2),
+                           (uint32_t)(k.hi >> 34), 0u};
+    const uint32_t mmask = (uint32_t)((1ull << (2 * p.M)) - 1);
+    const int last = p.K - p.M;
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j <= KMAX - 1; ++j) {
+        if (j <= last) {
+            const int b = 2 * j;
+            const uint32_t w = (b & 31) ? __builtin_amdgcn_alignbit(v[(b >> 5) + 1], v[b >> 5], b & 31) : v[b >> 5];
+            const uint32_t o = (win_order(w & mmask) << 6) | (uint32_t)j;
+            best = o < best ? o : best;
+        }
+    }
+    return best;
+#else
+    uint32_t best = 0xFFFFFFFFu;
+    for (int j = 0; j <= p.K - p.M; ++j) {
+        const uint32_t o = (win_order(win_bits(k, j, p)) << 6) | (uint32_t)j;
+        best = o < best ? o : best;
+    }
+    return best;
+#endif
+}
+// content of the minimizer window of k (mn = mini_scan(k))
+KH_HD uint32_t mini_window(Key k, uint32_t mn, const KParams& p) { return win_bits(k, (int)(mn & 63u), p); }
+
+// Region of a minimizer window (rbits bits of a mix of its content).
+KH_HD uint32_t mini_region(uint32_t win, const KParams& p) { return mix32(win ^ 0x5bd1e995u) >> (32 - p.rbits); }
+
+// Placement: the k-mer's region is a hash of its minimizer window; region r owns the slot range
+// [region_lo(r), region_lo(r + 1)) (2^rbits equal ranges of the cap slots), and the home slot is
+// region_lo(r) + the region length scaled by the 32-bit key hash. A run of consecutive k-mers of
+// a contig (same minimizer) lands in one region: the region build links them into chains
+// (kh_build.hip) that the walker crosses in one step.
+KH_HD uint64_t region_lo(uint32_t r, uint64_t cap, const KParams& p) {
+    return (r >> p.rbits) ? cap : mulhi64((uint64_t)r << (64 - p.rbits), cap);
+}
+KH_HD uint64_t home_in(uint64_t lo, uint64_t hi, uint32_t h) { return lo + (((hi - lo) * (uint64_t)h) >> 32); }
+struct Place {
+    uint32_t r, h;  // region, key_hash32
+};
+KH_HD Place place_w(uint32_t win, Key k, const KParams& p) { return Place{mini_region(win, p), key_hash32(k)}; }
+KH_HD Place place(Key k, const KParams& p) { return place_w(mini_window(k, mini_scan(k, p), p), k, p); }
+KH_HD uint64_t home_of(Place pl, uint64_t cap, const KParams& p) {
+    return home_in(region_lo(pl.r, cap, p), region_lo(pl.r + 1, cap, p), pl.h);
+}
+
+// Owner rank of a k-mer in the sharded table: a hash of its minimizer, not of the whole key.
+// Placement never changes the output (the reference's owner is std::hash<string> % P,
+// hash_map.hpp:28-30); this one keeps runs of consecutive k-mers on one rank so a walker migrates
+// only at minimizer changes, and a chain (same minimizer) never crosses ranks.
+KH_HD uint32_t owner_of_mini(uint32_t win, uint32_t nranks) {
+    return (uint32_t)(((uint64_t)mix32(win ^ 0x9e3779b9u) * nranks) >> 32);
+}
 KH_HD uint32_t owner_key(Key k, const KParams& p, uint32_t nranks) {
     if (nranks == 1) return 0;
     if (p.owner_mode == 1)  // SURVEY §8(e) proposal: hash bits independent of the home slot's
         return (uint32_t)(((key_hash(k) & 0xffffffffull) * nranks) >> 32);
-    const uint32_t mask = (uint32_t)((1ull << (2 * p.M)) - 1);
-    uint64_t lo = k.lo, hi = k.hi;  // V = hi * 2^62 + lo; windows from the last M bases upward
-    uint32_t best = 0xffffffffu;
-    for (int j = 0; j <= p.K - p.M; ++j) {
-        const uint32_t h = mix32(((uint32_t)lo & mask) ^ 0x5bd1e995u);
-        best = h < best ? h : best;
-        lo = (lo >> 2) | ((hi & 3u) << 60);
-        hi >>= 2;
-    }
-    return (uint32_t)(((uint64_t)mix32(best ^ 0x9e3779b9u) * nranks) >> 32);
+    return owner_of_mini(mini_window(k, mini_scan(k, p), p), nranks);
 }
 
 // Splitter k-mer: cuts long contigs into independently walked segments (sparse ruling set).
+// h = key_hash32 of the k-mer.
 KH_HD bool is_splitter(uint64_t h, const KParams& p) {
     return p.split_bits && (h & ((1ull << p.split_bits) - 1)) == 0;
 }
@@ -209,16 +355,52 @@ KH_HD uint64_t slot_w0(Key k, uint32_t ext, const KParams& p) {
 }
 KH_HD uint64_t slot_w1(Key k) { return k.lo; }
 
+// key bits of word0 (the j* / head-index bits above the key masked off)
+KH_HD uint64_t slot_keybits(uint64_t w0, const KParams& p) { return (w0 >> 6) & p.kmask; }
+
 KH_HD Key slot_key(uint64_t w0, uint64_t w1, const KParams& p) {
     Key k;
     if (p.W == 1) {
         k.hi = 0;
-        k.lo = w0 >> 6;
+        k.lo = slot_keybits(w0, p);
     } else {
-        k.hi = w0 >> 6;
+        k.hi = slot_keybits(w0, p);
         k.lo = w1;
     }
     return k;
+}
+// j* carried by a word of the partition passes
+KH_HD uint32_t slot_jstar(uint64_t w0) { return (uint32_t)(w0 >> JSTAR_SHIFT); }
+KH_HD uint64_t with_jstar(uint64_t w0, uint32_t j) {
+    return (w0 & ((1ull << JSTAR_SHIFT) - 1)) | ((uint64_t)j << JSTAR_SHIFT);
+}
+// head-record index + 1 of a built slot (0 = the walker steps this k-mer itself)
+KH_HD uint32_t slot_hidx(uint64_t w0, const KParams& p) {
+    return (uint32_t)((w0 >> p.idx_lo) & ((1ull << (SCRATCH_BIT - p.idx_lo)) - 1));
+}
+KH_HD uint64_t with_hidx(uint64_t w0, uint32_t v, const KParams& p) {
+    const uint64_t f = ((1ull << (SCRATCH_BIT - p.idx_lo)) - 1) << p.idx_lo;
+    return (w0 & ~f) | (((uint64_t)v << p.idx_lo) & f);
+}
+// key + ext + j* only (head index and scratch cleared)
+KH_HD uint64_t slot_clean(uint64_t w0, const KParams& p) {
+    return p.chain ? (w0 & (((1ull << p.idx_lo) - 1) | (63ull << JSTAR_SHIFT))) : w0;
+}
+// minimizer window / placement of a partition word: from its j* when the word carries one
+KH_HD uint32_t word_mini_window(uint64_t w0, uint64_t w1, const KParams& p) {
+    const Key k = slot_key(w0, w1, p);
+    return win_bits(k, p.chain ? (int)slot_jstar(w0) : (int)(mini_scan(k, p) & 63u), p);
+}
+KH_HD Place word_place(uint64_t w0, uint64_t w1, const KParams& p) {
+    return place_w(word_mini_window(w0, w1, p), slot_key(w0, w1, p), p);
+}
+// Partition words also carry the top bits of their minimizer order in the (then unused)
+// head-index field, so the region build's link test needs no window extraction.
+KH_HD int mtop_bits(const KParams& p) { return SCRATCH_BIT - p.idx_lo < 26 ? SCRATCH_BIT - p.idx_lo : 26; }
+KH_HD uint32_t order_top(uint32_t order26, const KParams& p) { return order26 >> (26 - mtop_bits(p)); }
+// word0 of a partition word: key + ext, j* and the minimizer order's top bits (chains only)
+KH_HD uint64_t part_word0(uint64_t w0, uint32_t mn, const KParams& p) {
+    return p.chain ? with_hidx(with_jstar(w0, mn & 63u), order_top(mn >> 6, p), p) : w0;
 }
 KH_HD uint32_t slot_ext(uint64_t w0) { return (uint32_t)(w0 & 63u); }
 KH_HD uint32_t ext_bwd(uint32_t ext) { return ext & 7u; }

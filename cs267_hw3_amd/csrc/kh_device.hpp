@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kh_codec.hpp"
 #include "kh_kernels.hpp"
 
@@ -13,6 +15,17 @@ static constexpr int SCAN_ITEMS = 8;
 static constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;  // 2048 elements per block
 static constexpr int WALK_GRAB = 64;                   // start k-mers per work-queue pull
 static constexpr int MAX_R = 17;                       // K <= 60 -> PACKED <= 15 -> R <= 17
+
+// Launch-side dispatch to the compile-time shape (specialize<KT>): f(integral_constant<KT>).
+template <int W, class F>
+inline auto with_kt(int K, F&& f) {
+    if constexpr (W == 2) {
+        if (K == 51) return f(std::integral_constant<int, 51>{});
+    } else {
+        if (K == 19) return f(std::integral_constant<int, 19>{});
+    }
+    return f(std::integral_constant<int, 0>{});
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
@@ -225,13 +238,14 @@ __device__ __forceinline__ void load_slot_nt(const uint64_t* slots, uint64_t s, 
     }
 }
 
+// w0: the slot's word0 (may carry j*); home: its home slot (home_of)
 template <int W>
-__device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p, uint64_t* slots,
-                                           uint64_t cap, unsigned long long* stats) {
+__device__ __forceinline__ void insert_one(Key k, unsigned long long w0, uint64_t home, const KParams& p,
+                                           uint64_t* slots, uint64_t cap, unsigned long long* stats) {
     unsigned long long* S = reinterpret_cast<unsigned long long*>(slots);
-    const unsigned long long w0 = slot_w0(k, ext, p);
     const unsigned long long w1 = k.lo;
-    uint64_t s = home_slot(key_hash(k), cap);
+    const uint64_t want0 = slot_keybits(w0, p);
+    uint64_t s = home;
     uint64_t probes = 0;
     uint32_t spins = 0;
     uint64_t c0, c1;
@@ -247,7 +261,7 @@ __device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p
             c0 = old;
             c1 = EMPTY;  // unknown: re-read coherently below if needed
         }
-        if ((c0 >> 6) == (w0 >> 6)) {
+        if (slot_keybits(c0, p) == want0) {
             if (W == 1) {
                 atomicAdd(&stats[ST_DUP], 1ull);
                 return;
@@ -282,13 +296,13 @@ __device__ __forceinline__ void insert_one(Key k, uint32_t ext, const KParams& p
 template <int W>
 __device__ __forceinline__ bool probe(Key k, const KParams& p, const uint64_t* __restrict__ slots,
                                       uint64_t cap, uint64_t& w0_out) {
-    uint64_t s = home_slot(key_hash(k), cap);
+    uint64_t s = home_of(place(k, p), cap, p);
     const uint64_t want0 = (W == 1) ? k.lo : k.hi;
     for (uint64_t probes = 0; probes < cap; ++probes) {
         uint64_t w0, w1;
         load_slot<W>(slots, s, w0, w1);
         const bool empty = w0 == EMPTY;
-        const bool hit = !empty & ((w0 >> 6) == want0) & ((W == 1) | (w1 == k.lo));
+        const bool hit = !empty & (slot_keybits(w0, p) == want0) & ((W == 1) | (w1 == k.lo));
         if (hit | empty) {
             w0_out = w0;
             return hit;

@@ -47,12 +47,12 @@ __global__ __launch_bounds__(BLOCK) void k_insert(KParams p, const uint8_t* __re
         const uint64_t wbase = base + (threadIdx.x & ~63u);
         if ((threadIdx.x & 63) == 0 && wbase < n) start_mask[wbase >> 6] = bal;
         if (split_mask) {
-            const uint64_t sb = __ballot(valid && !is_start && is_splitter(key_hash(k), p));
+            const uint64_t sb = __ballot(valid && !is_start && is_splitter(key_hash32(k), p));
             if ((threadIdx.x & 63) == 0 && wbase < n) split_mask[wbase >> 6] = sb;
         }
         if (valid) {
             if (ext_bwd(ext) == EXT_BAD || ext_fwd(ext) == EXT_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
-            insert_one<W>(k, ext, p, slots, cap, stats);
+            insert_one<W>(k, slot_w0(k, ext, p), home_of(place(k, p), cap, p), p, slots, cap, stats);
         }
     }
 }
@@ -242,6 +242,52 @@ __device__ __forceinline__ void append_base(const LaneOut& o, uint64_t c, uint32
     ++steps;
 }
 
+// Append m <= 32 - (steps & 31) bases at once (piece: base i at bits 2i), same layout as append_base.
+__device__ __forceinline__ void append_run(const LaneOut& o, uint64_t c, uint64_t piece, uint32_t m, uint32_t& steps,
+                                           uint32_t& chunk, uint64_t& buf, unsigned long long* ctr,
+                                           unsigned long long* stats) {
+    if (steps == 0) {
+        chunk = (uint32_t)c;
+    } else if ((steps & (CHUNK_BASES - 1)) == 0) {
+        chunk = (uint32_t)(o.n_first + atomicAdd(&ctr[CT_CHUNK_NEXT], 1ull));
+        if (chunk < o.chunk_cap) {
+            o.chunk_owner[chunk] = (uint32_t)c;
+            o.chunk_seq[chunk] = steps / CHUNK_BASES;
+        } else {
+            atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+        }
+    }
+    buf |= piece << (2 * (steps & 31));
+    steps += m;
+    if ((steps & 31) == 0) {
+        if (chunk < o.chunk_cap) o.chunk_data[(uint64_t)chunk * CHUNK_WORDS + (((steps - 1) >> 5) & 7)] = buf;
+        buf = 0;
+    }
+}
+
+// bits [sh, sh + 64) of V = hi * 2^62 + lo
+__device__ __forceinline__ uint64_t key_bits64(Key k, uint32_t sh) {
+    return sh < 62 ? (k.lo >> sh) | (sh ? k.hi << (62 - sh) : k.hi << 62) : k.hi >> (sh - 62);
+}
+// reverse the order of the 32 2-bit groups of x
+__device__ __forceinline__ uint64_t rev2_64(uint64_t x) {
+    const uint64_t r = ((uint64_t)__builtin_bitreverse32((uint32_t)x) << 32) | __builtin_bitreverse32((uint32_t)(x >> 32));
+    return ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1);
+}
+// Append the last n bases of k (oldest first): the links of a chain record (kh_build.hip).
+__device__ __forceinline__ void append_key_tail(const LaneOut& o, uint64_t c, Key k, uint32_t n, uint32_t& steps,
+                                                uint32_t& chunk, uint64_t& buf, unsigned long long* ctr,
+                                                unsigned long long* stats) {
+    while (n) {
+        const uint32_t room = 32u - (steps & 31u);
+        const uint32_t m = n < room ? n : room;
+        const uint64_t x = key_bits64(k, 2 * (n - m));
+        const uint64_t piece = rev2_64(m >= 32 ? x : x & ((1ull << (2 * m)) - 1)) >> (64 - 2 * m);
+        append_run(o, c, piece, m, steps, chunk, buf, ctr, stats);
+        n -= m;
+    }
+}
+
 __device__ __forceinline__ void finish_contig(const LaneOut& o, uint64_t c, uint32_t steps, uint32_t chunk,
                                               uint64_t buf) {
     o.contig_len[c] = steps + 1;
@@ -262,6 +308,13 @@ __device__ __forceinline__ uint64_t walk_splits(const WalkBuffers& wb) {
 // line: tools/membench chase16 / chase64q / chase128o). All intra-quad exchange is DPP quad_perm
 // (ALU, no LDS): each walker's probe position and key are broadcast to its quad, and the hit
 // slot's extension comes back by a quad OR-reduction.
+//
+// Chains (kh_build.hip region_chains): a looked-up k-mer whose slot carries a head-record index
+// is the head of a run of k-mers that share its minimizer; the walker then reads the record
+// (one 16-B load) and appends the run's bases in one step — the record holds the run's last
+// k-mer (tail) whose low 2*links bits ARE those bases — and continues from the tail's extension.
+// A C3 contig (~104 k-mers) costs ~6 such hops of two dependent requests instead of ~104 lookups.
+// Every walker starts by looking up its own start k-mer (to find its record).
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
@@ -277,24 +330,38 @@ __device__ __forceinline__ uint32_t qor32(uint32_t v) {
     return v;
 }
 
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __restrict__ slots,
+static constexpr uint64_t WQ_REC = 1ull << 63;  // walker's next load is a head record (index below)
+static constexpr uint64_t WQ_IDLE = ~0ull;
+
+template <int W, int KT>
+__global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* __restrict__ slots,
                                                   uint64_t cap, WalkBuffers wb,
                                                   unsigned long long* ctr,
                                                   unsigned long long* stats) {
+    const KParams p = specialize<KT>(p_in);
     const uint32_t lane = lane_id();
     const uint32_t q = lane & 3, ql = lane & ~3u;
     const uint64_t n = wb.n_starts + walk_splits(wb);
     const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
+    const bool chains = p.chain && wb.hcap != 0;
     uint64_t bbase = 0;
     uint32_t bused = WALK_GRAB;
     bool bdry = false;
     uint64_t bw0 = 0, bw1 = 0;
 
     bool active = false, done = false, resolved = false;
+    bool entry = false;  // looking up the walker's own start k-mer (fwd = the start record's)
     uint64_t c = 0, s = 0, buf = 0;
+    uint32_t reg = 0;  // region of the k-mer being looked up (its head records live there)
     Key k{0, 0};
     uint32_t fwd = 0, steps = 0, chunk = 0;
+    // look up key k: s = its home slot (the hit may carry a head-record index)
+    auto lookup = [&]() {
+        const Place pl = place(k, p);
+        reg = pl.r;
+        s = home_of(pl, cap, p);
+        resolved = false;
+    };
     while (true) {
         while (true) {
             const bool need = !active && !done;
@@ -348,7 +415,11 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __r
                         steps = 0;
                         buf = 0;
                         active = true;
-                        resolved = true;
+                        entry = chains;
+                        if (chains)
+                            lookup();  // its own slot tells whether a record covers its run
+                        else
+                            resolved = true;
                     } else {
                         done = true;
                     }
@@ -366,20 +437,19 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __r
         if (active && resolved) {
             append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
             k = key_next(k, fwd, p);
-            const uint64_t h = key_hash(k);
-            if (is_splitter(h, p)) {
+            if (is_splitter(key_hash32(k), p)) {
                 finish_contig(o, c, steps, chunk, buf);
                 wb.seg_next[c] = SEG_AT_SPLIT;
                 wb.seg_key[2 * c] = k.hi;
                 wb.seg_key[2 * c + 1] = k.lo;
                 active = false;
             } else {
-                s = home_slot(h, cap);
-                resolved = false;
+                lookup();
             }
         }
-        // -- quad block probes: 4 loads per lane, one per quad member's block ------------------
-        const uint64_t sp = active ? s : ~0ull;  // ~0: inactive walker, no load
+        // -- quad loads: a probe reads 4 slots per lane, one per quad member's block; a record
+        //    read loads the same 16 B in all 4 lanes (one request) ------------------------------
+        const uint64_t sp = active ? s : WQ_IDLE;
         uint64_t sj[4], w0[4], w1[4];
         sj[0] = qbcast64<0>(sp);
         sj[1] = qbcast64<1>(sp);
@@ -387,11 +457,16 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __r
         sj[3] = qbcast64<3>(sp);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint64_t my = (sj[j] & ~3ull) + q;
             w0[j] = EMPTY;
             w1[j] = 0;
-            if (sj[j] != ~0ull && my < cap) {
-                load_slot_nt<W>(slots, my, w0[j], w1[j]);
+            if (sj[j] == WQ_IDLE) continue;
+            if (sj[j] & WQ_REC) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(wb.headrec + (sj[j] & ~WQ_REC) * 2);
+                w0[j] = v.x;
+                w1[j] = v.y;
+            } else {
+                const uint64_t my = (sj[j] & ~3ull) + q;
+                if (my < cap) load_slot_nt<W>(slots, my, w0[j], w1[j]);
             }
         }
         uint64_t kh_[4], kl_[4];
@@ -404,37 +479,68 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p, const uint64_t* __r
         kl_[2] = qbcast64<2>(k.lo);
         kl_[3] = qbcast64<3>(k.lo);
         uint32_t myfh = 4, myfe = 4, myext = 0;
+        uint64_t r0 = 0, r1 = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint64_t my = (sj[j] & ~3ull) + q;
-            const bool valid = sj[j] != ~0ull && my >= sj[j] && my < cap;
+            const bool probe_j = sj[j] != WQ_IDLE && !(sj[j] & WQ_REC);
+            const bool valid = probe_j && my >= sj[j] && my < cap;
             const bool empty = w0[j] == EMPTY;
-            const bool hit = !empty & ((w0[j] >> 6) == ((W == 1) ? kl_[j] : kh_[j])) &
+            const bool hit = !empty & (slot_keybits(w0[j], p) == ((W == 1) ? kl_[j] : kh_[j])) &
                              ((W == 1) | (w1[j] == kl_[j]));
             const uint32_t bh = (uint32_t)(__ballot(valid && hit) >> ql) & 0xFu;
             const uint32_t be = (uint32_t)(__ballot(valid && empty) >> ql) & 0xFu;
             const uint32_t fh = bh ? (uint32_t)__builtin_ctz(bh) : 4u;
             const uint32_t fe = be ? (uint32_t)__builtin_ctz(be) : 4u;
-            const uint32_t ext = qor32(q == fh ? slot_ext(w0[j]) | 0x40u : 0u);
+            // hit slot: ext | found flag | head-record index << 7
+            const uint32_t ext =
+                qor32(q == fh ? (slot_ext(w0[j]) | 0x40u | ((chains ? slot_hidx(w0[j], p) : 0u) << 7)) : 0u);
             if (q == (uint32_t)j) {
                 myfh = fh;
                 myfe = fe;
                 myext = ext;
+                r0 = w0[j];
+                r1 = w1[j];
             }
         }
         if (active) {
-            if (myfh < myfe) {
-                fwd = ext_fwd(myext & 63u);
+            if (s & WQ_REC) {
+                // head record: jump to the run's tail, appending the bases of its links
+                k = slot_key(r0, r1, p);
+                fwd = ext_fwd(slot_ext(r0));
+                const uint32_t links = slot_hidx(r0, p);
+                append_key_tail(o, c, k, links, steps, chunk, buf, ctr, stats);
                 resolved = true;
                 if (steps > wb.max_steps) {
                     atomicAdd(&stats[ST_CYCLE], 1ull);
                     finish_contig(o, c, steps, chunk, buf);
                     active = false;
                 }
+            } else if (myfh < myfe) {
+                const uint32_t hidx = myext >> 7, tf = ext_fwd(myext & 63u);
+                // a start walks from its own record (kmer_hash.cpp:42-44): a record whose run
+                // begins with another extension (duplicate key) is not used for it
+                if (hidx && !(entry && tf != fwd)) {
+                    s = WQ_REC | ((uint64_t)reg * wb.hcap + hidx - 1);
+                } else {
+                    if (!entry) fwd = tf;
+                    resolved = true;
+                    if (steps > wb.max_steps) {
+                        atomicAdd(&stats[ST_CYCLE], 1ull);
+                        finish_contig(o, c, steps, chunk, buf);
+                        active = false;
+                    }
+                }
+                entry = false;
             } else if (myfe < 4u) {
-                atomicAdd(&stats[ST_MISSING], 1ull);
-                finish_contig(o, c, steps, chunk, buf);
-                active = false;
+                if (entry) {  // a start k-mer need not be in the table (kh_set_starts)
+                    resolved = true;
+                    entry = false;
+                } else {
+                    atomicAdd(&stats[ST_MISSING], 1ull);
+                    finish_contig(o, c, steps, chunk, buf);
+                    active = false;
+                }
             } else {
                 const uint64_t nx = (s & ~3ull) + 4;
                 s = nx >= cap ? 0 : nx;
@@ -452,9 +558,9 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
                                          (uint64_t)(grid_blocks > 0 ? grid_blocks : 2 * cu_count()));
     if (p.W == 1)
-        k_walk_q<1><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+        with_kt<1>(p.K, [&](auto kt) { k_walk_q<1, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); });
     else
-        k_walk_q<2><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats);
+        with_kt<2>(p.K, [&](auto kt) { k_walk_q<2, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); });
     return hipGetLastError();
 }
 
@@ -694,7 +800,7 @@ struct SplitKeepF {
     uint64_t mask;
     __device__ uint64_t operator()(uint64_t i) const {
         const uint64_t w0 = splits[i * p.W], w1 = p.W == 2 ? splits[i * p.W + 1] : 0;
-        return (key_hash(slot_key(w0, w1, p)) & mask) == 0;
+        return (key_hash32(slot_key(w0, w1, p)) & mask) == 0;
     }
 };
 
@@ -920,7 +1026,8 @@ __global__ __launch_bounds__(BLOCK) void k_insert_words(KParams p, const uint64_
         const uint64_t w1 = (W == 2) ? words[i * W + 1] : 0;
         const uint32_t ext = slot_ext(w0);
         if (ext_bwd(ext) == EXT_BAD || ext_fwd(ext) == EXT_BAD) atomicAdd(&stats[ST_BAD_EXT], 1ull);
-        insert_one<W>(slot_key(w0, w1, p), ext, p, slots, cap, stats);
+        const Key k = slot_key(w0, w1, p);  // routed words carry no j*: full placement hash
+        insert_one<W>(k, slot_w0(k, ext, p), home_of(place(k, p), cap, p), p, slots, cap, stats);
     }
 }
 

@@ -81,6 +81,9 @@ struct WalkBuffers {
     uint32_t* chunk_seq;      // chunk index within its contig
     uint64_t chunk_cap;
     uint64_t max_steps;
+    // chain head records of the last region build (kh_build.hip region_chains); hcap 0 = none
+    const uint64_t* headrec = nullptr;
+    uint32_t hcap = 0;
 };
 
 // Persistent per-lane walker (single GPU): every lane walks whole contigs, pulling start k-mers
@@ -234,7 +237,7 @@ hipError_t launch_insert_words(const KParams& p, const uint64_t* words, uint64_t
 // ---- partitioned (atomic-free) bulk build ------------------------------------------------------
 namespace kh {
 
-// The key space is cut into 2^17 hash ranges (top 17 bits of key_hash); because the home slot
+// The key space is cut into 2^rbits regions (kh_codec.hpp place: a hash of the minimizer); because the home slot
 // mulhi(h, cap) is monotonic in h, region r owns the slot range
 // [floor(r*cap/2^17), floor((r+1)*cap/2^17)). Two windowed LDS-sort passes (512 buckets, then 256
 // bins per bucket) group the batch by region, then one workgroup per region builds its slot range
@@ -244,7 +247,7 @@ static constexpr int PART_TILE = 4096;  // records per block-tile of k_part1_con
 static constexpr uint32_t PART_W1_COUNTERS = 512 * 8;  // pass-1 windows: 512 buckets x 8
 uint64_t part_count_words();                      // words of the pass-1 + pass-2 window counters
 uint64_t part_overflow_cap(uint64_t n);           // overflow entries
-uint32_t part_region_cap(uint64_t n);             // words per region window of pass 2
+uint32_t part_region_cap(const KParams& p, uint64_t n);  // words per region window of pass 2
 uint64_t part_buf2_words(const KParams& p, uint64_t n);  // buf2 size (region windows or n * W)
 uint32_t part_win1_cap(uint64_t n);               // words per pass-1 window
 uint64_t part_buf1_words(const KParams& p, uint64_t n);  // buf1 size (pass-1 windows or n * W)
@@ -259,7 +262,11 @@ struct PartBuffers {
     uint32_t* wcnt;      // pass-1 window fill counters
     uint32_t* rcnt;      // region window fill counters (wcnt + rcnt = part_count_words())
     uint64_t* overflow;  // part_overflow_cap(n) * W words
+    uint64_t* headrec = nullptr;  // 2^rbits * hcap chain head records of 2 words (null: no chains)
+    uint32_t hcap = 0;
 };
+// chain head records per region for a table of cap slots (0: K or LDS leave no room for chains)
+uint32_t part_head_cap(const KParams& p, uint64_t cap);
 
 // Build: input is either reference records (recs, R bytes each; start bits -> start_mask) or
 // internal words (words, W each). table_empty: skip loading the current region contents.

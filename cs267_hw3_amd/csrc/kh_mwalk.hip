@@ -51,7 +51,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
             nwords = 0;
             active = true;
             probing = st == MW_LOOKUP;
-            if (probing) s = home_slot(key_hash(k), cap);
+            if (probing) s = home_of(place(k, p), cap, p);
         }
         if (!__any(active)) break;
         if (active && !probing) {
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
                     buf = 0;
                 }
                 k = key_next(k, st, p);
-                const uint64_t hk = key_hash(k);
+                const uint64_t hk = key_hash32(k);
                 if (mw.split_bits && (hk & ((1ull << mw.split_bits) - 1)) == 0) {
                     // the next k-mer heads a segment of its own: report it as this segment's link
                     rec[2 * nrec] = rec_tag(origin, true, 1, idx);
@@ -84,7 +84,12 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
                     ++nrec;
                     fin = true;
                 }
-                const uint32_t q = fin ? mw.rank : owner_key(k, p, mw.P);
+                // one minimizer scan gives both the owner rank and the placement region
+                const uint32_t mv = fin ? 0u : mini_window(k, mini_scan(k, p), p);
+                const uint32_t q = fin ? mw.rank
+                                       : (mw.P == 1 ? 0u
+                                                    : (p.owner_mode == 1 ? owner_key(k, p, mw.P)
+                                                                         : owner_of_mini(mv, mw.P)));
                 if (fin) {
                     // finished below (length record, no message)
                 } else if (q != mw.rank || nwords >= MW_RUN_WORDS) {
@@ -98,7 +103,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
                     ovf = true;
                 } else {
                     probing = true;
-                    s = home_slot(hk, cap);
+                    s = home_of(place_w(mv, k, p), cap, p);
                 }
             }
             if (fin) {
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
             uint64_t w0, w1;
             load_slot<W>(slots, s, w0, w1);
             const bool empty = w0 == EMPTY;
-            const bool hit = !empty & ((w0 >> 6) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
+            const bool hit = !empty & (slot_keybits(w0, p) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
             if (hit) {
                 st = ext_fwd(slot_ext(w0));
                 probing = false;
