@@ -229,27 +229,33 @@ def main():
     value = ops / (ms / 1e3)
     avg = lambda key: sum(p[key] for p in phases) / len(phases)  # noqa: E731
     ins_ms, walk_ms = avg("ms_insert_kernel"), avg("ms_walk")
+    build_ms, walkk_ms = avg("ms_build"), avg("ms_walk_kernel")
     rec_bytes = kh.record_size(k)
     b_alg = 2 * rec_bytes      # read+write one kmer_pair per insert / lookup
-    # Dominant single kernel = the walk, k_walk_q (the insert phase is a pipeline of 5 kernels,
-    # reported separately below); duration = HIP events around its launch on the table's stream.
-    achieved = nl * b_alg / (walk_ms / 1e3) / 1e9
     traffic, tsrc = load_traffic(args.workload, n)
-    roof = {"bound": "hbm", "kernel": "k_walk_q (contig walk)", "achieved": achieved, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic.get("k_walk") if traffic else None,
-            "alg_bytes_per_unit": b_alg, "units_per_launch": nl, "avg_launch_ms": walk_ms,
-            "traffic_GBs": (traffic["k_walk"] / (walk_ms / 1e3) / 1e9) if traffic and "k_walk" in traffic else None,
-            "random_access_ceiling": {
-                "lookups_per_s": nl / (walk_ms / 1e3),
-                "measured_peak_random_64B_requests_per_s": 50.8e9,
-                "note": "tools/membench chase16/chase64q at a 6.4 GB table (profiles/r01/membench.jsonl): "
-                        "one random 16-64 B load = one 64-B HBM read request (TCC_EA0_RDREQ, calibrated in "
-                        "profiles/pmc_traffic.json 'membench'); the walk issues ~1.06 requests per lookup "
-                        "(4-lane block probes)"},
-            "note": "achieved = algorithmic bytes (2*sizeof(kmer_pair) per lookup) / HIP-event "
-                    "duration of k_walk" + (f"; traffic from {tsrc}" if tsrc else "")}
-    insert_pipe = {"kernels": "k_win1_rec (records pass 1), k_win2, k_part_build_pf, k_insert_overflow",
+
+    def kernel_roof(name, units, ms, tkey, what):
+        t = traffic.get(tkey) if traffic else None
+        return {"bound": "hbm", "kernel": name, "achieved": units * b_alg / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": units * b_alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": t,
+                "alg_bytes_per_unit": b_alg, "units_per_launch": units, "avg_launch_ms": ms,
+                "traffic_GBs": (t / (ms / 1e3) / 1e9) if t else None,
+                "note": f"achieved = {what} x 2*sizeof(kmer_pair) / HIP-event duration of the kernel"
+                        + (f"; traffic = PMC HBM bytes per launch from {tsrc}" if tsrc and t else "")}
+
+    # region build (k_part_build_pf: LDS build of every region + chain links + head records, then
+    # the overflow inserts), HIP events around it on the table's stream; its inherent traffic is a
+    # 16-B word in and two 16-B slots out per k-mer (load 0.5), 48 B
+    kb = kernel_roof("k_part_build_pf (region build + chains)", n, build_ms, "k_part_build", "inserts")
+    kb["inherent_bytes_per_unit"] = 48
+    # contig walk: one lookup per k-mer but, with chains, ~2 random requests per run of ~19 k-mers
+    kw = kernel_roof("k_walk_q (contig walk, chain hops)", nl, walkk_ms, "k_walk", "lookups")
+    rq = ((traffic or {}).get("requests") or {}).get("TCC_EA0_RDREQ_sum", {}).get("k_walk")
+    kw["requests_per_lookup"] = rq / nl if rq else None  # 64-B HBM read requests (PMC) per lookup
+    roof = dict(kb if build_ms >= walkk_ms else kw)
+    roof["kernels"] = {"k_part_build_pf": kb, "k_walk_q": kw}
+    insert_pipe = {"kernels": "k_part1_convert (records -> words + minimizer), k_win1, k_win2, k_part_build_pf, "
+                              "k_insert_overflow",
                    "ms": ins_ms, "achieved_alg_GBs": n * b_alg / (ins_ms / 1e3) / 1e9,
                    "inserts_per_s": n / (ins_ms / 1e3),
                    "traffic": traffic.get("insert_pipeline") if traffic else None}
@@ -274,8 +280,8 @@ def main():
                                       "4 nodes x 128 CPU ranks (BASELINE.md)"},
         "inserts_per_s": n / (ms / 1e3), "lookups_per_s": nl / (ms / 1e3),
         "contigs_per_s": nc / (ms / 1e3),
-        "phases_ms": {"insert_total": avg("ms_insert"), "k_insert": ins_ms, "k_walk": walk_ms,
-                      "materialize": avg("ms_materialize")},
+        "phases_ms": {"insert_total": avg("ms_insert"), "k_insert": ins_ms, "build": build_ms,
+                      "k_walk": walk_ms, "walk_kernel": walkk_ms, "materialize": avg("ms_materialize")},
         "verified_vs_truth": ok,
         "roofline": roof, "insert_pipeline": insert_pipe, "end_to_end": e2e, "cpu_baseline": cpu,
     }

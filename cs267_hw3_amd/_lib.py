@@ -32,7 +32,8 @@ class KhStats(ctypes.Structure):
         "capacity", "n_inserted", "n_starts", "n_contigs", "n_lookups", "out_bytes", "n_chunks",
         "n_dup", "n_full", "n_bad_ext", "n_missing", "n_cycle", "n_spin", "n_chunk_ovf")] + [
         (name, ctypes.c_double) for name in (
-            "ms_insert", "ms_insert_kernel", "ms_walk", "ms_materialize")] + [("n_bad_base", c_u64)]
+            "ms_insert", "ms_insert_kernel", "ms_walk", "ms_materialize")] + [("n_bad_base", c_u64)] + \
+            [(f, ctypes.c_double) for f in ("ms_build", "ms_walk_kernel")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -1059,7 +1059,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
                               TableView t, bool table_empty, const PartBuffers& B, uint64_t* start_mask,
                               uint64_t* split_mask, unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
                               hipEvent_t after_records = nullptr, uint64_t* wsplits = nullptr,
-                              uint64_t wsplits_cap = 0) {
+                              uint64_t wsplits_cap = 0, hipEvent_t before_build = nullptr) {
     hipError_t e;
     const uint64_t ovf_cap = part_overflow_cap(n);
     const uint32_t CAP1 = part_win1_cap(n), RC = part_region_cap(p, n);
@@ -1095,6 +1095,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     // start / splitter bits are complete: the caller's compaction may start
     if (after_records && (e = hipEventRecord(after_records, s)) != hipSuccess) return e;
     if ((e = win2_launch<W>(p, B, n, RC, rcnt, ovf_cap, ctr, stats, CAP1, wcnt, s)) != hipSuccess) return e;
+    if (before_build && (e = hipEventRecord(before_build, s)) != hipSuccess) return e;
     return build_launch<W>(p, n, t, table_empty, B, ctr, stats, s);
 }
 
@@ -1139,13 +1140,13 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
                               TableView t, bool table_empty, const PartBuffers& b,
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
                               unsigned long long* stats, hipStream_t s, hipEvent_t after_records,
-                              uint64_t* wsplits, uint64_t wsplits_cap) {
+                              uint64_t* wsplits, uint64_t wsplits_cap, hipEvent_t before_build) {
     if (n == 0) return hipSuccess;
     if (recs) {
         return p.W == 1 ? part_insert<1, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
-                                               stats, s, after_records)
+                                               stats, s, after_records, nullptr, 0, before_build)
                         : part_insert<2, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
-                                               stats, s, after_records);
+                                               stats, s, after_records, nullptr, 0, before_build);
     }
     return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s,
                                             nullptr, wsplits, wsplits_cap)

@@ -126,6 +126,8 @@ struct kh_table {
 
     hipEvent_t ev_ins0 = nullptr, ev_ins1 = nullptr, ev_ins2 = nullptr;
     hipEvent_t ev_walk0 = nullptr, ev_walk1 = nullptr, ev_mat1 = nullptr;
+    hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_wk1 = nullptr;  // build / walk-kernel brackets
+    bool build_timed = false;
     // side stream: start / splitter compaction overlapped with the partition passes
     hipStream_t side = nullptr;
     hipEvent_t ev_conv = nullptr, ev_side = nullptr;
@@ -298,7 +300,8 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     t->stream = t->own_stream;
     if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(KH_ERR_HIP, "hipStreamCreate failed"));
-    hipEvent_t* evs[] = {&t->ev_ins0, &t->ev_ins1, &t->ev_ins2, &t->ev_walk0, &t->ev_walk1, &t->ev_mat1};
+    hipEvent_t* evs[] = {&t->ev_ins0, &t->ev_ins1, &t->ev_ins2, &t->ev_walk0, &t->ev_walk1, &t->ev_mat1,
+                         &t->ev_b0, &t->ev_b1, &t->ev_wk1};
     for (auto* ev : evs)
         if (hipEventCreate(ev) != hipSuccess) return bail(fail(KH_ERR_HIP, "hipEventCreate failed"));
     for (auto* ev : {&t->ev_conv, &t->ev_side})
@@ -328,7 +331,8 @@ int kh_destroy(kh_table* t) {
                       &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec};
     for (auto* b : bufs) b->release();
     if (t->side) (void)hipStreamSynchronize(t->side);
-    hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_conv,
+    hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_b0,
+                        t->ev_b1, t->ev_wk1, t->ev_conv,
                         t->ev_side};
     for (auto ev : evs)
         if (ev) (void)hipEventDestroy(ev);
@@ -421,13 +425,15 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     // compaction runs on the side stream, overlapped with the partition passes and the build
     const bool overlap = part && !kh::debug_flag("no_overlap");
     hipStream_t cs = overlap ? t->side : t->stream;
-    if (part)
+    t->build_timed = part;
+    if (part) {
         KH_HIP(kh::launch_part_insert(t->kp, (const uint8_t*)dev_recs, nullptr, n, view(t),
                                       fresh, pb, t->mask.as<uint64_t>(), split_mask,
                                       t->ctr.as<unsigned long long>(),
                                       t->stats.as<unsigned long long>(), t->stream,
-                                      overlap ? t->ev_conv : nullptr));
-    else
+                                      overlap ? t->ev_conv : nullptr, nullptr, 0, t->ev_b0));
+        KH_HIP(hipEventRecord(t->ev_b1, t->stream));
+    } else
         KH_HIP(kh::launch_insert(t->kp, (const uint8_t*)dev_recs, n, view(t), t->mask.as<uint64_t>(),
                                  split_mask, t->stats.as<unsigned long long>(), t->stream));
     t->last_insert_part = part;
@@ -608,6 +614,7 @@ int kh_assemble_dev(kh_table* t) {
         KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
         KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
         KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, 0, t->stream));
+        KH_HIP(hipEventRecord(t->ev_wk1, t->stream));
         if (kp.split_bits) KH_HIP(kh::launch_segments(kp, wb, sb, stats, t->stream));
         KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
         if (kp.split_bits)
@@ -728,7 +735,9 @@ int kh_get_stats(kh_table* t, kh_stats* s) {
     if (t->walk_timed) {
         if (hipEventElapsedTime(&ms, t->ev_walk0, t->ev_walk1) == hipSuccess) s->ms_walk = ms;
         if (hipEventElapsedTime(&ms, t->ev_walk1, t->ev_mat1) == hipSuccess) s->ms_materialize = ms;
+        if (hipEventElapsedTime(&ms, t->ev_walk0, t->ev_wk1) == hipSuccess) s->ms_walk_kernel = ms;
     }
+    if (t->build_timed && hipEventElapsedTime(&ms, t->ev_b0, t->ev_b1) == hipSuccess) s->ms_build = ms;
     return KH_OK;
 }
 

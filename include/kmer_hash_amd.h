@@ -64,6 +64,8 @@ typedef struct kh_stats {
     double ms_walk;          /* device ms, k_walk, last assemble */
     double ms_materialize;   /* device ms, offsets scan + contig text, last assemble */
     uint64_t n_bad_base;     /* kh_pack_text_dev lines with a k-mer base outside {A,C,G,T} */
+    double ms_build;         /* device ms, region build + overflow inserts of the last partitioned insert */
+    double ms_walk_kernel;   /* device ms, k_walk_q alone, last assemble */
 } kh_stats;
 
 /* ---- sizes / info --------------------------------------------------------------------------*/
