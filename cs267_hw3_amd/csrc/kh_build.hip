@@ -1088,8 +1088,9 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
                 k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
             words = B.buf2;
         }
+        // converted records and routed words (k_route_scatter) both carry j* and the order bits
         if ((e = win1_launch<W>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, REC ? nullptr : wsplits,
-                                wsplits_cap, REC)) != hipSuccess)
+                                wsplits_cap, true)) != hipSuccess)
             return e;
     }
     // start / splitter bits are complete: the caller's compaction may start
@@ -1115,7 +1116,7 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(p, total);
     if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = win1_launch<W>(p, words, m, CAP1, B.wcnt, B, part_overflow_cap(total), ctr, stats, s, wsplits,
-                            wsplits_cap)) != hipSuccess)
+                            wsplits_cap, true)) != hipSuccess)
         return e;
     if ((e = win2_launch<W>(p, B, m, RC, B.rcnt, part_overflow_cap(total), ctr, stats, CAP1, B.wcnt, s)) != hipSuccess)
         return e;

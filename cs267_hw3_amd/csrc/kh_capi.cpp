@@ -827,10 +827,10 @@ int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void
     if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
     if (int rc = set_device(t)) return rc;
     if (int rc = ensure_route(t, n, nranks)) return rc;
-    if (int rc = t->route_own.ensure(n + 16)) return rc;
+    if (int rc = t->route_own.ensure((n + 16) * 4)) return rc;
     KH_HIP(kh::launch_route(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks,
                             t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
-                            t->route_scratch.as<uint64_t>(), t->route_own.as<uint8_t>(), (uint64_t*)words_out,
+                            t->route_scratch.as<uint64_t>(), t->route_own.as<uint32_t>(), (uint64_t*)words_out,
                             (uint64_t*)counts_out, t->stream));
     return KH_OK;
 }
@@ -872,7 +872,7 @@ int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nrank
     if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
     if (int rc = set_device(t)) return rc;
     if (int rc = ensure_route(t, n, nranks)) return rc;
-    if (int rc = t->route_own.ensure(n + 16)) return rc;
+    if (int rc = t->route_own.ensure((n + 16) * 4)) return rc;
     const uint64_t nw = (n + 63) / 64;
     int rc;
     if ((rc = t->mask.ensure(nw * 8 + 8))) return rc;
@@ -882,7 +882,7 @@ int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nrank
     if ((rc = ensure_starts(t, t->collected_n + n))) return rc;
     KH_HIP(kh::launch_route(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks,
                             t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
-                            t->route_scratch.as<uint64_t>(), t->route_own.as<uint8_t>(), (uint64_t*)words_out,
+                            t->route_scratch.as<uint64_t>(), t->route_own.as<uint32_t>(), (uint64_t*)words_out,
                             (uint64_t*)counts_out, t->stream, n ? t->mask.as<uint64_t>() : nullptr));
     if (n)
         KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
@@ -1241,6 +1241,8 @@ int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, vo
     mw.P = t->mw_P;
     mw.rank = t->mw_rank;
     mw.split_bits = t->ms_on ? (uint32_t)mseg_params(t).split_bits : 0u;
+    mw.headrec = t->headrec.as<uint64_t>();
+    mw.hcap = t->headrec.p ? t->hcap : 0u;
     mw.max_steps = t->rw_total;
     mw.in = src;
     mw.n_in = n;

@@ -912,8 +912,9 @@ hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, 
     return hipGetLastError();
 }
 
-// Route = records -> owner-grouped words in two streaming passes over the records (the owner,
-// a minimizer hash, is computed once and kept as one byte per record). Records are staged
+// Route = records -> owner-grouped words in two streaming passes over the records (the minimizer
+// scan runs once, in the first pass, and is kept per record: it gives the owner rank and the
+// j* / order bits the routed words carry into the owner's partition passes). Records are staged
 // through LDS with 16-B loads (15-/7-byte records are unaligned for per-lane loads).
 __device__ __forceinline__ void stage_records(const uint8_t* recs, uint64_t sub, uint32_t cnt, uint32_t R,
                                               uint8_t* st) {
@@ -941,9 +942,17 @@ __device__ __forceinline__ void load_parse_record(const KParams& p, const uint8_
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
-                                                     uint32_t P, uint8_t* own, uint64_t* hist,
+// owner rank of a k-mer whose minimizer scan is mn
+__device__ __forceinline__ uint32_t owner_mn(Key k, uint32_t mn, const KParams& p, uint32_t P) {
+    if (P == 1) return 0;
+    return p.owner_mode == 1 ? owner_key(k, p, P) : owner_of_mini(mini_window(k, mn, p), P);
+}
+
+template <int KT>
+__global__ __launch_bounds__(BLOCK) void k_route_own(KParams p_in, const uint8_t* __restrict__ recs, uint64_t n,
+                                                     uint32_t P, uint32_t* own, uint64_t* hist,
                                                      uint64_t* start_mask) {
+    const KParams p = specialize<KT>(p_in);
     __shared__ uint32_t h[MAX_RANKS];
     __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
     for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
@@ -957,9 +966,9 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* _
         uint32_t ext = 0;
         load_parse_record(p, recs, sub, cnt, st, k, ext);
         if (threadIdx.x < cnt) {
-            const uint32_t q = owner_key(k, p, P);
-            own[sub + threadIdx.x] = (uint8_t)q;
-            atomicAdd(&h[q], 1u);
+            const uint32_t mn = mini_scan(k, p);
+            own[sub + threadIdx.x] = mn;
+            atomicAdd(&h[owner_mn(k, mn, p, P)], 1u);
         }
         if (start_mask) {  // kmer_hash.cpp:27-31 start bits, same pass (ROUTE_TILE is 64-aligned)
             const uint64_t bal = __ballot(threadIdx.x < cnt && ext_bwd(ext) == EXT_F);
@@ -971,10 +980,11 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p, const uint8_t* _
     for (uint32_t q = threadIdx.x; q < P; q += BLOCK) hist[(uint64_t)blockIdx.x * P + q] = h[q];
 }
 
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
-                                                         uint32_t P, const uint8_t* __restrict__ own,
+template <int W, int KT>
+__global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p_in, const uint8_t* __restrict__ recs, uint64_t n,
+                                                         uint32_t P, const uint32_t* __restrict__ own,
                                                          const uint64_t* off, uint64_t nb, uint64_t* out) {
+    const KParams p = specialize<KT>(p_in);
     __shared__ uint32_t h[MAX_RANKS];
     __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
     for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
@@ -988,31 +998,36 @@ __global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p, const uint8_
         uint32_t ext = 0;
         load_parse_record(p, recs, sub, cnt, st, k, ext);
         if (threadIdx.x < cnt) {
-            const uint32_t q = own[sub + threadIdx.x];
+            const uint32_t mn = own[sub + threadIdx.x];
+            const uint32_t q = owner_mn(k, mn, p, P);
             const uint64_t d = off[(uint64_t)q * nb + blockIdx.x] + atomicAdd(&h[q], 1u);
+            const uint64_t w0 = part_word0(slot_w0(k, ext, p), mn, p);  // + j*, order bits
             if (W == 2)
-                *reinterpret_cast<ulonglong2*>(out + d * 2) = make_ulonglong2(slot_w0(k, ext, p), k.lo);
+                *reinterpret_cast<ulonglong2*>(out + d * 2) = make_ulonglong2(w0, k.lo);
             else
-                out[d] = slot_w0(k, ext, p);
+                out[d] = w0;
         }
     }
 }
 
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
-                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint8_t* own, uint64_t* out_words,
+                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint32_t* own, uint64_t* out_words,
                         uint64_t* counts, hipStream_t s, uint64_t* start_mask) {
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
     const uint64_t nb = route_blocks(n);
     if (nb == 0) return hipMemsetAsync(counts, 0, (nranks + 1) * 8, s);
-    k_route_own<<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask);
+    if (p.W == 1)
+        with_kt<1>(p.K, [&](auto kt) { k_route_own<decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask); });
+    else
+        with_kt<2>(p.K, [&](auto kt) { k_route_own<decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask); });
     hipError_t e = scan_exclusive(HistF{hist, nb, nranks}, nb * nranks, off, scratch + 1,
                                   (unsigned long long*)nullptr, total, s);
     if (e != hipSuccess) return e;
     k_route_counts<0><<<1, MAX_RANKS, 0, s>>>(off, nb, nranks, total, counts);
     if (p.W == 1)
-        k_route_scatter<1><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, off, nb, out_words);
+        with_kt<1>(p.K, [&](auto kt) { k_route_scatter<1, decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, off, nb, out_words); });
     else
-        k_route_scatter<2><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, off, nb, out_words);
+        with_kt<2>(p.K, [&](auto kt) { k_route_scatter<2, decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, off, nb, out_words); });
     return hipGetLastError();
 }
 

@@ -138,6 +138,8 @@ struct MWalkRound {
     uint8_t* dst;         // n_in: its destination rank (0xFF = finished)
     uint64_t* stage;      // n_in * MW_REC_SLOTS * 2: text records of input j
     uint8_t* nrec;        // n_in
+    const uint64_t* headrec = nullptr;  // chain head records of this shard's build (hcap 0 = none)
+    uint32_t hcap = 0;
 };
 hipError_t launch_mw_init(const KParams& p, const uint64_t* starts, uint64_t n, uint32_t rank, uint64_t* msgs,
                           hipStream_t s, uint64_t idx0 = 0);
@@ -225,7 +227,7 @@ hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, 
 // Records -> internal words (W per record) grouped by owner rank (owner_key).
 // hist/off: route_blocks(n) * nranks words each; counts: nranks + 1 words (last = n).
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
-                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint8_t* own, uint64_t* out_words,
+                        uint64_t* hist, uint64_t* off, uint64_t* scratch, uint32_t* own, uint64_t* out_words,
                         uint64_t* counts, hipStream_t s, uint64_t* start_mask = nullptr);
 
 // Insert routed internal words.

@@ -26,9 +26,29 @@ __device__ __forceinline__ uint64_t rec_tag(uint32_t origin, bool fin, uint64_t 
 // One lane per input message (static stride, no work-queue atomics), one table probe per loop
 // iteration, like k_walk. A lane's run ends when the walker finishes, migrates, or has flushed
 // MW_RUN_WORDS words this round (it then re-sends itself, bounding the per-input text region).
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __restrict__ slots, uint64_t cap,
+// Chains (kh_build.hip): a probed k-mer whose slot names a head record is crossed in one step —
+// the record's tail key carries the run's bases. A chain shares one minimizer, hence one owner,
+// so it never crosses ranks.
+template <int W, int KT>
+__global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
                                                   MWalkRound mw, unsigned long long* stats) {
+    const KParams p = specialize<KT>(p_in);
+    const bool chains = p.chain && mw.hcap != 0;
+    uint32_t reg = 0;  // region of the k-mer being probed (its head records live there)
+    // append n bases (base i at bits 2i of piece, n <= room in the current word) to the walker's
+    // buffer, flushing a finished 32-base word as a text record
+    auto put = [&](uint64_t piece, uint32_t n, uint64_t& buf, uint32_t& steps, uint32_t& nrec, uint32_t& nwords,
+                   uint64_t* rec, uint32_t origin, uint32_t idx) {
+        buf |= piece << (2 * (steps & 31));
+        steps += n;
+        if ((steps & 31) == 0) {
+            rec[2 * nrec] = rec_tag(origin, false, (steps >> 5) - 1, idx);
+            rec[2 * nrec + 1] = buf;
+            ++nrec;
+            ++nwords;
+            buf = 0;
+        }
+    };
     const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
     uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     bool active = false, probing = false;
@@ -51,7 +71,11 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
             nwords = 0;
             active = true;
             probing = st == MW_LOOKUP;
-            if (probing) s = home_of(place(k, p), cap, p);
+            if (probing) {
+                const Place pl = place(k, p);
+                reg = pl.r;
+                s = home_of(pl, cap, p);
+            }
         }
         if (!__any(active)) break;
         if (active && !probing) {
@@ -103,7 +127,9 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
                     ovf = true;
                 } else {
                     probing = true;
-                    s = home_of(place_w(mv, k, p), cap, p);
+                    const Place pl = place_w(mv, k, p);
+                    reg = pl.r;
+                    s = home_of(pl, cap, p);
                 }
             }
             if (fin) {
@@ -129,7 +155,27 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p, const uint64_t* __r
             const bool empty = w0 == EMPTY;
             const bool hit = !empty & (slot_keybits(w0, p) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
             if (hit) {
-                st = ext_fwd(slot_ext(w0));
+                const uint32_t hidx = chains ? slot_hidx(w0, p) : 0u;
+                if (hidx && nwords + 3 <= MW_RUN_WORDS) {  // the run's <= 2 words fit this round
+                    const ulonglong2 rv =
+                        *reinterpret_cast<const ulonglong2*>(mw.headrec + ((uint64_t)reg * mw.hcap + hidx - 1) * 2);
+                    k = slot_key(rv.x, rv.y, p);
+                    st = ext_fwd(slot_ext(rv.x));
+                    uint32_t n = slot_hidx(rv.x, p);  // links: the last n bases of the tail key
+                    while (n) {
+                        const uint32_t room = 32u - (steps & 31u), m = n < room ? n : room;
+                        const int sh = 2 * (int)(n - m);  // bits [sh, sh + 2m) of V, oldest base first
+                        const uint64_t x = sh < 62 ? (k.lo >> sh) | (k.hi << (62 - sh)) : k.hi >> (sh - 62);
+                        const uint64_t v = m >= 32 ? x : x & ((1ull << (2 * m)) - 1);
+                        const uint64_t r = ((uint64_t)__builtin_bitreverse32((uint32_t)v) << 32) |
+                                           __builtin_bitreverse32((uint32_t)(v >> 32));
+                        const uint64_t rev = ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1);
+                        put(rev >> (64 - 2 * m), m, buf, steps, nrec, nwords, rec, origin, idx);
+                        n -= m;
+                    }
+                } else {
+                    st = ext_fwd(slot_ext(w0));
+                }
                 probing = false;
             } else if (empty) {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
                 atomicAdd(&stats[ST_MISSING], 1ull);
@@ -267,9 +313,9 @@ hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, un
     // ~4 inputs per lane keeps lanes busy through the run-length tail without a work queue
     const unsigned g = grid_for((mw.n_in + 3) / 4, 4096);
     if (p.W == 1)
-        k_mw_run<1><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats);
+        with_kt<1>(p.K, [&](auto kt) { k_mw_run<1, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats); });
     else
-        k_mw_run<2><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats);
+        with_kt<2>(p.K, [&](auto kt) { k_mw_run<2, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats); });
     return hipGetLastError();
 }
 

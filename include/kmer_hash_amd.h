@@ -133,6 +133,8 @@ int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void
  * come from the route's owner pass); successive calls append starts in call order. */
 int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
                         void* dev_counts_out);
+/* dev_words: internal words as kh_route_dev / kh_route_starts_dev emit them (they carry the
+ * k-mer's placement bits: minimizer window, order bits). */
 int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);
 /* Staged insert of routed words (one call per received all-to-all chunk, hash_map.hpp:55-80's
  * insert_all split so that partitioning overlaps the exchange): stage partitions m words toward
