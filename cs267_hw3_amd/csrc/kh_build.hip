@@ -93,18 +93,20 @@ uint64_t part_buf2_words(const KParams& p, uint64_t n) {
 }
 
 static uint64_t region_max_slots(const KParams& p, uint64_t cap) { return cap / nreg(p) + 1; }
-// build LDS: the slice, plus one 16-bit successor per slot when chains are built
+// build LDS: the slice, plus the chain head list (<= slots/8 + 32 entries, part_head_cap) when
+// chains are built (successors live in the slots' own index fields)
 static uint64_t build_lds(const KParams& p, uint64_t cap, bool chains) {
-    // chains: a 16-bit successor per slot + the head list (<= slots/8 + 32 entries, part_head_cap)
     const uint64_t sm = region_max_slots(p, cap);
-    return sm * 8ull * p.W + (chains ? sm * 2 + (sm / 8 + 32) * 2 : 0) + 16;
+    return sm * 8ull * p.W + (chains ? (sm / 8 + 32) * 2 : 0) + 16;
 }
 
 bool region_slots_fit(const KParams& p, uint64_t cap) { return build_lds(p, cap, false) <= LDS_BYTES; }
 
 // head records per region: room for chains of >= 8 slots (C3: 413 for ~75 heads); 0 = no chains
 uint32_t part_head_cap(const KParams& p, uint64_t cap) {
-    if (!p.chain || build_lds(p, cap, true) > LDS_BYTES || region_max_slots(p, cap) >= 0xFFFF) return 0;
+    // a slot's successor (index + 1) must fit its [idx_lo, 58) field while the build links
+    if (!p.chain || build_lds(p, cap, true) > LDS_BYTES || region_max_slots(p, cap) >= (1ull << (58 - p.idx_lo)))
+        return 0;
     const uint64_t lim = (1ull << (SCRATCH_BIT - p.idx_lo)) - 1;
     const uint64_t h = region_max_slots(p, cap) / 8 + 32;
     return (uint32_t)(h < lim ? h : lim);
@@ -261,17 +263,41 @@ __device__ unsigned long long g_build_prof[8];
 // chain record is exact whatever the regions are. Heads (a successor, no predecessor) of this
 // region get a record {tail word0 with the link count in the index field, tail word1} and their
 // slot the record index + 1. succ: S 16-bit entries; hcnt: the region's record counter (zeroed).
-static constexpr uint16_t NO_SUCC = 0xFFFFu;
+// While a region's chains are built, a slot's [idx_lo, 58) field holds its successor's slot + 1
+// (0 = none) and a spare top bit marks "has a linked predecessor" (w1 bit 63 at W=2: lo < 2^62;
+// w0 bit 63 at W=1: j* < 32 there); both are set with LDS atomicOr. After the head records are
+// written, a head slot's field holds its record index + 1 (heads have no predecessor) and every
+// slot that has a predecessor is cleaned at write-out.
+static constexpr uint32_t NO_SUCC = 0xFFFFFFFFu;
+template <int W>
+__device__ __forceinline__ uint32_t succ_of(uint64_t w0, const KParams& p) {
+    return (uint32_t)((w0 >> p.idx_lo) & ((1ull << (58 - p.idx_lo)) - 1)) - 1u;  // NO_SUCC when 0
+}
+template <int W>
+__device__ __forceinline__ unsigned long long* pred_word(unsigned long long* lt, uint32_t t) {
+    return &lt[W * t + (W - 1)];
+}
+static constexpr unsigned long long PRED = 1ull << 63;
+// slot as written to the table: successor field and predecessor bit cleaned unless it is a head
+// whose field is its record index
+template <int W>
+__device__ __forceinline__ void clean_out(uint64_t& w0, uint64_t& w1, const KParams& p) {
+    const bool pred = ((W == 2 ? w1 : w0) & PRED) != 0;
+    if (pred) w0 = slot_clean(w0, p);
+    if (W == 2) w1 &= LO_MASK;
+    else w0 &= ~PRED;
+}
+
 // The slot of x's successor in this slice, or NO_SUCC. With mtop (x is a word of this region's
 // window carrying the top bits of its minimizer order) the test needs no window extraction and
 // y's home is this region's; a tie in the top bits counts as "no link" (never a wrong link).
 template <int W, bool MTOP>
-__device__ __forceinline__ uint16_t chain_link(const KParams& p, const unsigned long long* lt, uint32_t S,
+__device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned long long* lt, uint32_t S,
                                                uint64_t lo, uint64_t cap, uint64_t w0, uint64_t w1) {
     const uint32_t f = ext_fwd(slot_ext(w0));
-    const uint32_t j = slot_jstar(w0);
+    const uint32_t j = slot_jstar(w0) & (W == 1 ? 31u : 63u);
     if (f > 3u || (int)j >= p.K - p.M) return NO_SUCC;
-    const Key x = slot_key(w0, w1, p);
+    const Key x = slot_key(w0, w1 & LO_MASK, p);
     const Key y = key_next(x, f, p);
     uint32_t mw = 0;
     if (MTOP) {
@@ -288,61 +314,79 @@ __device__ __forceinline__ uint16_t chain_link(const KParams& p, const unsigned 
     for (uint32_t t = (uint32_t)(home - lo); t < S; ++t) {
         const uint64_t v0 = lt[W * t];
         if (v0 == EMPTY) break;
-        if (slot_keybits(v0, p) == want0 && (W == 1 || lt[W * t + 1] == y.lo)) return (uint16_t)t;
+        if (slot_keybits(v0, p) == want0 && (W == 1 || (lt[W * t + 1] & LO_MASK) == y.lo)) return t;
     }
     return NO_SUCC;
 }
 
+// record x's link (own slot i: successor field; the successor's predecessor bit)
+template <int W>
+__device__ __forceinline__ void put_link(unsigned long long* lt, uint32_t i, uint32_t nx, const KParams& p) {
+    if (nx == NO_SUCC) return;
+    atomicOr(&lt[W * i], (unsigned long long)(nx + 1) << p.idx_lo);
+    atomicOr(pred_word<W>(lt, nx), PRED);
+}
+template <int W>
+__device__ __forceinline__ bool is_head(const unsigned long long* lt, uint32_t i, const KParams& p) {
+    const uint64_t w0 = lt[W * i];
+    return w0 != EMPTY && succ_of<W>(w0, p) != NO_SUCC && !(lt[W * i + (W - 1)] & PRED);
+}
+
 // Head records of the listed heads (hlist[0, min(*hcnt, hcap))): walk each chain to its tail.
 template <int W, int TB>
-__device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long* lt, const uint16_t* succ,
-                                            const uint16_t* hlist, uint32_t r, bool fresh, uint64_t* headrec,
-                                            uint32_t hcap, const uint32_t* hcnt) {
+__device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long* lt, const uint16_t* hlist,
+                                            uint32_t r, bool fresh, uint64_t* headrec, uint32_t hcap,
+                                            const uint32_t* hcnt) {
     const uint32_t nh = min(*hcnt, hcap);
     for (uint32_t id = threadIdx.x; id < nh; id += TB) {
         const uint32_t i = hlist[id];
         const uint64_t w0 = lt[W * i];
+        bool own = true;
         if (!fresh) {
             // the walker reads a record at the region of the key it looked up: in a slice reloaded
             // from the table only keys of this region may own one (others may have spilled in)
-            const Key hk = slot_key(w0, W == 2 ? lt[W * i + 1] : 0ull, p);
-            if (mini_region(mini_window(hk, mini_scan(hk, p), p), p) != r) continue;
+            const Key hk = slot_key(w0, W == 2 ? lt[W * i + 1] & LO_MASK : 0ull, p);
+            own = mini_region(mini_window(hk, mini_scan(hk, p), p), p) == r;
         }
-        uint32_t t = succ[i], links = 1;
-        while (succ[t] != NO_SUCC && links < 63u) {
-            t = succ[t];
+        if (!own) {
+            lt[W * i] = slot_clean(w0, p);  // no record: the walker steps this k-mer itself
+            continue;
+        }
+        uint32_t t = succ_of<W>(w0, p), links = 1;
+        uint64_t tw0 = lt[W * t];
+        while (succ_of<W>(tw0, p) != NO_SUCC && links < 63u) {
+            t = succ_of<W>(tw0, p);
+            tw0 = lt[W * t];
             ++links;
         }
-        const uint64_t tw0 = lt[W * t], tw1 = W == 2 ? lt[W * t + 1] : 0ull;
+        const uint64_t tw1 = W == 2 ? lt[W * t + 1] & LO_MASK : 0ull;
         *reinterpret_cast<ulonglong2*>(headrec + ((uint64_t)r * hcap + id) * 2) =
-            make_ulonglong2(with_hidx(slot_clean(tw0, p), links, p), tw1);
-        lt[W * i] = with_hidx(w0, id + 1, p);
+            make_ulonglong2(with_hidx(slot_clean(tw0, p) & (W == 1 ? ~PRED : ~0ull), links, p), tw1);
+        lt[W * i] = with_hidx(slot_clean(w0, p), id + 1, p);
     }
 }
 
+// Chains over every slot of the slice (a slice reloaded from the table, or the large-window
+// build): links, then heads into the dense list, then the records.
 template <int W, int TB>
-__device__ __forceinline__ void region_chains(const KParams& p, unsigned long long* lt, uint16_t* succ,
-                                              uint16_t* hlist, uint32_t S, uint64_t lo, uint64_t cap, uint32_t r,
-                                              bool fresh, uint64_t* headrec, uint32_t hcap, uint32_t* hcnt) {
+__device__ __forceinline__ void region_chains(const KParams& p, unsigned long long* lt, uint16_t* hlist, uint32_t S,
+                                              uint64_t lo, uint64_t cap, uint32_t r, bool fresh, uint64_t* headrec,
+                                              uint32_t hcap, uint32_t* hcnt) {
     for (uint32_t i = threadIdx.x; i < S; i += TB) {
         const uint64_t w0 = lt[W * i];
-        uint16_t nx = NO_SUCC;
-        if (w0 != EMPTY) {
-            nx = chain_link<W, false>(p, lt, S, lo, cap, w0, W == 2 ? lt[W * i + 1] : 0ull);
-            if (nx != NO_SUCC) atomicOr(&lt[W * nx], 1ull << SCRATCH_BIT);  // nx has a predecessor
-        }
-        succ[i] = nx;
+        if (w0 != EMPTY)
+            put_link<W>(lt, i, chain_link<W, false>(p, lt, S, lo, cap, w0, W == 2 ? lt[W * i + 1] : 0ull), p);
     }
     lds_barrier();
-    // heads (a successor, no predecessor) -> a dense list: the chain walks keep whole waves busy
     for (uint32_t i = threadIdx.x; i < S; i += TB) {
-        if (succ[i] != NO_SUCC && !((lt[W * i] >> SCRATCH_BIT) & 1ull)) {
+        if (is_head<W>(lt, i, p)) {
             const uint32_t id = atomicAdd(hcnt, 1u);
             if (id < hcap) hlist[id] = (uint16_t)i;
+            else lt[W * i] = slot_clean(lt[W * i], p);  // no record room: no index
         }
     }
     lds_barrier();
-    chain_heads<W, TB>(p, lt, succ, hlist, r, fresh, headrec, hcap, hcnt);
+    chain_heads<W, TB>(p, lt, hlist, r, fresh, headrec, hcap, hcnt);
     lds_barrier();
 }
 
@@ -357,8 +401,7 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
                                                               uint32_t RC, const uint32_t* rcnt,
                                                               uint64_t* headrec, uint32_t hcap, uint32_t smax) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
-    uint16_t* succ = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
-    uint16_t* hlist = succ + smax;
+    uint16_t* hlist = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
     __shared__ uint32_t hcnt;
     const uint32_t NR = nreg(p);
     for (uint32_t r = blockIdx.x; r < NR; r += gridDim.x) {
@@ -404,24 +447,36 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
             }
         }
         __syncthreads();
-        if (hcap) region_chains<W, BUILD_THREADS>(p, lt, succ, hlist, S, lo, cap, r, table_empty != 0, headrec, hcap, &hcnt);
+        if (hcap) region_chains<W, BUILD_THREADS>(p, lt, hlist, S, lo, cap, r, table_empty != 0, headrec, hcap, &hcnt);
         if (W == 2) {
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
             const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) dst[i] = l2[i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                const ulonglong2 v = l2[i];
+                uint64_t x = v.x, y = v.y;
+                if (hcap && x != EMPTY) clean_out<W>(x, y, p);
+                dst[i] = make_ulonglong2(x, y);
+            }
         } else {
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) slots[lo + i] = lt[i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                uint64_t v = lt[i], u = 0;
+                if (hcap && v != EMPTY) clean_out<W>(v, u, p);
+                slots[lo + i] = v;
+            }
         }
         __syncthreads();
     }
 }
 
-// Build from fixed region windows with the next region's words prefetched: each thread holds up
-// to IPT words of the region it inserts and issues the loads of its words of the next region
-// before the LDS inserts and the slice write-out, and region hand-offs use LDS-only barriers,
-// so a block's window loads, LDS work and slice stores overlap.
+// Build from fixed region windows: each thread holds up to IPT words of the region it inserts;
+// region hand-offs use LDS-only barriers, so a block's window loads (issued right after the
+// previous region's write-out), LDS work and slice stores overlap across blocks.
+// Occupancy: three 512-thread blocks per CU (LDS ~50 KB per block with the chain head list, and
+// <= 80 VGPRs: 6 waves per SIMD) beat two blocks that prefetch the next region's window into
+// registers during this one (C3: 4.34 vs 5.20 ms): the next window is loaded after the write-out
+// and the other blocks' phases hide it.
 template <int W, int IPT, int KT>
-__global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p_in, const uint64_t* __restrict__ buf2,
+__global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_part_build_pf(KParams p_in, const uint64_t* __restrict__ buf2,
                                                                  uint64_t* slots, uint64_t cap, int table_empty,
                                                                  uint64_t* ovf, uint64_t ovf_cap,
                                                                  unsigned long long* ctr,
@@ -431,8 +486,7 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p_in, c
                                                                  int prof) {
     const KParams p = specialize<KT>(p_in);
     extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
-    uint16_t* succ = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
-    uint16_t* hlist = succ + smax;
+    uint16_t* hlist = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
     __shared__ uint32_t hcnt;
     unsigned long long pt_ = prof ? __builtin_amdgcn_s_memtime() : 0ull;
     uint64_t a[IPT], b[IPT];
@@ -482,8 +536,6 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p_in, c
         else
             __syncthreads();
         BPROF(0);
-        uint64_t na[IPT], nb[IPT];
-        load(r + gridDim.x, na, nb);  // next region's words in flight during this one
         int pos[IPT];  // LDS slot of each word inserted here (chains walk from these)
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
@@ -506,45 +558,49 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build_pf(KParams p_in, c
         lds_barrier();
         BPROF(1);
         if (hcap && !table_empty) {
-            region_chains<W, BUILD_THREADS>(p, lt, succ, hlist, S, lo, cap, r, false, headrec, hcap, &hcnt);
+            region_chains<W, BUILD_THREADS>(p, lt, hlist, S, lo, cap, r, false, headrec, hcap, &hcnt);
         } else if (hcap) {
             // fresh slice: its keys are exactly this thread's words, so links are computed from
             // registers (no pass over empty slots) and every key knows its slot
 #pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                if (pos[j] < 0) continue;
-                const uint16_t nx = chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j]);
-                succ[pos[j]] = nx;
-                if (nx != NO_SUCC) atomicOr(&lt[W * nx], 1ull << SCRATCH_BIT);
-            }
+            for (int j = 0; j < IPT; ++j)
+                if (pos[j] >= 0) put_link<W>(lt, (uint32_t)pos[j], chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j]), p);
             lds_barrier();
             BPROF(2);
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
-                if (pos[j] < 0 || succ[pos[j]] == NO_SUCC || ((lt[W * pos[j]] >> SCRATCH_BIT) & 1ull)) continue;
+                if (pos[j] < 0 || !is_head<W>(lt, (uint32_t)pos[j], p)) continue;
                 const uint32_t id = atomicAdd(&hcnt, 1u);
-                if (id < hcap) hlist[id] = (uint16_t)pos[j];
+                if (id < hcap)
+                    hlist[id] = (uint16_t)pos[j];
+                else
+                    lt[W * pos[j]] = slot_clean(lt[W * pos[j]], p);  // no record room: no index
             }
             lds_barrier();
             BPROF(3);
-            chain_heads<W, BUILD_THREADS>(p, lt, succ, hlist, r, true, headrec, hcap, &hcnt);
+            chain_heads<W, BUILD_THREADS>(p, lt, hlist, r, true, headrec, hcap, &hcnt);
             lds_barrier();
             BPROF(4);
         }
         if (W == 2) {
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
             const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) dst[i] = l2[i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                const ulonglong2 v = l2[i];
+                uint64_t x = v.x, y = v.y;
+                if (hcap && x != EMPTY) clean_out<W>(x, y, p);
+                dst[i] = make_ulonglong2(x, y);
+            }
         } else {
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) slots[lo + i] = lt[i];
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                uint64_t v = lt[i], u = 0;
+                if (hcap && v != EMPTY) clean_out<W>(v, u, p);
+                slots[lo + i] = v;
+            }
         }
         lds_barrier();
         BPROF(5);
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            a[j] = na[j];
-            b[j] = nb[j];
-        }
+        load(r + gridDim.x, a, b);  // the next region's window (other blocks' phases hide it)
     }
 }
 
