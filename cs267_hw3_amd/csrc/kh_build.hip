@@ -472,9 +472,9 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
 // region hand-offs use LDS-only barriers, so a block's window loads (issued right after the
 // previous region's write-out), LDS work and slice stores overlap across blocks.
 // Occupancy: three 512-thread blocks per CU (LDS ~50 KB per block with the chain head list, and
-// <= 80 VGPRs: 6 waves per SIMD) beat two blocks that prefetch the next region's window into
-// registers during this one (C3: 4.34 vs 5.20 ms): the next window is loaded after the write-out
-// and the other blocks' phases hide it.
+// <= 80 VGPRs: 6 waves per SIMD) beat two blocks that hold a second register copy of the next
+// region's window during the whole region (C3: 4.34 vs 5.20 ms); the next window reuses the
+// registers of this one once its words are consumed.
 template <int W, int IPT, int KT>
 __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_part_build_pf(KParams p_in, const uint64_t* __restrict__ buf2,
                                                                  uint64_t* slots, uint64_t cap, int table_empty,
@@ -490,8 +490,14 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
     __shared__ uint32_t hcnt;
     unsigned long long pt_ = prof ? __builtin_amdgcn_s_memtime() : 0ull;
     uint64_t a[IPT], b[IPT];
-    auto load = [&](uint32_t r, uint64_t (&x)[IPT], uint64_t (&y)[IPT]) {
-        const uint32_t m = r < nreg(p) ? min(rcnt[r], RC) : 0u;
+    // window of region r (m = its fill, read one region ahead as a vector load: a scalar load
+    // would be waited for at the next LDS barrier, which waits on lgkmcnt)
+    auto fill = [&](uint32_t r) {
+        uint32_t z;  // an opaque zero in a VGPR makes the address per-lane
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        return r < nreg(p) ? min(rcnt[r + z], RC) : 0u;
+    };
+    auto load = [&](uint32_t r, uint32_t m, uint64_t (&x)[IPT], uint64_t (&y)[IPT]) {
         const uint64_t base = (uint64_t)(r < nreg(p) ? r : 0) * RC;
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
@@ -510,12 +516,13 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         }
     };
     uint32_t r = blockIdx.x;
-    load(r, a, b);
+    load(r, fill(r), a, b);
     const uint32_t NR = nreg(p);
     for (; r < NR; r += gridDim.x) {
         const uint64_t lo = mulhi64((uint64_t)r << (64 - p.rbits), cap);
         const uint64_t hi = (r + 1 < NR) ? mulhi64((uint64_t)(r + 1) << (64 - p.rbits), cap) : cap;
         const uint32_t S = (uint32_t)(hi - lo);
+        const uint32_t m_next = fill(r + gridDim.x);  // in flight during this region
         if (threadIdx.x == 0) hcnt = 0;
         if (W == 2) {
             ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
@@ -557,7 +564,11 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         }
         lds_barrier();
         BPROF(1);
+        // The next region's window goes into a/b as soon as this region's words are consumed
+        // (after the inserts, or after the links that read them), so its loads are in flight
+        // during the remaining phases and never queue behind the write-out's stores.
         if (hcap && !table_empty) {
+            load(r + gridDim.x, m_next, a, b);
             region_chains<W, BUILD_THREADS>(p, lt, hlist, S, lo, cap, r, false, headrec, hcap, &hcnt);
         } else if (hcap) {
             // fresh slice: its keys are exactly this thread's words, so links are computed from
@@ -565,6 +576,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
 #pragma unroll
             for (int j = 0; j < IPT; ++j)
                 if (pos[j] >= 0) put_link<W>(lt, (uint32_t)pos[j], chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j]), p);
+            load(r + gridDim.x, m_next, a, b);
             lds_barrier();
             BPROF(2);
 #pragma unroll
@@ -581,6 +593,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             chain_heads<W, BUILD_THREADS>(p, lt, hlist, r, true, headrec, hcap, &hcnt);
             lds_barrier();
             BPROF(4);
+        } else {
+            load(r + gridDim.x, m_next, a, b);
         }
         if (W == 2) {
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
@@ -600,7 +614,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         }
         lds_barrier();
         BPROF(5);
-        load(r + gridDim.x, a, b);  // the next region's window (other blocks' phases hide it)
     }
 }
 
