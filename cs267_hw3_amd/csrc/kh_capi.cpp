@@ -131,7 +131,7 @@ struct kh_table {
     // side stream: start / splitter compaction overlapped with the partition passes
     hipStream_t side = nullptr;
     hipEvent_t ev_conv = nullptr, ev_side = nullptr;
-    bool ins_timed = false, walk_timed = false;
+    bool ins_timed = false, walk_timed = false, wk_timed = false;  // wk: ev_wk1 recorded by this walk
 };
 
 namespace {
@@ -339,6 +339,9 @@ int kh_destroy(kh_table* t) {
     if (t->side) (void)hipStreamDestroy(t->side);
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
     delete t;
+    // teardown errors are not the caller's: leave the thread's HIP last-error clear, or the
+    // caller's next launch check (torch's, say) reports it as its own
+    (void)hipGetLastError();
     return KH_OK;
 }
 
@@ -615,6 +618,7 @@ int kh_assemble_dev(kh_table* t) {
         KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
         KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, 0, t->stream));
         KH_HIP(hipEventRecord(t->ev_wk1, t->stream));
+        t->wk_timed = true;
         if (kp.split_bits) KH_HIP(kh::launch_segments(kp, wb, sb, stats, t->stream));
         KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
         if (kp.split_bits)
@@ -735,9 +739,10 @@ int kh_get_stats(kh_table* t, kh_stats* s) {
     if (t->walk_timed) {
         if (hipEventElapsedTime(&ms, t->ev_walk0, t->ev_walk1) == hipSuccess) s->ms_walk = ms;
         if (hipEventElapsedTime(&ms, t->ev_walk1, t->ev_mat1) == hipSuccess) s->ms_materialize = ms;
-        if (hipEventElapsedTime(&ms, t->ev_walk0, t->ev_wk1) == hipSuccess) s->ms_walk_kernel = ms;
+        if (t->wk_timed && hipEventElapsedTime(&ms, t->ev_walk0, t->ev_wk1) == hipSuccess) s->ms_walk_kernel = ms;
     }
     if (t->build_timed && hipEventElapsedTime(&ms, t->ev_b0, t->ev_b1) == hipSuccess) s->ms_build = ms;
+    (void)hipGetLastError();  // a failed elapsed-time query is not the caller's error
     return KH_OK;
 }
 
@@ -1082,6 +1087,7 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     t->rw_total = total_kmers > ns ? total_kmers : ns;
     t->mw_store_n = 0;
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
+    t->wk_timed = false;
     KH_HIP(kh::launch_mw_init(t->kp, t->starts.as<uint64_t>(), ns, (uint32_t)rank, t->mw_init.as<uint64_t>(),
                               t->stream));
     if (t->ms_on) {

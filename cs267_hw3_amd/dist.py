@@ -717,8 +717,9 @@ def bench_main(args, w, world, rank):
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)
-    dm.close()
-    shard.table.close()
+    torch.cuda.synchronize()
     dist.barrier()
     dist.destroy_process_group()
+    dm.close()
+    shard.table.close()
     return 0

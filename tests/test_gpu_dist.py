@@ -149,3 +149,23 @@ def test_sharded_skewed_c5(P):
     g = kh.SyntheticKmers(51, 600_000, 2, 16, 0, seed=55, n_long=4, long_len=20_000, front_starts=True)
     info = {}
     check_ranks(g, run_threaded(51, g.records(), P, info=info), P)
+
+
+def test_sharded_stats_leave_no_hip_error():
+    """The migrating walk records no walk-kernel event; stats() must not leave a failed event
+    query as the thread's HIP last-error (torch's next launch check would raise it)."""
+    import torch
+    from cs267_hw3_amd.dist import DistributedKmerHashMap, GpuShard, ThreadComm
+    g = kh.SyntheticKmers(51, 200_000, 8, 200, 0, seed=9)
+    sh = GpuShard(51, 200_000)
+    dm = DistributedKmerHashMap(ThreadComm.group(1)[0], sh)
+    with torch.cuda.stream(sh.stream):
+        dm.insert_all(torch.from_numpy(g.records()).cuda())
+        dm.assemble(200_000)
+    sh.sync()
+    s = sh.stats()
+    assert s["ms_walk"] >= 0 and s["ms_walk_kernel"] == 0
+    assert dm.contigs_text() == g.truth()
+    assert torch.ones(64, device="cuda").sum().item() == 64  # raises on a stale HIP error
+    sh.table.close()
+    assert torch.ones(64, device="cuda").sum().item() == 64
