@@ -475,9 +475,13 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
 // <= 80 VGPRs: 6 waves per SIMD) beat two blocks that hold a second register copy of the next
 // region's window during the whole region (C3: 4.34 vs 5.20 ms); the next window reuses the
 // registers of this one once its words are consumed.
-template <int W, int IPT, int KT>
+// FRESH (the table was empty: every slice starts EMPTY) is a compile-time variant: with the
+// reload-and-rechain path compiled in, spills on that path made the compiler drain every
+// outstanding store (vmcnt(0)) at the top of each region; the fresh kernel has no spills and its
+// slice stores drain in the background (C3 build 4.31 -> 3.86 ms).
+template <int W, int IPT, int KT, bool FRESH>
 __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_part_build_pf(KParams p_in, const uint64_t* __restrict__ buf2,
-                                                                 uint64_t* slots, uint64_t cap, int table_empty,
+                                                                 uint64_t* slots, uint64_t cap,
                                                                  uint64_t* ovf, uint64_t ovf_cap,
                                                                  unsigned long long* ctr,
                                                                  unsigned long long* stats, uint32_t RC,
@@ -492,11 +496,9 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
     uint64_t a[IPT], b[IPT];
     // window of region r (m = its fill, read one region ahead as a vector load: a scalar load
     // would be waited for at the next LDS barrier, which waits on lgkmcnt)
-    auto fill = [&](uint32_t r) {
-        uint32_t z;  // an opaque zero in a VGPR makes the address per-lane
-        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-        return r < nreg(p) ? min(rcnt[r + z], RC) : 0u;
-    };
+    // z: a per-lane zero the compiler cannot fold (prof is 0 or 1) makes the address per-lane
+    const uint32_t z = threadIdx.x & (uint32_t)(prof >> 8);
+    auto fill = [&](uint32_t r) { return r < nreg(p) ? min(rcnt[r + z], RC) : 0u; };
     auto load = [&](uint32_t r, uint32_t m, uint64_t (&x)[IPT], uint64_t (&y)[IPT]) {
         const uint64_t base = (uint64_t)(r < nreg(p) ? r : 0) * RC;
 #pragma unroll
@@ -528,17 +530,17 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
             const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                ulonglong2 v = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
+                ulonglong2 v = FRESH ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
                 if (v.x != EMPTY) v.x = slot_clean(v.x, p);  // earlier chain bits are rebuilt
                 l2[i] = v;
             }
         } else {
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                const unsigned long long v = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
+                const unsigned long long v = FRESH ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
                 lt[i] = v == EMPTY ? v : slot_clean(v, p);
             }
         }
-        if (table_empty)
+        if (FRESH)
             lds_barrier();
         else
             __syncthreads();
@@ -567,7 +569,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         // The next region's window goes into a/b as soon as this region's words are consumed
         // (after the inserts, or after the links that read them), so its loads are in flight
         // during the remaining phases and never queue behind the write-out's stores.
-        if (hcap && !table_empty) {
+        if (hcap && !FRESH) {
             load(r + gridDim.x, m_next, a, b);
             region_chains<W, BUILD_THREADS>(p, lt, hlist, S, lo, cap, r, false, headrec, hcap, &hcnt);
         } else if (hcap) {
@@ -597,13 +599,18 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             load(r + gridDim.x, m_next, a, b);
         }
         if (W == 2) {
+            // two slots per step: both LDS reads are in flight before either store
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
             const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                const ulonglong2 v = l2[i];
-                uint64_t x = v.x, y = v.y;
+            for (uint32_t i = threadIdx.x; i < S; i += 2 * BUILD_THREADS) {
+                const uint32_t i2 = i + BUILD_THREADS;
+                const bool two = i2 < S;
+                const ulonglong2 v = l2[i], u = l2[two ? i2 : i];
+                uint64_t x = v.x, y = v.y, x2 = u.x, y2 = u.y;
                 if (hcap && x != EMPTY) clean_out<W>(x, y, p);
+                if (hcap && x2 != EMPTY) clean_out<W>(x2, y2, p);
                 dst[i] = make_ulonglong2(x, y);
+                if (two) dst[i2] = make_ulonglong2(x2, y2);
             }
         } else {
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
@@ -615,6 +622,14 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         lds_barrier();
         BPROF(5);
     }
+}
+
+template <int W, int IPT, int KT, class... A>
+static void pf_launch(bool fresh, size_t lds, hipStream_t s, A... a) {
+    if (fresh)
+        k_part_build_pf<W, IPT, KT, true><<<8192, BUILD_THREADS, lds, s>>>(a...);
+    else
+        k_part_build_pf<W, IPT, KT, false><<<8192, BUILD_THREADS, lds, s>>>(a...);
 }
 
 // Region-window build: the prefetching kernel when a window fits IPT words per thread.
@@ -634,13 +649,13 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap, ctr,
                                                          stats, RC, rcnt, B.headrec, hcap, smax);
     else if (RC <= 4u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { k_part_build_pf<W, 4, decltype(kt)::value><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 4, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.overflow, ovf_cap,
                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else if (RC <= 6u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { k_part_build_pf<W, 6, decltype(kt)::value><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 6, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.overflow, ovf_cap,
                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else if (RC <= 12u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { k_part_build_pf<W, 12, decltype(kt)::value><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 12, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.overflow, ovf_cap,
                                                                 ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap, ctr,
@@ -649,8 +664,12 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
         unsigned long long v[8];
         (void)hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_build_prof), sizeof v, 0, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
+        unsigned long long novf = 0;
+        (void)hipMemcpyAsync(&novf, ctr + CT_OVF, 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
         fprintf(stderr, "build_prof (s_memtime, summed over blocks): slice-init %llu insert %llu link %llu "
-                        "heads %llu walk+rec %llu write %llu\n", v[0], v[1], v[2], v[3], v[4], v[5]);
+                        "heads %llu walk+rec %llu write %llu | RC %u overflow %llu\n", v[0], v[1], v[2], v[3], v[4],
+                v[5], RC, novf);
     }
 }
 
@@ -1110,9 +1129,12 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
     if ((e = with_kt<W>(p.K, [&](auto kt) {
              constexpr int KT = decltype(kt)::value;
              hipError_t x;
-             if ((x = allow_lds(k_part_build_pf<W, 4, KT>, lds)) != hipSuccess) return x;
-             if ((x = allow_lds(k_part_build_pf<W, 6, KT>, lds)) != hipSuccess) return x;
-             return allow_lds(k_part_build_pf<W, 12, KT>, lds);
+             if ((x = allow_lds(k_part_build_pf<W, 4, KT, true>, lds)) != hipSuccess) return x;
+             if ((x = allow_lds(k_part_build_pf<W, 6, KT, true>, lds)) != hipSuccess) return x;
+             if ((x = allow_lds(k_part_build_pf<W, 12, KT, true>, lds)) != hipSuccess) return x;
+             if ((x = allow_lds(k_part_build_pf<W, 4, KT, false>, lds)) != hipSuccess) return x;
+             if ((x = allow_lds(k_part_build_pf<W, 6, KT, false>, lds)) != hipSuccess) return x;
+             return allow_lds(k_part_build_pf<W, 12, KT, false>, lds);
          })) != hipSuccess)
         return e;
     const uint32_t RC = part_region_cap(p, total);
