@@ -130,15 +130,12 @@ inline void set_region_bits(KParams& p, uint64_t cap) {
 }
 
 KH_HD uint32_t base_code(uint8_t c) {
-    // 'A'=65 'C'=67 'G'=71 'T'=84 'F'=70
-    switch (c) {
-    case 'A': return 0;
-    case 'C': return 1;
-    case 'G': return 2;
-    case 'T': return 3;
-    case 'F': return EXT_F;
-    default: return EXT_BAD;
-    }
+    // 'A'=65 'C'=67 'G'=71 'T'=84 'F'=70 -> 0 1 2 3 EXT_F, anything else EXT_BAD. Branchless (no
+    // divergent switch on the device): the low nibbles of the five are distinct, a 16 x 4-bit table
+    // gives the candidate code and the code's own character confirms the whole byte.
+    const uint32_t k = (uint32_t)(0x5555555524531505ull >> ((c & 15u) * 4u)) & 15u;
+    const uint32_t back = (uint32_t)(0x4654474341ull >> (k * 8u)) & 0xFFu;  // k = 5: 0
+    return back == c ? k : EXT_BAD;
 }
 
 KH_HD uint8_t code_char(uint32_t code) {

@@ -14,6 +14,6 @@ acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(f)):
     acc[r["Kernel_Name"][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in acc.items():
-    if any(x in k for x in ("k_walk", "k_part_build", "k_win1", "k_win2")):
+    if any(x in k for x in ("k_walk", "k_part_build", "k_win1", "k_win2", "k_part1_convert", "k_route")):
         print(k, {c: "%.4g" % (sum(v) / len(v)) for c, v in d.items()})
 PY
