@@ -312,9 +312,16 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned 
     if (home < lo || home >= lo + S) return NO_SUCC;
     const uint64_t want0 = W == 1 ? y.lo : y.hi;
     for (uint32_t t = (uint32_t)(home - lo); t < S; ++t) {
-        const uint64_t v0 = lt[W * t];
+        uint64_t v0, v1 = 0;
+        if (W == 2) {  // both words in one LDS read: a match needs no second round trip
+            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(lt)[t];
+            v0 = v.x;
+            v1 = v.y;
+        } else {
+            v0 = lt[t];
+        }
         if (v0 == EMPTY) break;
-        if (slot_keybits(v0, p) == want0 && (W == 1 || (lt[W * t + 1] & LO_MASK) == y.lo)) return t;
+        if (slot_keybits(v0, p) == want0 && (W == 1 || (v1 & LO_MASK) == y.lo)) return t;
     }
     return NO_SUCC;
 }
@@ -328,8 +335,15 @@ __device__ __forceinline__ void put_link(unsigned long long* lt, uint32_t i, uin
 }
 template <int W>
 __device__ __forceinline__ bool is_head(const unsigned long long* lt, uint32_t i, const KParams& p) {
-    const uint64_t w0 = lt[W * i];
-    return w0 != EMPTY && succ_of<W>(w0, p) != NO_SUCC && !(lt[W * i + (W - 1)] & PRED);
+    uint64_t w0, wp;  // wp: the word holding the predecessor bit (one 16-B LDS read at W=2)
+    if (W == 2) {
+        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(lt)[i];
+        w0 = v.x;
+        wp = v.y;
+    } else {
+        w0 = wp = lt[i];
+    }
+    return w0 != EMPTY && succ_of<W>(w0, p) != NO_SUCC && !(wp & PRED);
 }
 
 // Head records of the listed heads (hlist[0, min(*hcnt, hcap))): walk each chain to its tail.
