@@ -55,6 +55,21 @@ def test_pack_rejects_non_acgt():
         kh.pack_kmer(19, "ACGTACGTACGTACGTACN")
 
 
+def test_pack_every_byte_value():
+    # the branch-free base decode (kh_codec.hpp base_code) against all 256 byte values: exactly
+    # A C G T pack (to codes 0..3), anything else is rejected
+    head = b"ACGTACGTACGTACGTAC"
+    for b in range(256):
+        s = head + bytes([b])
+        if b in b"ACGT":
+            got = kh.pack_kmer(19, s)
+            # base i sits in byte i/4 at bits 7-2(i%4)..6-2(i%4) (packing.hpp:50-75): base 18 -> bits 3..2
+            assert (got[-1] >> 2) & 3 == b"ACGT".index(b), b
+        else:
+            with pytest.raises(kh.KmerHashError):
+                kh.pack_kmer(19, s)
+
+
 @pytest.mark.parametrize("name", sorted(MANIFEST))
 def test_pack_text_matches_oracle(name):
     k = MANIFEST[name]["k"]
