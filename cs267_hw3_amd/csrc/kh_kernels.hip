@@ -571,23 +571,38 @@ template <int W>
 __global__ __launch_bounds__(BLOCK) void k_write_heads(KParams p, const uint64_t* starts, uint64_t nc,
                                                        const uint32_t* len, const uint64_t* off,
                                                        char* out) {
-    for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < nc;
-         c += (uint64_t)gridDim.x * BLOCK) {
+    // 16 lanes per contig: lane l owns the aligned dword at (o & ~3) + 4l of the contig's K head
+    // characters (o = its text offset), so a store instruction writes four contigs' heads as
+    // contiguous runs; the first and last dword of a head are shared with the neighbouring text
+    // (previous line, appended bases) and written byte by byte.
+    constexpr uint32_t G = 16;
+    static_assert(KMAX + 3 <= 4 * G, "a head spans at most 16 dwords");
+    const uint32_t l = threadIdx.x & (G - 1);
+    const uint64_t groups = (uint64_t)gridDim.x * (BLOCK / G);
+    for (uint64_t c = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / G; c < nc; c += groups) {
         const uint64_t w0 = starts[c * W];
         const uint64_t w1 = (W == 2) ? starts[c * W + 1] : 0;
         const Key k = slot_key(w0, w1, p);
-        char* o = out + off[c];
-        // base j of the k-mer sits at bit 2(K-1-j) of V = hi:lo
-        store_chars(o, (uint32_t)p.K, [&](uint32_t i) {
-            uint32_t c8 = 0;
+        const uint64_t o = off[c];
+        const uint32_t a = (uint32_t)(o & 3u);
+        const int c0 = (int)(4 * l) - (int)a;  // first character of this lane's dword
+        if (c0 < p.K) {
+            uint32_t dw = 0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const int j = 4 * (int)i + b;
-                c8 |= (j < p.K ? key_base(k, j, p) : 0u) << (2 * b);
+                const int j = c0 + b;
+                const uint32_t code = (j >= 0 && j < p.K) ? key_base(k, j, p) : 0u;
+                dw |= ((0x54474341u >> (8 * code)) & 0xFFu) << (8 * b);
             }
-            return codes4_chars(c8);
-        });
-        o[p.K + len[c] - 1] = '\n';
+            char* d = out + (o - a) + 4 * (uint64_t)l;
+            if (c0 >= 0 && c0 + 4 <= p.K) {
+                *reinterpret_cast<uint32_t*>(d) = dw;
+            } else {
+                for (int b = 0; b < 4; ++b)
+                    if (c0 + b >= 0 && c0 + b < p.K) d[b] = (char)(dw >> (8 * b));
+            }
+        }
+        if (l == 0) out[o + p.K + len[c] - 1] = '\n';
     }
 }
 
@@ -693,7 +708,7 @@ hipError_t launch_contig_offsets(int K, const uint32_t* len, uint64_t nc, uint64
 hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t nc, const uint32_t* len,
                               const uint64_t* offsets, char* out, hipStream_t s) {
     if (nc == 0) return hipSuccess;
-    const unsigned gh = (unsigned)hmin((nc + BLOCK - 1) / BLOCK, 8192);
+    const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
     if (p.W == 1)
         k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, starts, nc, len, offsets, out);
     else
@@ -712,7 +727,7 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
         if (e != hipSuccess) return e;
     }
     if (!(phases & MAT_WRITE)) return hipSuccess;
-    const unsigned gh = (unsigned)hmin((nc + BLOCK - 1) / BLOCK, 8192);
+    const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
     if (p.W == 1)
         k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out);
     else
