@@ -854,6 +854,10 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
 }
 
 // Chunk words of segment g go to contig seg_contig[g] at base offset seg_off[g].
+// Four threads per chunk (words q and q + 4 of it): C3 segments (~100 bases) use ~4 of a chunk's
+// 8 words and C5's ~21M contigs of 2-16 k-mers one, so eight threads per chunk (one per word)
+// mostly load the segment metadata only to find their word unused.
+static constexpr uint32_t WC_TPC = 4;
 __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_t* chunk_data, const uint32_t* owner,
                                                             const uint32_t* seq, const unsigned long long* ctr,
                                                             uint64_t chunk_cap, uint64_t n_starts,
@@ -863,20 +867,23 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
                                                             char* out) {
     const uint64_t nseg = n_starts + (nsp_dev ? (uint64_t)*nsp_dev : nsp);
     const uint64_t nchunks = min(nseg + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
-    const uint64_t nwords = nchunks * CHUNK_WORDS;
-    for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nwords; t += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t ch = t / CHUNK_WORDS;
-        const uint32_t w = (uint32_t)(t % CHUNK_WORDS);
+    const uint64_t nt = nchunks * WC_TPC;
+    for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nt; t += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t ch = t / WC_TPC;
+        const uint32_t q = (uint32_t)(t % WC_TPC);
         const uint32_t g = ch < nseg ? (uint32_t)ch : owner[ch];
         const uint32_t c = seg_contig[g];
         if (c == SEG_NONE) continue;  // a segment no contig reached
-        const uint64_t j0 = (ch < nseg ? 0ull : (uint64_t)seq[ch] * CHUNK_BASES) + (uint64_t)w * 32;
+        const uint64_t cb = ch < nseg ? 0ull : (uint64_t)seq[ch] * CHUNK_BASES;
         const uint64_t app = (uint64_t)seg_len[g] - 1;
-        if (j0 >= app) continue;
-        const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
-        const uint64_t word = chunk_data[t];
-        char* o = out + off[c] + K + seg_off[g] + j0;
-        store_chars(o, cntb, [&](uint32_t i) { return codes4_chars((uint32_t)(word >> (8 * i)) & 0xFFu); });
+        if (cb + 32 * q >= app) continue;
+        const uint32_t cnt = (uint32_t)min<uint64_t>(CHUNK_BASES, app - cb);
+        char* o = out + off[c] + K + seg_off[g] + cb;
+        for (uint32_t w = q; 32 * w < cnt; w += WC_TPC) {
+            const uint64_t word = chunk_data[ch * CHUNK_WORDS + w];
+            store_chars(o + 32 * w, min(32u, cnt - 32 * w),
+                        [&](uint32_t i) { return codes4_chars((uint32_t)(word >> (8 * i)) & 0xFFu); });
+        }
     }
 }
 
@@ -893,7 +900,7 @@ hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const
     }
     if (!(phases & MAT_WRITE)) return hipSuccess;
     if ((e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s)) != hipSuccess) return e;
-    const unsigned gc = (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
+    const unsigned gc = (unsigned)hmin((wb.chunk_cap * WC_TPC + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks_seg<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr, wb.chunk_cap,
                                             nc, wb.n_splits_dev, wb.n_splits, wb.contig_len, sb.seg_contig,
                                             sb.seg_off, offsets, out);
