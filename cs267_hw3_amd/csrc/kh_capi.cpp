@@ -92,6 +92,7 @@ struct kh_table {
     DevBuf slots, starts, ctr, stats;
     DevBuf splits, splits_w;                 // splitter k-mers (walk segments) / walk subset
     DevBuf seg_next, seg_key, seg_contig, seg_off, clen, stab, stab_id;  // splitter segments
+    DevBuf seg_jump, seg_jsum, seg_anchor, seg_pend;
     DevBuf mask, mask_off, scratch;          // per insert batch
     DevBuf stage;                            // host-API staging of records / keys
     DevBuf stage2, stage3;
@@ -325,6 +326,7 @@ int kh_destroy(kh_table* t) {
                       &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->splits, &t->splits_w, &t->seg_next,
                       &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id,
+                      &t->seg_jump, &t->seg_jsum, &t->seg_anchor, &t->seg_pend,
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
@@ -592,7 +594,9 @@ int kh_assemble_dev(kh_table* t) {
         if ((rc = t->seg_next.ensure((nseg + 1) * 4)) || (rc = t->seg_key.ensure((nseg + 1) * 16)) ||
             (rc = t->seg_contig.ensure((nseg + 1) * 4)) || (rc = t->seg_off.ensure((nseg + 1) * 4)) ||
             (rc = t->clen.ensure((ns + 1) * 4)) || (rc = t->stab.ensure(cap2 * 16)) ||
-            (rc = t->stab_id.ensure(cap2 * 4)))
+            (rc = t->stab_id.ensure(cap2 * 4)) || (rc = t->seg_jump.ensure((nseg + 1) * 4)) ||
+            (rc = t->seg_jsum.ensure((nseg + 1) * 4)) || (rc = t->seg_anchor.ensure(nseg + 1)) ||
+            (rc = t->seg_pend.ensure((ns + 2) * 4)))
             return rc;
         wb.splits = splits;
         wb.n_splits = nsp;
@@ -605,6 +609,11 @@ int kh_assemble_dev(kh_table* t) {
         sb.seg_contig = t->seg_contig.as<uint32_t>();
         sb.seg_off = t->seg_off.as<uint32_t>();
         sb.clen = t->clen.as<uint32_t>();
+        sb.jump = t->seg_jump.as<uint32_t>();
+        sb.jsum = t->seg_jsum.as<uint32_t>();
+        sb.anchor = t->seg_anchor.as<uint8_t>();
+        sb.pend = t->seg_pend.as<uint32_t>();
+        sb.long_flag = sb.pend + ns + 1;
         KH_HIP(hipMemsetAsync(wb.seg_next, 0xff, nseg * 4, t->stream));
     }
     unsigned long long* ctr = t->ctr.as<unsigned long long>();

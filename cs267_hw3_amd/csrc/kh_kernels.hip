@@ -789,11 +789,20 @@ __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, const uint64
     }
 }
 
+// Each contig's chain of segments -> its length and every segment's contig and base offset.
+// One thread per contig walks its chain serially for up to SEG_SERIAL segments (C3: 1-3, C2: ~80).
+// Longer chains (C5: ~4K segments per 10^6-k-mer chain, 2 ms as one serial walk) raise a flag and
+// continue over jump pointers: every segment gets a pointer SEG_JUMP links ahead and the bases of
+// those links (k_seg_jump, all segments in parallel); the contig walks the jump pointers only,
+// marking the segments it lands on (k_seg_chain_jump); each marked segment fills in the
+// SEG_JUMP - 1 segments after it (k_seg_fill). Without the flag those three kernels return at once.
+static constexpr uint32_t SEG_SERIAL = 256, SEG_JUMP = 16;
 __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
     for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < wb.n_starts; c += (uint64_t)gridDim.x * BLOCK) {
         uint32_t g = (uint32_t)c;
         uint64_t off = 0, hops = 0;
+        uint32_t pend = SEG_NONE;
         while (true) {
             sb.seg_contig[g] = (uint32_t)c;
             sb.seg_off[g] = (uint32_t)off;
@@ -804,8 +813,70 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers 
                 atomicAdd(&stats[ST_CYCLE], 1ull);
                 break;
             }
+            if (hops == SEG_SERIAL) {  // a long chain: the rest goes over jump pointers
+                pend = g;
+                *sb.long_flag = 1u;
+                break;
+            }
+        }
+        sb.pend[c] = pend;
+        sb.clen[c] = (uint32_t)(off + 1);  // pending: the bases before segment pend
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seg_jump(WalkBuffers wb, SegBuffers sb) {
+    if (!*sb.long_flag) return;
+    const uint64_t nseg = wb.n_starts + walk_splits(wb);
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg; i += (uint64_t)gridDim.x * BLOCK) {
+        uint32_t g = (uint32_t)i, sum = 0;
+        for (uint32_t h = 0; h < SEG_JUMP && g != SEG_NONE; ++h) {
+            sum += wb.contig_len[g] - 1;
+            g = wb.seg_next[g];
+        }
+        sb.jump[i] = g;
+        sb.jsum[i] = sum;
+        sb.anchor[i] = 0;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seg_chain_jump(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
+    if (!*sb.long_flag) return;
+    const uint64_t nseg = wb.n_starts + walk_splits(wb);
+    for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < wb.n_starts; c += (uint64_t)gridDim.x * BLOCK) {
+        uint32_t g = sb.pend[c];
+        if (g == SEG_NONE) continue;
+        uint64_t off = sb.clen[c] - 1, hops = 0;
+        while (true) {
+            sb.seg_contig[g] = (uint32_t)c;
+            sb.seg_off[g] = (uint32_t)off;
+            sb.anchor[g] = 1;
+            off += sb.jsum[g];
+            g = sb.jump[g];
+            if (g == SEG_NONE) break;
+            if (++hops * SEG_JUMP > nseg || off > wb.max_steps) {  // segments in a cycle
+                atomicAdd(&stats[ST_CYCLE], 1ull);
+                break;
+            }
         }
         sb.clen[c] = (uint32_t)(off + 1);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seg_fill(WalkBuffers wb, SegBuffers sb) {
+    if (!*sb.long_flag) return;
+    const uint64_t nseg = wb.n_starts + walk_splits(wb);
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg; i += (uint64_t)gridDim.x * BLOCK) {
+        if (!sb.anchor[i]) continue;
+        uint32_t g = (uint32_t)i;
+        const uint32_t c = sb.seg_contig[g];
+        uint64_t off = sb.seg_off[g];
+        for (uint32_t h = 1; h < SEG_JUMP; ++h) {
+            off += wb.contig_len[g] - 1;
+            g = wb.seg_next[g];
+            if (g == SEG_NONE) break;
+            sb.seg_contig[g] = c;
+            sb.seg_off[g] = (uint32_t)off;
+        }
     }
 }
 
@@ -848,8 +919,15 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
             p, wb, sb.stab, sb.stab_id, sb.cap2);
     k_seg_link<<<(unsigned)hmin((nseg + BLOCK - 1) / BLOCK, 8192), BLOCK, 0, s>>>(wb, sb.stab, sb.stab_id, sb.cap2,
                                                                                    stats);
-    if (wb.n_starts)
-        k_seg_chain<<<(unsigned)hmin((wb.n_starts + BLOCK - 1) / BLOCK, 8192), BLOCK, 0, s>>>(wb, sb, stats);
+    if (wb.n_starts) {
+        const unsigned gs = (unsigned)hmin((nseg + BLOCK - 1) / BLOCK, 8192);
+        const unsigned gc = (unsigned)hmin((wb.n_starts + BLOCK - 1) / BLOCK, 8192);
+        if ((e = hipMemsetAsync(sb.long_flag, 0, 4, s)) != hipSuccess) return e;
+        k_seg_chain<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
+        k_seg_jump<<<gs, BLOCK, 0, s>>>(wb, sb);
+        k_seg_chain_jump<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
+        k_seg_fill<<<gs, BLOCK, 0, s>>>(wb, sb);
+    }
     return hipGetLastError();
 }
 

@@ -103,6 +103,11 @@ struct SegBuffers {
     uint32_t* seg_contig;  // nseg
     uint32_t* seg_off;     // nseg: bases of the contig before this segment
     uint32_t* clen;        // n_starts: final contig k-mers
+    uint32_t* jump;        // nseg: the segment SEG_JUMP links ahead (k_seg_chain)
+    uint32_t* jsum;        // nseg: bases of the SEG_JUMP segments from this one
+    uint8_t* anchor;       // nseg: a contig's walk over jump pointers visited this segment
+    uint32_t* pend;        // n_starts: segment where a contig's serial walk stopped (SEG_NONE: done)
+    uint32_t* long_flag;   // one word: some contig has more than SEG_SERIAL segments
 };
 // splits with (hash & (2^bits - 1)) == 0 -> out (count to *count)
 hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64_t n, int bits, uint64_t* off,
