@@ -638,12 +638,26 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
     }
 }
 
+// Grid of the prefetching build: 16384 blocks (8 regions each at C3). A resident grid (3 blocks
+// per CU, ~170 regions each) measured slower, 3.71 -> 4.05 ms, and 2 generations of blocks 3.93:
+// region loads vary (sd ~7 %), so dynamic block dispatch balances better than a static split.
+// Same box, C3 build: 8192 blocks 3.73-3.79, 16384 3.69, 32768 3.72, 65536 3.75 ms.
+// KH_BUILD_GRID=<blocks> overrides it (A/B runs).
+static unsigned pf_grid() {
+    if (const char* e = getenv("KH_BUILD_GRID")) {
+        const int g = atoi(e);
+        if (g > 0) return (unsigned)g;
+    }
+    return 16384u;
+}
+
 template <int W, int IPT, int KT, class... A>
 static void pf_launch(bool fresh, size_t lds, hipStream_t s, A... a) {
-    if (fresh)
-        k_part_build_pf<W, IPT, KT, true><<<8192, BUILD_THREADS, lds, s>>>(a...);
-    else
-        k_part_build_pf<W, IPT, KT, false><<<8192, BUILD_THREADS, lds, s>>>(a...);
+    if (fresh) {
+        k_part_build_pf<W, IPT, KT, true><<<pf_grid(), BUILD_THREADS, lds, s>>>(a...);
+    } else {
+        k_part_build_pf<W, IPT, KT, false><<<pf_grid(), BUILD_THREADS, lds, s>>>(a...);
+    }
 }
 
 // Region-window build: the prefetching kernel when a window fits IPT words per thread.
