@@ -241,12 +241,14 @@ KH_HD uint32_t key_hash32(Key k) {
 
 // ---- minimizer ---------------------------------------------------------------------------------
 // Window j (0 = the last M bases, K-M = the first M) = bits [2j, 2j + 2M) of V. Its order key is
-// (w[23:0] * C + (w >> 8)) mod 2^32 (one v_mad_u32_u24), top 26 bits; the minimizer is the
+// (w[23:0] * C + w) mod 2^32 (one v_mad_u32_u24 with w itself as the addend: the top 8 bits of
+// w enter the top of the key; an addend of w >> 8 cost a shift per window, ~36 VALU per scan in
+// the convert pass and in every walk hop), top 26 bits; the minimizer is the
 // window of smallest order, ties to the smallest j (j*). Packed result: order26 << 6 | j*. The
 // region and the owner rank hash the minimizer window's *content* (2M bits), never its order
 // (26 bits: distinct windows share values).
 static constexpr uint32_t MINI_C = 0x9E3779u;
-KH_HD uint32_t win_order(uint32_t w) { return ((w & 0xFFFFFFu) * MINI_C + (w >> 8)) >> 6; }
+KH_HD uint32_t win_order(uint32_t w) { return ((w & 0xFFFFFFu) * MINI_C + w) >> 6; }
 
 KH_HD uint32_t win_bits(Key k, int j, const KParams& p) {
     const int b = 2 * j;  // V = hi * 2^62 + lo
