@@ -34,7 +34,14 @@ WORKLOADS = {
     "c5": dict(k=51, n=200_000_000, len_min=2, len_max=16, single=0, seed=5199,
                gen=dict(n_long=8, long_len=1_000_000, front_starts=True),
                desc="C5: k=51, 200M synthetic k-mers per GPU, 8 chains of 10^6 k-mers + contigs "
-                    "U[2,16], start k-mers first in record order, table load 0.5"),
+                    "U[2,16], start k-mers first in record order"),
+    # BASELINE.json configs[4] hot-bucket half: 30% of the contigs carry one of 8 shared 16-mer
+    # motifs in every k-mer (the motifs are their minimizers: 60M k-mers share 8 minimizer
+    # windows, i.e. 8 placement regions / shard owners before the table remaps them)
+    "c5h": dict(k=51, n=200_000_000, len_min=8, len_max=200, single=0, seed=5198,
+                gen=dict(hot_permille=300, n_motifs=8),
+                desc="C5 hot-bucket: k=51, 200M synthetic k-mers per GPU, contigs U[8,200], 30% of "
+                     "them built around one of 8 shared minimizer motifs"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 BEST_PUBLISHED_OPS = 72.6e6    # k=51, 4 nodes x 128 ranks (512 CPU ranks)
@@ -162,6 +169,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--n", type=int, default=0, help="override k-mers per GPU")
+    ap.add_argument("--load", type=float, default=0.5,
+                    help="table load factor (kmer_hash.cpp:109 uses 0.5; SURVEY C5 names a 0.85 variant)")
     ap.add_argument("--cpu-sample", type=int, default=20_000_000,
                     help="k-mers for the serial CPU baseline sample (0 = skip the serial leg)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
@@ -195,7 +204,7 @@ def main():
     dptr = ctypes.c_void_p()
     kh._lib.check(L.kh_dev_malloc(ctypes.byref(dptr), host.nbytes, 0))
     kh._lib.check(L.kh_memcpy_htod(dptr, ctypes.c_void_p(host.ctypes.data), host.nbytes))
-    table = kh.KmerHashTable(k, n, 0.5, device=0)
+    table = kh.KmerHashTable(k, n, args.load, device=0)
 
     def step():
         table.clear()
@@ -275,7 +284,8 @@ def main():
         "ms_per_step_median": sorted(step_ms)[len(step_ms) // 2], "step_ms": step_ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": value / BEST_PUBLISHED_OPS, "dtype": "u64", "data": "synthetic",
         "config": {"workload": w["desc"], "k": k, "n_kmers_per_gpu": n, "contigs": nc,
-                   "lookups": nl, "parallelism": "1 GPU", "load_factor": 0.5,
+                   "lookups": nl, "parallelism": "1 GPU", "load_factor": args.load,
+                   "hot_regions": s["n_hot_regions"], "overflow_cas_keys": s["n_overflow"],
                    "vs_baseline_ref": "72.6e6 ops/s: reference best, k=51 human-chr14, "
                                       "4 nodes x 128 CPU ranks (BASELINE.md)"},
         "inserts_per_s": n / (ms / 1e3), "lookups_per_s": nl / (ms / 1e3),

@@ -33,7 +33,8 @@ class KhStats(ctypes.Structure):
         "n_dup", "n_full", "n_bad_ext", "n_missing", "n_cycle", "n_spin", "n_chunk_ovf")] + [
         (name, ctypes.c_double) for name in (
             "ms_insert", "ms_insert_kernel", "ms_walk", "ms_materialize")] + [("n_bad_base", c_u64)] + \
-            [(f, ctypes.c_double) for f in ("ms_build", "ms_walk_kernel")]
+            [(f, ctypes.c_double) for f in ("ms_build", "ms_walk_kernel")] + \
+            [(f, c_u64) for f in ("n_hot_regions", "n_overflow")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -108,6 +109,10 @@ _SIGS = {
     "kh_gen_create_skewed": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_int, c_u64, ctypes.c_uint32,
                                             ctypes.c_uint32, ctypes.c_uint32, c_u64, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]),
+    "kh_gen_create_hot": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_int, c_u64, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.c_uint32, c_u64, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.c_uint32, ctypes.c_uint32]),
     "kh_gen_destroy": (ctypes.c_int, [c_vp]),
     "kh_gen_num_contigs": (c_u64, [c_vp]),
     "kh_gen_records": (ctypes.c_int, [c_vp, c_u64, c_u64, c_vp]),

@@ -62,9 +62,11 @@ static uint64_t win_G(uint64_t n) {
     return (tiles_per_bucket + 1) / 2;
 }
 
-uint64_t part_count_words() { return (NW1 + NREG_MAX) / 2; }
+uint64_t part_count_words() { return (NW1 + 2 * NREG_MAX) / 2; }
 
-uint64_t part_overflow_cap(uint64_t n) { return n / 4 + 65536; }
+// Every word can miss its windows (a hot bucket fills all of its pass-1 windows): the list holds
+// the whole batch, so it never runs out while the table has free slots.
+uint64_t part_overflow_cap(uint64_t n) { return n + 65536; }
 
 // Window capacities. Regions are picked by minimizer, so a region's load is a sum of runs of
 // ~19 k-mers (compound Poisson: variance = mu * E[S^2]/E[S] ~ 30 mu at K=51, M=16: C3 sd 210 for
@@ -360,7 +362,7 @@ __device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long
             // the walker reads a record at the region of the key it looked up: in a slice reloaded
             // from the table only keys of this region may own one (others may have spilled in)
             const Key hk = slot_key(w0, W == 2 ? lt[W * i + 1] & LO_MASK : 0ull, p);
-            own = mini_region(mini_window(hk, mini_scan(hk, p), p), p) == r;
+            own = place_w(mini_window(hk, mini_scan(hk, p), p), hk, p).r == r;
         }
         if (!own) {
             lt[W * i] = slot_clean(w0, p);  // no record: the walker steps this k-mer itself
@@ -450,8 +452,9 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
             }
             // every word of region r's window is a key of region r; the slot keeps key, ext and j*
             const uint64_t home = home_in(lo, hi, key_hash32(slot_key(w0, w1, p)));
-            if (lds_insert<W>(p, lt, S, home - lo, slot_clean(w0, p), w1, stats) == LDS_OUT) {
-                const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
+            const bool out = lds_insert<W>(p, lt, S, home - lo, slot_clean(w0, p), w1, stats) == LDS_OUT;
+            const unsigned long long idx = wave_reserve(&ctr[CT_OVF2], out);
+            if (out) {
                 if (idx < ovf_cap) {
                     ovf[idx * W] = w0;
                     if (W == 2) ovf[idx * W + 1] = w1;
@@ -568,8 +571,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             // (the order bits stay in the register copy for the link test)
             const uint64_t home = home_in(lo, hi, key_hash32(slot_key(a[j], b[j], p)));
             pos[j] = lds_insert<W>(p, lt, S, home - lo, slot_clean(a[j], p), b[j], stats);
+            const unsigned long long idx = wave_reserve(&ctr[CT_OVF2], pos[j] == LDS_OUT);
             if (pos[j] == LDS_OUT) {
-                const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
                 if (idx < ovf_cap) {
                     ovf[idx * W] = a[j];
                     if (W == 2) ovf[idx * W + 1] = b[j];
@@ -674,26 +677,26 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_build_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, s);
     }
     if (debug_flag("plain_build"))  // tests: the large-window kernel at small sizes
-        k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap, ctr,
+        k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
                                                          stats, RC, rcnt, B.headrec, hcap, smax);
     else if (RC <= 4u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 4, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.overflow, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 4, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else if (RC <= 6u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 6, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.overflow, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 6, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else if (RC <= 12u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 12, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.overflow, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 12, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
                                                                 ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
     else
-        k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.overflow, ovf_cap, ctr,
+        k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
                                                          stats, RC, rcnt, B.headrec, hcap, smax);
     if (prof) {
         unsigned long long v[8];
         (void)hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_build_prof), sizeof v, 0, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
         unsigned long long novf = 0;
-        (void)hipMemcpyAsync(&novf, ctr + CT_OVF, 8, hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(&novf, ctr + CT_OVF2, 8, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
         fprintf(stderr, "build_prof (s_memtime, summed over blocks): slice-init %llu insert %llu link %llu "
                         "heads %llu walk+rec %llu write %llu | RC %u overflow %llu\n", v[0], v[1], v[2], v[3], v[4],
@@ -705,7 +708,7 @@ template <int W>
 __global__ __launch_bounds__(PB) void k_insert_overflow(KParams p, const uint64_t* ovf, uint64_t ovf_cap,
                                                         const unsigned long long* ctr, uint64_t* slots,
                                                         uint64_t cap, unsigned long long* stats) {
-    const uint64_t m = min((uint64_t)ctr[CT_OVF], ovf_cap);
+    const uint64_t m = min((uint64_t)ctr[CT_OVF2], ovf_cap);
     for (uint64_t i = (uint64_t)blockIdx.x * PB + threadIdx.x; i < m; i += (uint64_t)gridDim.x * PB) {
         const uint64_t w0 = ovf[i * W], w1 = (W == 2) ? ovf[i * W + 1] : 0;
         // overflow words come from the partition passes: their j* gives the placement hash
@@ -802,7 +805,9 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
                                                    unsigned long long* ctr, unsigned long long* stats, NextF next) {
     constexpr int IPT = TILE / TB;
     static_assert(NB <= TB, "one bin per thread");
+    __shared__ uint32_t spill;  // some bin's run passes its window's end (block-uniform after the barrier)
     if (threadIdx.x < NB) hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) spill = 0;
     lds_barrier();
     uint32_t rank[IPT];
 #pragma unroll
@@ -813,7 +818,9 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
     const uint32_t st = block_scan_u32<TB>(hv, total, wsum);
     if (threadIdx.x < NB) {
         start[threadIdx.x] = st;
-        gpos[threadIdx.x] = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
+        const uint32_t g = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
+        gpos[threadIdx.x] = g;
+        if (hv && g + hv > cap) spill = 1;
     }
     lds_barrier();
 #pragma unroll
@@ -832,21 +839,29 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
     for (uint32_t x = threadIdx.x; x < total; x += TB) {
         const uint32_t q = sbin[x];
         const uint32_t w = gpos[q] + (x - start[q]);
-        const uint64_t v0 = items[W * x], v1 = (W == 2) ? items[W * x + 1] : 0;
         if (w < cap) {
+            const uint64_t v0 = items[W * x], v1 = (W == 2) ? items[W * x + 1] : 0;
             const uint64_t g = window(q) + w;
             if (W == 2) {
                 *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(v0, v1);
             } else {
                 out[g] = v0;
             }
-        } else {
-            const unsigned long long idx = atomicAdd(&ctr[CT_OVF], 1ull);
-            if (idx < ovf_cap) {
-                ovf[idx * W] = v0;
-                if (W == 2) ovf[idx * W + 1] = v1;
-            } else {
-                atomicAdd(&stats[ST_FULL], 1ull);
+        }
+    }
+    if (spill) {  // full windows: the overflow list, one reservation per wave (a hot bucket spills whole tiles)
+        for (uint32_t x0 = threadIdx.x & ~63u; x0 < total; x0 += TB) {
+            const uint32_t x = x0 + (threadIdx.x & 63u);
+            const uint32_t q = x < total ? sbin[x] : 0u;
+            const bool sp = x < total && gpos[q] + (x - start[q]) >= cap;
+            const unsigned long long idx = wave_reserve(&ctr[CT_OVF], sp);
+            if (sp) {
+                if (idx < ovf_cap) {
+                    ovf[idx * W] = items[W * x];
+                    if (W == 2) ovf[idx * W + 1] = items[W * x + 1];
+                } else {
+                    atomicAdd(&stats[ST_FULL], 1ull);
+                }
             }
         }
     }
@@ -1148,6 +1163,118 @@ static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n
     });
 }
 
+// ---- hot regions ---------------------------------------------------------------------------------
+// A minimizer window shared by far more k-mers than a region holds (a repeat family, a low-complexity
+// run; the C5 hot-bucket set) would pile its whole family into one ~3K-slot slice: the window
+// overflows, the slice fills, and every spilled key linear-probes from inside the full slice. The
+// fixup between pass 2 and the build remaps such regions as a whole (kh_codec.hpp place_w): keys of a
+// remapped region go to the region of a second mix of their key hash, i.e. evenly over all regions,
+// and every lookup (find, walk, CAS insert) places keys the same way from the bitmap.
+//   k_hot_mark     region r is remapped when it already was, or (an empty table's build) when its
+//                  count exceeds what its window (RC) or its slice (S_r slots) holds; the bitmap is
+//                  rewritten and the remapped regions listed (CT_HOT)
+//   k_hot_gather   the listed regions' window words join the overflow list; their windows empty
+//   k_ovf_scatter  every overflow-list word goes to the window of its (remapped) region; what does
+//                  not fit goes to list B (buf1, CT_OVF2), which the global CAS insert takes
+// Cost without hot regions: three launches over nothing (~15 us); words move only for remapped
+// regions and for windows that were full.
+template <int Unused = 0>
+__global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint32_t RC, int slack16,
+                                                  const uint32_t* rcnt, uint32_t* hot, uint32_t* hot_list,
+                                                  unsigned long long* ctr, int allow_new) {
+    const uint32_t NR = nreg(p);
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    bool h = false;
+    if (r < NR) {
+        const uint32_t S = (uint32_t)(region_lo(r + 1, cap, p) - region_lo(r, cap, p));
+        const uint32_t T = min(RC, S - (slack16 ? S / 16u : 0u));
+        h = ((hot[r >> 5] >> (r & 31u)) & 1u) || (allow_new && rcnt[r] > T);
+    }
+    const uint64_t m = __ballot(h);
+    const uint32_t lane = lane_id();
+    const uint32_t r0 = r - lane;  // the wave's 64 regions: two bitmap words
+    if (r0 < NR && (lane == 0 || lane == 32)) hot[(r0 >> 5) + (lane >> 5)] = (uint32_t)(m >> lane);
+    const unsigned long long i = wave_reserve(&ctr[CT_HOT], h);
+    if (h) hot_list[i] = r;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_hot_gather(uint32_t RC, uint32_t* rcnt, const uint32_t* hot_list,
+                                                    const uint64_t* __restrict__ buf2, uint64_t* ovf, uint64_t ovf_cap,
+                                                    unsigned long long* ctr, unsigned long long* stats) {
+    __shared__ unsigned long long base;
+    const uint64_t nh = ctr[CT_HOT];
+    for (uint64_t i = blockIdx.x; i < nh; i += gridDim.x) {
+        const uint32_t r = hot_list[i];
+        const uint32_t m = min(rcnt[r], RC);
+        if (threadIdx.x == 0) base = m ? atomicAdd(&ctr[CT_OVF], (unsigned long long)m) : 0ull;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < m; j += 256) {
+            const uint64_t d = base + j;
+            if (d >= ovf_cap) {
+                atomicAdd(&stats[ST_FULL], 1ull);
+                continue;
+            }
+            const uint64_t g = (uint64_t)r * RC + j;
+            if (W == 2) {
+                *reinterpret_cast<ulonglong2*>(ovf + d * 2) = *reinterpret_cast<const ulonglong2*>(buf2 + g * 2);
+            } else {
+                ovf[d] = buf2[g];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) rcnt[r] = 0;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ovf_scatter(KParams p, uint32_t RC, uint32_t* rcnt,
+                                                     const uint64_t* __restrict__ ovf, uint64_t ovf_cap, uint64_t* buf2,
+                                                     uint64_t* ovf2, uint64_t ovf2_cap, unsigned long long* ctr,
+                                                     unsigned long long* stats) {
+    const uint64_t m = min((uint64_t)ctr[CT_OVF], ovf_cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+        uint64_t w0, w1 = 0;
+        if (W == 2) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(ovf + i * 2);
+            w0 = v.x;
+            w1 = v.y;
+        } else {
+            w0 = ovf[i];
+        }
+        const uint32_t r = word_place(w0, w1, p).r;  // remapped regions: the key-hash region
+        const uint32_t pos = wave_count_add(rcnt, r, true);
+        if (pos < RC) {
+            const uint64_t g = (uint64_t)r * RC + pos;
+            if (W == 2) {
+                *reinterpret_cast<ulonglong2*>(buf2 + g * 2) = make_ulonglong2(w0, w1);
+            } else {
+                buf2[g] = w0;
+            }
+        }
+        const unsigned long long d = wave_reserve(&ctr[CT_OVF2], pos >= RC);
+        if (pos >= RC) {
+            if (d < ovf2_cap) {
+                ovf2[d * W] = w0;
+                if (W == 2) ovf2[d * W + 1] = w1;
+            } else {
+                atomicAdd(&stats[ST_FULL], 1ull);
+            }
+        }
+    }
+}
+
+template <int W>
+static void hot_fixup(const KParams& p, uint64_t cap, uint32_t RC, bool allow_new, const PartBuffers& B,
+                      uint64_t ovf_cap, uint64_t ovf2_cap, unsigned long long* ctr, unsigned long long* stats,
+                      hipStream_t s) {
+    KParams q = p;
+    q.hot = B.hot;
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, B.rcnt, B.hot, B.hot_list, ctr, allow_new ? 1 : 0);
+    k_hot_gather<W><<<1024, 256, 0, s>>>(RC, B.rcnt, B.hot_list, B.buf2, B.overflow, ovf_cap, ctr, stats);
+    k_ovf_scatter<W><<<2048, 256, 0, s>>>(q, RC, B.rcnt, B.overflow, ovf_cap, B.buf2, B.buf1, ovf2_cap, ctr, stats);
+}
+
 template <int W>
 static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bool table_empty, const PartBuffers& B,
                                unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
@@ -1166,9 +1293,55 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
          })) != hipSuccess)
         return e;
     const uint32_t RC = part_region_cap(p, total);
-    launch_build_windows<W>(p, B, t, table_empty, part_overflow_cap(total), ctr, stats, RC,
+    const uint64_t ovf2_cap = part_buf1_words(p, total) / p.W;  // list B lives in buf1 (dead after pass 2)
+    if ((e = hipMemsetAsync(ctr + CT_OVF2, 0, 16, s)) != hipSuccess) return e;  // CT_OVF2, CT_HOT
+    static_assert(CT_HOT == CT_OVF2 + 1, "counter layout");
+    hot_fixup<W>(p, t.cap, RC, table_empty, B, part_overflow_cap(total), ovf2_cap, ctr, stats, s);
+    KParams q = p;  // the build and the CAS inserts place keys of remapped regions by key hash
+    q.hot = B.hot;
+    launch_build_windows<W>(q, B, t, table_empty, ovf2_cap, ctr, stats, RC,
                             reinterpret_cast<const uint32_t*>(B.rcnt), lds, s);
-    k_insert_overflow<W><<<1024, PB, 0, s>>>(p, B.overflow, part_overflow_cap(total), ctr, t.slots, t.cap, stats);
+    k_insert_overflow<W><<<1024, PB, 0, s>>>(q, B.buf1, ovf2_cap, ctr, t.slots, t.cap, stats);
+    return hipGetLastError();
+}
+
+// ---- CAS-path hot prepass --------------------------------------------------------------------------
+template <int W, bool REC>
+__global__ __launch_bounds__(256) void k_region_count(KParams p, const uint8_t* __restrict__ recs,
+                                                      const uint64_t* __restrict__ words, uint64_t n, uint32_t* rcnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        uint32_t win;
+        if (REC) {
+            Key k;
+            uint32_t ext;
+            parse_record(recs + i * (uint64_t)p.R, p, k, ext);
+            win = mini_window(k, mini_scan(k, p), p);
+        } else {
+            const uint64_t w0 = words[i * W], w1 = W == 2 ? words[i * W + 1] : 0ull;
+            win = word_mini_window(w0, w1, p);
+        }
+        (void)wave_count_add(rcnt, mini_region(win, p), true);
+    }
+}
+
+hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
+                              uint64_t cap, uint32_t* rcnt, uint32_t* hot, uint32_t* hot_list,
+                              unsigned long long* ctr, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 8, s)) != hipSuccess) return e;
+    if (n) {
+        const unsigned grid = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+        if (p.W == 2) {
+            if (recs) k_region_count<2, true><<<grid, 256, 0, s>>>(p, recs, nullptr, n, rcnt);
+            else k_region_count<2, false><<<grid, 256, 0, s>>>(p, nullptr, words, n, rcnt);
+        } else {
+            if (recs) k_region_count<1, true><<<grid, 256, 0, s>>>(p, recs, nullptr, n, rcnt);
+            else k_region_count<1, false><<<grid, 256, 0, s>>>(p, nullptr, words, n, rcnt);
+        }
+    }
+    // linear probing across region boundaries: remap what would fill more than 15/16 of a slice
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(p, cap, 0xFFFFFFFFu, 1, rcnt, hot, hot_list, ctr, 1);
     return hipGetLastError();
 }
 

@@ -100,6 +100,7 @@ struct kh_table {
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
     DevBuf headrec;                           // chain head records (region build -> walker)
+    DevBuf hot;                               // remapped-region bitmap (KParams::hot), HOT_WORDS words
     uint32_t hcap = 0;                        // head records per region (0 = no chains)
     bool last_insert_part = false;
     bool staging = false, stage_part = false, stage_fresh = false;  // kh_insert_words_stage_dev build
@@ -115,6 +116,7 @@ struct kh_table {
     uint64_t mw_store_n = 0;   // text records in mw_store
     uint32_t mw_P = 0, mw_rank = 0;
     bool mw_live = false, mw_stepped = false;
+    bool mw_hot = true;        // the shard has remapped regions (the walk reads the bitmap)
     uint64_t rw_n = 0, rw_total = 0;  // migrating walk: local walkers, bound on contig length
     uint64_t starts_cap = 0;                 // start entries the starts buffer holds
     uint64_t splits_cap = 0, splits_w_cap = 0;
@@ -225,13 +227,28 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     b.buf2 = t->pb_buf2.as<uint64_t>();
     b.wcnt = t->pb_cnt.as<uint32_t>();
     b.rcnt = b.wcnt + kh::PART_W1_COUNTERS;
+    b.hot_list = b.rcnt + kh::HOT_WORDS * 32;
     b.overflow = t->pb_ovf.as<uint64_t>();
+    b.hot = t->hot.as<uint32_t>();
     // chain head records: sized by the table (regions x records per region), kept across builds
     const uint32_t hcap = kh::debug_flag("no_chains") ? 0u : kh::part_head_cap(t->kp, t->cap);
     if (hcap && (rc = t->headrec.ensure((uint64_t)hcap * (1ull << t->kp.rbits) * 16))) return rc;
     t->hcap = hcap;
     b.headrec = hcap ? t->headrec.as<uint64_t>() : nullptr;
     b.hcap = hcap;
+    return KH_OK;
+}
+
+// CAS-path insert into an empty table: remap the minimizer regions the batch would overfill
+// (kh_build.hip launch_hot_prepass); later batches place keys with the same bitmap.
+int cas_hot_prepass(kh_table* t, const void* recs, const void* words, uint64_t n) {
+    if (t->n_inserted != 0 || kh::debug_flag("no_hot")) return KH_OK;
+    if (int rc = t->pb_cnt.ensure(kh::part_count_words() * 8)) return rc;
+    uint32_t* rcnt = t->pb_cnt.as<uint32_t>() + kh::PART_W1_COUNTERS;
+    KH_HIP(hipMemsetAsync(t->hot.p, 0, kh::HOT_WORDS * 4, t->stream));
+    KH_HIP(kh::launch_hot_prepass(t->kp, (const uint8_t*)recs, (const uint64_t*)words, n, t->cap, rcnt,
+                                  t->hot.as<uint32_t>(), rcnt + kh::HOT_WORDS * 32, t->ctr.as<unsigned long long>(),
+                                  t->stream));
     return KH_OK;
 }
 
@@ -309,6 +326,8 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
         if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
             return bail(fail(KH_ERR_HIP, "hipEventCreate failed"));
     if ((rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8))) return bail(rc);
+    if ((rc = t->hot.ensure(kh::HOT_WORDS * 4))) return bail(rc);
+    t->kp.hot = t->hot.as<uint32_t>();
     if ((rc = t->ctr.ensure(kh::CT_NUM * 8))) return bail(rc);
     if ((rc = t->stats.ensure(kh::ST_NUM * 8))) return bail(rc);
     if ((rc = kh_clear(t))) return bail(rc);
@@ -330,7 +349,7 @@ int kh_destroy(kh_table* t) {
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
-                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec};
+                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot};
     for (auto* b : bufs) b->release();
     if (t->side) (void)hipStreamSynchronize(t->side);
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_b0,
@@ -374,6 +393,7 @@ int kh_clear(kh_table* t) {
     t->slots_stale = true;
     KH_HIP(hipMemsetAsync(t->ctr.p, 0, kh::CT_NUM * 8, t->stream));
     KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
+    KH_HIP(hipMemsetAsync(t->hot.p, 0, kh::HOT_WORDS * 4, t->stream));  // placement by minimizer again
     t->n_inserted = 0;
     t->assembled = false;
     t->split_ok = true;
@@ -422,7 +442,7 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     kh::PartBuffers pb{};
     if (part && (rc = ensure_part(t, n, pb))) return rc;
     // a partitioned build into a fresh table rewrites every slot: no clear needed
-    const bool fresh = part && t->n_inserted == 0 && t->slots_stale;
+    const bool fresh = part && t->n_inserted == 0;  // empty (stale or clean): the build writes every slot
     if (!fresh && (rc = clean_slots(t))) return rc;
     t->slots_stale = false;
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
@@ -438,9 +458,11 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
                                       t->stats.as<unsigned long long>(), t->stream,
                                       overlap ? t->ev_conv : nullptr, nullptr, 0, t->ev_b0));
         KH_HIP(hipEventRecord(t->ev_b1, t->stream));
-    } else
+    } else {
+        if ((rc = cas_hot_prepass(t, dev_recs, nullptr, n))) return rc;
         KH_HIP(kh::launch_insert(t->kp, (const uint8_t*)dev_recs, n, view(t), t->mask.as<uint64_t>(),
                                  split_mask, t->stats.as<unsigned long long>(), t->stream));
+    }
     t->last_insert_part = part;
     if (overlap) KH_HIP(hipStreamWaitEvent(t->side, t->ev_conv, 0));
     KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
@@ -536,6 +558,7 @@ int kh_assemble_dev(kh_table* t) {
     uint64_t nsp = 0;
     const unsigned long long* nsp_dev = nullptr;
     kh::KParams kp = t->kp;
+    if (!cv[kh::CT_HOT]) kp.hot = nullptr;  // no remapped region: the walker skips the bitmap load
     if (kp.split_bits && t->split_ok)
         nsp = cv[kh::CT_N_SPLIT];
     else
@@ -751,6 +774,8 @@ int kh_get_stats(kh_table* t, kh_stats* s) {
         if (t->wk_timed && hipEventElapsedTime(&ms, t->ev_walk0, t->ev_wk1) == hipSuccess) s->ms_walk_kernel = ms;
     }
     if (t->build_timed && hipEventElapsedTime(&ms, t->ev_b0, t->ev_b1) == hipSuccess) s->ms_build = ms;
+    s->n_hot_regions = ct[kh::CT_HOT];
+    s->n_overflow = t->last_insert_part ? ct[kh::CT_OVF2] : 0;
     (void)hipGetLastError();  // a failed elapsed-time query is not the caller's error
     return KH_OK;
 }
@@ -924,7 +949,7 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     kh::PartBuffers pb{};
     if (part)
         if (int rc = ensure_part(t, m, pb)) return rc;
-    const bool fresh = part && t->n_inserted == 0 && t->slots_stale;
+    const bool fresh = part && t->n_inserted == 0;  // empty (stale or clean): the build writes every slot
     if (!fresh)
         if (int rc = clean_slots(t)) return rc;
     t->slots_stale = false;
@@ -934,9 +959,11 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
                                       fresh, pb, nullptr, nullptr, t->ctr.as<unsigned long long>(),
                                       t->stats.as<unsigned long long>(), t->stream, nullptr,
                                       coll ? t->splits.as<uint64_t>() : nullptr, coll ? t->splits_cap : 0));
-    else
+    else {
+        if (int rc = cas_hot_prepass(t, nullptr, words, m)) return rc;
         KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
                                        t->stats.as<unsigned long long>(), t->stream));
+    }
     t->last_insert_part = part;
     KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
     KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
@@ -964,7 +991,7 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
         if (t->stage_part)
             if (int rc = ensure_part(t, total_hint, pb)) return rc;
         // a partitioned build into a fresh table rewrites every slot: no clear needed
-        t->stage_fresh = t->stage_part && t->n_inserted == 0 && t->slots_stale;
+        t->stage_fresh = t->stage_part && t->n_inserted == 0;
         if (!t->stage_fresh)
             if (int rc = clean_slots(t)) return rc;
         KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
@@ -991,6 +1018,8 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
                                      t->stream, coll ? t->splits.as<uint64_t>() : nullptr,
                                      coll ? t->splits_cap : 0));
     } else {
+        if (t->stage_n == 0)
+            if (int rc = cas_hot_prepass(t, nullptr, words, m)) return rc;
         KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
                                        t->stats.as<unsigned long long>(), t->stream));
     }
@@ -1057,8 +1086,9 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     if (int rc = set_device(t)) return rc;
     if (int rc = clean_slots(t)) return rc;
     int rc;
-    uint64_t ns = 0;
-    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns))) return rc;
+    uint64_t ns = 0, nhot = 0;
+    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns)) || (rc = read_ctr(t, kh::CT_HOT, &nhot))) return rc;
+    t->mw_hot = nhot != 0;
     if (ns >= (1ull << 31)) return fail(KH_ERR_ARG, "%llu start k-mers on one rank (max 2^31)", (unsigned long long)ns);
     // splitter segments: every splitter this shard owns seeds a walker too (kh_mseg.hip)
     // on or off the same way on every rank (walkers stop before splitters owned anywhere)
@@ -1265,7 +1295,9 @@ int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, vo
     mw.dst = t->mw_dst.as<uint8_t>();
     mw.stage = t->mw_stage.as<uint64_t>();
     mw.nrec = t->mw_nrec.as<uint8_t>();
-    KH_HIP(kh::launch_mw_run(t->kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
+    kh::KParams kp = t->kp;
+    if (!t->mw_hot) kp.hot = nullptr;
+    KH_HIP(kh::launch_mw_run(kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
     // text records of this round -> the rank-local store (the host needs their count to size it)
     unsigned long long* tot = t->mw_misc.as<unsigned long long>();
     KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), tot, t->stream));

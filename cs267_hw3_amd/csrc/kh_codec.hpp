@@ -59,6 +59,10 @@ struct KParams {
     int chain;          // word0 has room for j* and a head-record index (chain links, kh_build.hip)
     int idx_lo;         // first bit of the head-record index field in word0 (field = [idx_lo, 57))
     int rbits;          // placement regions = 2^rbits (9..17, by table size: set_region_bits)
+    // device bitmap of remapped ("hot") regions, one bit per region (nullptr = none): a region
+    // whose minimizer windows bring more k-mers than its window or slice holds has all its keys
+    // placed by a hash of the whole key instead (kh_build.hip k_hot_mark; place_w)
+    const uint32_t* hot;
 };
 
 // Minimizer length: consecutive k-mers of a contig share their minimizer for ~(K-M+2)/2 steps on
@@ -92,6 +96,7 @@ inline KParams make_params(int K) {
     // chain links need j* (6 bits, K-M+1 <= 49 windows) and an index field of >= 8 bits
     p.chain = (SCRATCH_BIT - p.idx_lo >= 8) && K >= 14 ? 1 : 0;
     p.rbits = REGION_BITS_MAX;
+    p.hot = nullptr;
     return p;
 }
 
@@ -322,7 +327,18 @@ KH_HD uint64_t home_in(uint64_t lo, uint64_t hi, uint32_t h) { return lo + (((hi
 struct Place {
     uint32_t r, h;  // region, key_hash32
 };
-KH_HD Place place_w(uint32_t win, Key k, const KParams& p) { return Place{mini_region(win, p), key_hash32(k)}; }
+// Hot regions (a repeat family, a low-complexity run, the C5 hot-bucket set: one minimizer window
+// shared by far more k-mers than a region holds) are remapped as a whole: their keys go to the
+// region of a second mix of the key hash, so they spread evenly over every region (the home
+// inside it is still home_in(.., key_hash32): the extra mix keeps region and home independent).
+KH_HD uint32_t hot_region(uint32_t h, const KParams& p) { return mix32(h ^ 0x2545F491u) >> (32 - p.rbits); }
+KH_HD bool region_is_hot(const uint32_t* hot, uint32_t r) { return hot && ((hot[r >> 5] >> (r & 31u)) & 1u); }
+KH_HD Place place_w(uint32_t win, Key k, const KParams& p) {
+    uint32_t r = mini_region(win, p);
+    const uint32_t h = key_hash32(k);
+    if (region_is_hot(p.hot, r)) r = hot_region(h, p);
+    return Place{r, h};
+}
 KH_HD Place place(Key k, const KParams& p) { return place_w(mini_window(k, mini_scan(k, p), p), k, p); }
 KH_HD uint64_t home_of(Place pl, uint64_t cap, const KParams& p) {
     return home_in(region_lo(pl.r, cap, p), region_lo(pl.r + 1, cap, p), pl.h);

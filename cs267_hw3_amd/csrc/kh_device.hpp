@@ -34,6 +34,37 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// One slot of a global list per lane that wants one, with ONE atomicAdd per wave on the list's
+// counter (a hot region spilling thousands of words per wave would otherwise serialise on a single
+// address). Call with every lane of the wave that reached this point; returns the lane's slot.
+__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* counter, bool want) {
+    const uint64_t m = __ballot(want);
+    if (!m) return 0ull;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    unsigned long long base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + mbcnt64(m);
+}
+
+// atomicAdd(&cnt[key], 1) for every lane that wants it. The lanes sharing the first lane's key are
+// served by one atomic (a hot region's words arrive whole waves at a time: ~1 atomic per wave
+// instead of 64 on one address); the others issue their own, all in flight at once (distinct
+// random keys: one round trip, not one per key).
+__device__ __forceinline__ uint32_t wave_count_add(uint32_t* cnt, uint32_t key, bool want) {
+    const uint64_t act = __ballot(want);
+    if (!act) return 0u;
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const uint32_t lk = __shfl(key, leader, 64);
+    const uint64_t grp = __ballot(want && key == lk);
+    const bool in_grp = (grp >> lane_id()) & 1ull;
+    uint32_t old = 0;
+    if ((int)lane_id() == leader) old = atomicAdd(&cnt[lk], (uint32_t)__popcll(grp));
+    old = __shfl(old, leader, 64);
+    if (in_grp) return old + mbcnt64(grp);
+    return want ? atomicAdd(&cnt[key], 1u) : 0u;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Block-wide exclusive scan of one uint64 per thread (256 threads = 4 waves of 64).
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its

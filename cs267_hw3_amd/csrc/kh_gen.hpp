@@ -76,6 +76,9 @@ KH_HD uint64_t upper_index(const uint64_t* a, uint64_t m, uint64_t x) {
     return lo - 1;
 }
 
+// Hot-minimizer stress (BASELINE configs[4] "hot-bucket"): up to this many shared M-mer motifs.
+static constexpr int GEN_MAX_MOTIFS = 64;
+
 // The generator's parameters and per-contig arrays (host or device pointers).
 struct GenView {
     int K = 0;
@@ -87,11 +90,39 @@ struct GenView {
     const uint32_t* salt = nullptr;   // re-draw counter per contig [C] (uniqueness)
     const uint64_t* nb = nullptr;     // front_starts: non-start k-mers before contig i [C]
     Perm perm, perm_s, perm_n;
+    // Hot contigs (hot_pm per mille of contigs, chosen by a hash of the contig index): the motif
+    // motif[h] (M bases, first base in the top bits) is planted at every position j with
+    // j % period < M, period = K - M + 1 when that leaves >= 8 free bases between occurrences
+    // (k=51: every k-mer of the contig holds exactly one full occurrence), else K (k=19, 31).
+    // The motifs are the M-mers of smallest minimizer order among 2^16 seeded draws,
+    // so the occurrence is (almost always) the k-mer's minimizer: all k-mers of the hot contigs
+    // of motif h share one minimizer window, one placement region and one shard owner.
+    uint32_t hot_pm = 0, n_motifs = 0, period = 0, M = 0;
+    uint32_t motif[GEN_MAX_MOTIFS] = {};
 
+    KH_HD uint64_t hot_hash(uint64_t i) const { return splitmix(seed ^ 0x3f84d5b5b5470917ull ^ (i * 0xd1b54a32d192ed03ull)); }
+    // motif index of contig i, or -1 when the contig is not hot
+    KH_HD int hot_motif(uint64_t i) const {
+        if (!hot_pm) return -1;
+        const uint64_t h = hot_hash(i);
+        return (h % 1000) < hot_pm ? (int)((h >> 32) % n_motifs) : -1;
+    }
     // 32 bases of contig i per 64-bit word: base j = bits 2(j%32).. of word(i, j/32).
     KH_HD uint64_t word(uint64_t i, uint64_t b) const {
-        return splitmix(splitmix(seed ^ 0x6a09e667f3bcc908ull ^ (i * 0x9e3779b97f4a7c15ull)) ^
-                        ((uint64_t)salt[i] << 40) ^ b);
+        uint64_t r = splitmix(splitmix(seed ^ 0x6a09e667f3bcc908ull ^ (i * 0x9e3779b97f4a7c15ull)) ^
+                              ((uint64_t)salt[i] << 40) ^ b);
+        const int h = hot_motif(i);
+        if (h < 0) return r;
+        const uint32_t mo = motif[h];
+        uint32_t q = (uint32_t)((b * 32) % period);
+        for (int x = 0; x < 32; ++x) {
+            if (q < M) {
+                const uint64_t base = (mo >> (2 * (M - 1 - q))) & 3u;
+                r = (r & ~(3ull << (2 * x))) | (base << (2 * x));
+            }
+            if (++q == period) q = 0;
+        }
+        return r;
     }
     KH_HD uint32_t base(uint64_t i, uint64_t j) const { return (uint32_t)(word(i, j >> 5) >> (2 * (j & 31))) & 3u; }
     // k-mer t of contig i as (hi, lo) plus the ext code.

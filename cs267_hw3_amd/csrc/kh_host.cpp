@@ -180,10 +180,19 @@ int kh_gen_create(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t le
 int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
                          uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
                          uint32_t long_len, int front_starts) {
+    return kh_gen_create_hot(out, k, n, len_min, len_max, single_permille, seed, shuffle, threads, n_long, long_len,
+                             front_starts, 0, 0);
+}
+
+int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
+                      uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
+                      uint32_t long_len, int front_starts, uint32_t hot_permille, uint32_t n_motifs) {
     if (!out) return hfail(KH_ERR_ARG, "out is NULL");
     *out = nullptr;
     if (k < 1 || k > KH_K_MAX || len_min < 1 || len_max < len_min || single_permille > 1000)
         return hfail(KH_ERR_ARG, "bad generator parameters");
+    if (hot_permille > 1000 || (hot_permille && (n_motifs < 1 || n_motifs > (uint32_t)kh::GEN_MAX_MOTIFS)))
+        return hfail(KH_ERR_ARG, "bad hot-motif parameters (hot_permille <= 1000, 1 <= n_motifs <= 64)");
     kh_gen* g = new (std::nothrow) kh_gen();
     if (!g) return hfail(KH_ERR_NOMEM, "host allocation failed");
     kh::GenView& v = g->v;
@@ -193,6 +202,31 @@ int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint
     v.seed = seed;
     v.shuffle = shuffle != 0;
     g->threads = pick_threads(threads);
+    if (hot_permille && v.kp.M < k) {
+        // motifs: per motif the M-mer of smallest minimizer order among 2^16 seeded draws
+        v.hot_pm = hot_permille;
+        v.n_motifs = n_motifs;
+        v.M = (uint32_t)v.kp.M;
+        // every k-mer holds a full occurrence when the period is K - M + 1, which needs
+        // K >= 2M + 7 to leave 8 free bases between occurrences (k=51: 20); shorter k (19, 31)
+        // plant one motif per K bases: every k-mer keeps K - M free bases (4^7 at k=19) and
+        // K - M + 1 of the K phases hold a full occurrence
+        const uint32_t full = (uint32_t)(k - v.kp.M + 1);
+        v.period = full >= v.M + 8 ? full : (uint32_t)k;
+        const uint32_t mmask = (uint32_t)((1ull << (2 * v.M)) - 1);
+        for (uint32_t h = 0; h < n_motifs; ++h) {
+            uint32_t best = 0, bo = 0xFFFFFFFFu;
+            for (uint32_t t = 0; t < (1u << 16); ++t) {
+                const uint32_t c = (uint32_t)kh::splitmix(seed ^ 0x7a5c9e1bd4f30c2dull ^ ((uint64_t)h << 20) ^ t) & mmask;
+                const uint32_t o = kh::win_order(c);
+                if (o < bo) {
+                    bo = o;
+                    best = c;
+                }
+            }
+            v.motif[h] = best;
+        }
+    }
     // 1) contig lengths until n k-mers (last one truncated); the first n_long contigs have
     //    long_len k-mers (C5: a handful of 10^6-k-mer chains among short contigs)
     uint64_t sum = 0;
@@ -221,8 +255,16 @@ int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint
     // 2) uniqueness: re-draw every contig holding a k-mer that occurs more than once, until none.
     //    Skipped when the expected number of repeats n^2 / (2 * 4^k) is below 1e-9 (k=51 and
     //    anything below 10^12 k-mers); the table's duplicate counter still checks it on insert.
+    //    Hot contigs draw only K - M bases per k-mer (one of n_motifs motifs at one of `period`
+    //    phases): their expected repeats are counted on that space (checked above 1e-6; the
+    //    table's duplicate counter still reports any on insert).
     const double expect = (double)n * (double)n / 2.0 / __builtin_powi(4.0, k);
-    if (expect > 1e-9 && n > 1) {
+    double expect_hot = 0.0;
+    if (v.hot_pm) {
+        const double nh = (double)n * v.hot_pm / 1000.0;
+        expect_hot = nh * nh / 2.0 / ((double)v.n_motifs * v.period * __builtin_powi(4.0, k - (int)v.M));
+    }
+    if ((expect > 1e-9 || expect_hot > 1e-6) && n > 1) {
         const uint64_t C = g->len.size();
         std::vector<uint8_t> redo(C, 1);
         for (int round = 0; round < 256; ++round) {

@@ -33,7 +33,10 @@ enum CtrIdx : int {
     CT_MW_FIN = 5,     // migrating walk: finish records received by the origin
     CT_N_SPLIT = 6,    // splitter k-mers collected (walk segments beyond the contig starts)
     CT_N_SPLIT_W = 7,  // splitters of the walk subset (denser collection filtered at assemble)
-    CT_NUM = 8
+    CT_OVF2 = 8,       // partitioned build: keys left for the global CAS insert (full windows, probe
+                       // runs that left their slice) after the hot-region fixup
+    CT_HOT = 9,        // remapped ("hot") placement regions of the table (kh_build.hip k_hot_mark)
+    CT_NUM = 10
 };
 
 // Chunk of appended bases: 8 words x 32 bases (2 bits each) = 256 bases.
@@ -264,14 +267,26 @@ bool part_usable(const KParams& p, uint64_t cap, uint64_t n);
 bool region_slots_fit(const KParams& p, uint64_t cap);
 
 struct PartBuffers {
-    uint64_t* buf1;      // part_buf1_words(p, n) words: pass-1 windows
+    uint64_t* buf1;      // part_buf1_words(p, n) words: pass-1 windows; after pass 2 the list of
+                         // keys left for the global CAS insert (counter CT_OVF2)
     uint64_t* buf2;      // part_buf2_words(p, n) words: region windows
     uint32_t* wcnt;      // pass-1 window fill counters
-    uint32_t* rcnt;      // region window fill counters (wcnt + rcnt = part_count_words())
-    uint64_t* overflow;  // part_overflow_cap(n) * W words
+    uint32_t* rcnt;      // region window fill counters
+    uint32_t* hot_list;  // remapped regions of this build (NREG_MAX; wcnt + rcnt + hot_list = part_count_words())
+    uint64_t* overflow;  // part_overflow_cap(n) * W words: words that missed their pass-1/2 window (CT_OVF)
+    uint32_t* hot;       // the table's remapped-region bitmap (KParams::hot, writable)
     uint64_t* headrec = nullptr;  // 2^rbits * hcap chain head records of 2 words (null: no chains)
     uint32_t hcap = 0;
 };
+// Bitmap words of the remapped-region set (one bit per region, 2^17 regions at most).
+static constexpr uint32_t HOT_WORDS = (1u << 17) / 32;
+
+// CAS-path inserts into an empty table (batches too small for the partitioned build): count the
+// batch's keys per minimizer region and remap the regions that cannot hold theirs (records or
+// routed words), so a repeat family does not pile up one linear-probing run.
+hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
+                              uint64_t cap, uint32_t* rcnt, uint32_t* hot, uint32_t* hot_list,
+                              unsigned long long* ctr, hipStream_t s);
 // chain head records per region for a table of cap slots (0: K or LDS leave no room for chains)
 uint32_t part_head_cap(const KParams& p, uint64_t cap);
 

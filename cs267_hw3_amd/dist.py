@@ -557,7 +557,7 @@ class DistributedKmerHashMap:
 
 # --------------------------------------------------------------------------------------------
 def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard_kmers=None,
-                 check=None):
+                 check=None, load_factor=0.5):
     """P logical ranks on one GPU (threads): returns the per-rank contig texts. recs: a host
     record array, or a SyntheticKmers whose blocks each rank generates on the GPU (C4-size
     inputs). Shards start at shard_kmers (default n / P) and grow to what they are routed.
@@ -577,7 +577,7 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
             torch.cuda.set_device(device)
             b = min(r * split, n)
             e = min(b + split, n)
-            shard = GpuShard(k, start, device=device)
+            shard = GpuShard(k, start, device=device, load_factor=load_factor)
             with torch.cuda.stream(shard.stream):
                 if gen is not None:
                     mine = gen.records_dev(b, e, device=device, stream=shard.stream)

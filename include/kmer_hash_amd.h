@@ -66,6 +66,9 @@ typedef struct kh_stats {
     uint64_t n_bad_base;     /* kh_pack_text_dev lines with a k-mer base outside {A,C,G,T} */
     double ms_build;         /* device ms, region build + overflow inserts of the last partitioned insert */
     double ms_walk_kernel;   /* device ms, k_walk_q alone, last assemble */
+    uint64_t n_hot_regions;  /* placement regions remapped by key hash (shared minimizers overfilled them) */
+    uint64_t n_overflow;     /* keys of the last partitioned build inserted by global CAS (full windows,
+                                probe runs that left their region slice) */
 } kh_stats;
 
 /* ---- sizes / info --------------------------------------------------------------------------*/
@@ -219,6 +222,16 @@ int kh_gen_create(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t le
 int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
                          uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
                          uint32_t long_len, int front_starts);
+/* Hot-minimizer / hot-bucket variant (BASELINE configs[4] "skewed/hot-bucket"): additionally,
+ * hot_permille / 1000 of the contigs (picked by a seeded hash) carry one of n_motifs (1..64) shared
+ * M-mers (M = the table's minimizer length: 16 at k >= 31, 12 at k = 19) every K - M + 1 bases, so
+ * every k-mer of a hot contig contains one and the motifs (chosen for the smallest minimizer order)
+ * are their minimizers: all k-mers of motif h share one minimizer window, hence one placement
+ * region and one shard owner before the table's hot-region remap. Uniqueness and the ground
+ * truth hold as for kh_gen_create. hot_permille = 0 is kh_gen_create_skewed. */
+int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
+                      uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
+                      uint32_t long_len, int front_starts, uint32_t hot_permille, uint32_t n_motifs);
 int kh_gen_destroy(kh_gen* g);
 uint64_t kh_gen_num_contigs(const kh_gen* g);
 /* records at output positions [pos_begin, pos_end) in kmer_pair layout (block split of

@@ -24,6 +24,9 @@ pytestmark = pytest.mark.gpu
 
 C3 = dict(k=51, len_min=8, len_max=200, single=0, seed=51)
 C5 = dict(k=51, len_min=2, len_max=16, single=0, seed=5199, n_long=8, long_len=1_000_000, front_starts=True)
+# C5's hot-bucket half: 30 % of the contigs carry one of 8 shared minimizer motifs (60M k-mers in
+# 8 minimizer windows: each window alone is ~2,500 region slices' worth of keys)
+C5H = dict(k=51, len_min=8, len_max=200, single=0, seed=5198, hot_permille=300, n_motifs=8)
 
 
 def _gen(cfg, n):
@@ -32,9 +35,9 @@ def _gen(cfg, n):
                              seed=c.pop("seed"), **c)
 
 
-def _single_gpu(g, n):
+def _single_gpu(g, n, load=0.5):
     """One table, records generated in HBM, one insert + assemble; returns the contig text."""
-    with kh.KmerHashTable(g.k, n, 0.5) as t:
+    with kh.KmerHashTable(g.k, n, load) as t:
         s = torch.cuda.Stream()
         t.set_stream(s.cuda_stream)
         recs = g.records_dev(stream=s)
@@ -79,6 +82,27 @@ def test_c3_shape_20m_vs_oracle():
     assert text == want
 
 
+@pytest.mark.parametrize("load", [0.5, 0.85])
+def test_c5_hot_bucket_200m_one_gpu(load):
+    """BASELINE configs[4] hot-bucket half at 200M on one GPU, at load 0.5 and SURVEY's 0.85."""
+    n = 200_000_000
+    g = _gen(C5H, n)
+    text, st = _single_gpu(g, n, load)
+    assert st["n_contigs"] == g.num_contigs and st["n_hot_regions"] >= 8
+    assert text == g.truth()
+
+
+def test_c5_hot_bucket_20m_vs_oracle():
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_bind as ob
+    n = 20_000_000
+    g = _gen(C5H, n)
+    rc, want, nc, _, _, _ = ob.assemble(51, g.records())
+    assert rc == 0
+    text, st = _single_gpu(g, n)
+    assert st["n_contigs"] == nc and text == want
+
+
 def _sharded(g, P, **kw):
     from cs267_hw3_amd.dist import run_threaded
     bad = []
@@ -104,4 +128,12 @@ def test_c4_1b_kmers_8_ranks():
 def test_c5_skewed_200m_8_ranks():
     """BASELINE configs[4]: the skewed set at 200M over 8 ranks (logical, one GPU)."""
     info = _sharded(_gen(C5, 200_000_000), 8)
+    assert sum(s["n_inserted"] for s in info["stats"].values()) == 200_000_000
+
+
+@pytest.mark.parametrize("load", [0.5, 0.85])
+def test_c5_hot_bucket_200m_8_ranks(load):
+    """The hot-bucket set over 8 ranks (logical, one GPU): the owner of a shared minimizer window
+    receives its whole family (the all-to-all imbalance the config names)."""
+    info = _sharded(_gen(C5H, 200_000_000), 8, load_factor=load)
     assert sum(s["n_inserted"] for s in info["stats"].values()) == 200_000_000

@@ -336,3 +336,45 @@ def test_gpu_skewed_c5(k, n, n_long, long_len):
     g = kh.SyntheticKmers(k, n, 2, 16, 0, seed=k + n_long, n_long=n_long, long_len=long_len, front_starts=True)
     t, got, nc = run(k, g.records())
     assert nc == g.num_contigs and got == g.truth()
+
+
+# ---- C5 hot-bucket half: many k-mers sharing a few minimizer windows (BASELINE configs[4]) -------
+# kh_gen_create_hot plants one of a few shared M-mers in every k-mer of the hot contigs, so their
+# k-mers share one minimizer window: one placement region before the table remaps it (k_hot_mark).
+@pytest.mark.parametrize("mode", ["part", "cas"])
+@pytest.mark.parametrize("k,n,lmax,hot,motifs,load,batches", [
+    (51, 2_000_000, 200, 300, 4, 0.5, 1),     # 30 % of contigs on 4 motifs
+    (51, 2_000_000, 200, 1000, 1, 0.5, 1),    # every k-mer shares ONE minimizer window
+    (51, 1_500_000, 200, 300, 8, 0.85, 1),    # SURVEY C5's 0.85-load variant
+    (51, 2_000_000, 200, 500, 2, 0.5, 3),     # later batches place keys with the first batch's remap
+    # k=19, M=12: a hot k-mer has 7 free bases (8 phases x 4^7 = 131K distinct per motif), so a
+    # family of ~5K k-mers (2x a region) in short contigs is what stays unique
+    (19, 1_200_000, 20, 20, 1, 0.5, 1),
+    (31, 1_000_000, 200, 500, 2, 0.7, 1),
+])
+def test_gpu_hot_minimizers_vs_oracle(monkeypatch, mode, k, n, lmax, hot, motifs, load, batches):
+    monkeypatch.setenv("KH_INSERT", mode)
+    g = kh.SyntheticKmers(k, n, 8, lmax, 10, seed=k * 31 + hot + motifs, hot_permille=hot, n_motifs=motifs)
+    recs = g.records()
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0 and want == g.truth()
+    t, got, gnc = run(k, recs, batches=batches, load=load)
+    assert gnc == nc and got == want
+    s = t.stats()
+    assert s["n_full"] == s["n_dup"] == s["n_missing"] == 0
+    if hot >= 300:
+        assert s["n_hot_regions"] > 0      # the shared windows were remapped
+    # find agrees with the oracle table on present keys of the hot contigs too
+    P = (k + 3) // 4
+    sel = recs[np.random.default_rng(k).choice(len(recs), 2000, replace=False)]
+    out, found = t.find(sel[:, :P])
+    assert found.all() and np.array_equal(out, sel)
+
+
+def test_gpu_hot_remap_off_is_not_needed_for_random_sets():
+    """Random (non-repetitive) C3-shape input: no region is remapped, nothing takes the CAS path."""
+    g = kh.SyntheticKmers(51, 4_000_000, 8, 200, 0, seed=51)
+    t, got, _ = run(51, g.records())
+    assert got == g.truth()
+    s = t.stats()
+    assert s["n_hot_regions"] == 0 and s["n_overflow"] == 0
