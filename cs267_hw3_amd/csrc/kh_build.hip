@@ -119,6 +119,13 @@ bool part_usable(const KParams& p, uint64_t cap, uint64_t n) {
 }
 
 
+// Region of a partition word in passes 1 and 2: the minimizer region, or the key-hash region when
+// that one is remapped (hot_on: the table has remapped regions; one uniform test per block).
+__device__ __forceinline__ uint32_t part_region(uint32_t win, Key k, const KParams& p, bool hot_on) {
+    const uint32_t r = mini_region(win, p);
+    return (hot_on && region_is_hot(p.hot, r)) ? hot_region(key_hash32(k), p) : r;
+}
+
 // ---- record -> word conversion (k other than 51 / 19) ---------------------------------------------
 // Parse the reference records once, one per thread per 256-record sub-tile (the next sub-tile's
 // 16-B loads are in flight while this one is parsed), emit internal words in input order and the
@@ -129,7 +136,7 @@ __device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, in
 template <int W, int PK = 0, int KT = 0>
 __global__ __launch_bounds__(PB) void k_part1_convert(KParams p_in, const uint8_t* __restrict__ recs,
                                                       uint64_t n, uint64_t* words_out,
-                                                      uint64_t* start_mask, uint64_t* split_mask) {
+                                                      uint64_t* start_mask, uint64_t* split_mask, uint32_t* samp) {
     const KParams p = specialize<KT>(p_in);
     __shared__ __attribute__((aligned(16))) uint8_t stage[2][PB * 17 + 16];
     const uint64_t b0 = (uint64_t)blockIdx.x * T1 * PART_TILE;
@@ -180,7 +187,11 @@ __global__ __launch_bounds__(PB) void k_part1_convert(KParams p_in, const uint8_
         }
         if (valid) {
             // the word carries its minimizer window j* (pass 1 reads the region from it)
-            const uint64_t w0 = part_word0(slot_w0(k, ext, p), mini_scan(k, p), p);
+            const uint32_t mn = mini_scan(k, p);
+            // 1-in-256 sample of the minimizer regions (one lane per sub-tile; records are in
+            // shuffled order) for the hot-region mark before pass 1
+            if (samp && threadIdx.x == 0) atomicAdd(&samp[mini_region(mini_window(k, mn, p), p)], 1u);
+            const uint64_t w0 = part_word0(slot_w0(k, ext, p), mn, p);
             const uint64_t i = sub + threadIdx.x;
             if (W == 2) {
                 *reinterpret_cast<ulonglong2*>(words_out + i * 2) = make_ulonglong2(w0, k.lo);
@@ -849,16 +860,32 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
             }
         }
     }
-    if (spill) {  // full windows: the overflow list, one reservation per wave (a hot bucket spills whole tiles)
-        for (uint32_t x0 = threadIdx.x & ~63u; x0 < total; x0 += TB) {
-            const uint32_t x = x0 + (threadIdx.x & 63u);
-            const uint32_t q = x < total ? sbin[x] : 0u;
-            const bool sp = x < total && gpos[q] + (x - start[q]) >= cap;
-            const unsigned long long idx = wave_reserve(&ctr[CT_OVF], sp);
-            if (sp) {
-                if (idx < ovf_cap) {
-                    ovf[idx * W] = items[W * x];
-                    if (W == 2) ovf[idx * W + 1] = items[W * x + 1];
+    if (spill) {
+        // full windows: the spilled tail of each bin's run goes to the overflow list with ONE
+        // reservation per tile (a hot bucket spills most of every tile; per-wave reservations on
+        // the list's single counter serialised: c5h pass 1 1.4 -> 13.5 ms)
+        __shared__ uint32_t keepv[NB];
+        __shared__ unsigned long long sbase;
+        uint32_t sp = 0;
+        if (threadIdx.x < NB) {
+            const uint32_t g = gpos[threadIdx.x];
+            const uint32_t keep = g >= cap ? 0u : min(hv, cap - g);
+            keepv[threadIdx.x] = keep;
+            sp = hv - keep;
+        }
+        uint32_t stot;
+        const uint32_t so = block_scan_u32<TB>(sp, stot, wsum);
+        if (threadIdx.x < NB) hist[threadIdx.x] = so;  // hist is free after the bin scan
+        if (threadIdx.x == 0) sbase = atomicAdd(&ctr[CT_OVF], (unsigned long long)stot);
+        lds_barrier();
+        for (uint32_t x = threadIdx.x; x < total; x += TB) {
+            const uint32_t q = sbin[x];
+            const uint32_t rr = x - start[q];
+            if (rr >= keepv[q]) {
+                const uint64_t d = sbase + hist[q] + (rr - keepv[q]);
+                if (d < ovf_cap) {
+                    ovf[d * W] = items[W * x];
+                    if (W == 2) ovf[d * W + 1] = items[W * x + 1];
                 } else {
                     atomicAdd(&stats[ST_FULL], 1ull);
                 }
@@ -876,6 +903,7 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p_in, const uint64_t* __res
                                              unsigned long long* stats, uint64_t* splits, uint64_t splits_cap,
                                              int jstar_in) {
     const KParams p = specialize<KT>(p_in);
+    const bool hot_on = p.hot && ctr[CT_HOT];  // uniform: some region is remapped
     constexpr int IPT = TILE / TB;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
@@ -905,7 +933,7 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p_in, const uint64_t* __res
             const Key kk = slot_key(a[j], b[j], p);
             // words of k_part1_convert carry j*; routed words do not
             const uint32_t mn = jstar_in ? slot_jstar(a[j]) : mini_scan(kk, p);
-            bin[j] = mini_region(mini_window(kk, mn, p), p) >> (p.rbits - B1);
+            bin[j] = part_region(mini_window(kk, mn, p), kk, p, hot_on) >> (p.rbits - B1);
             const bool live = a[j] != EMPTY;
             // splitter k-mers this shard owns (they head migrating-walk segments, kh_mseg.hip)
             if (COLLECT && live && ext_bwd(slot_ext(a[j])) != EXT_F && is_splitter(key_hash32(kk), p)) {
@@ -971,6 +999,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __res
                                                  uint64_t ovf_cap, unsigned long long* ctr,
                                                  unsigned long long* stats) {
     constexpr int IPT = TILE / TB;
+    const bool hot_on = p.hot && ctr[CT_HOT];
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
     uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + TILE * 2);
@@ -1041,7 +1070,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __res
             }
             a[j] = valid ? part_word0(slot_w0(k, ext, p), mn, p) : EMPTY;
             b[j] = (valid && W == 2) ? k.lo : 0;
-            bin[j] = mini_region(mini_window(k, mn, p), p) >> (p.rbits - B1);
+            bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on) >> (p.rbits - B1);
         }
         const uint64_t nt = t + gridDim.x, nbase = nt * TILE;
         sort_reserve_write<W, TB, NB1, TILE>(
@@ -1060,6 +1089,7 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p_in, const uint64_t* __res
                                              unsigned long long* ctr, unsigned long long* stats, uint32_t CAP1,
                                              const uint32_t* wcnt) {
     const KParams p = specialize<KT>(p_in);
+    const bool hot_on = p.hot && ctr[CT_HOT];
     constexpr int IPT = TILE / TB;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
@@ -1085,7 +1115,8 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p_in, const uint64_t* __res
         uint32_t bin[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
-            bin[j] = mini_region(word_mini_window(a[j], b[j], p), p) & ((1u << b2) - 1u);
+            bin[j] = part_region(word_mini_window(a[j], b[j], p), slot_key(a[j], b[j], p), p, hot_on) &
+                     ((1u << b2) - 1u);
         sort_reserve_write<W, TB, NB2, TILE>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
             [&](uint32_t q) { return &rcnt[(bk << b2) | q]; },
@@ -1178,24 +1209,43 @@ static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n
 //                  not fit goes to list B (buf1, CT_OVF2), which the global CAS insert takes
 // Cost without hot regions: three launches over nothing (~15 us); words move only for remapped
 // regions and for windows that were full.
+// counts: exact region counts (sample_shift 0) or a 1-in-2^sample_shift sample of the batch
+// (k_part1_convert / k_sample_regions); a sampled region counts as hot only above twice the
+// threshold (the exact mark after pass 2 catches what the sample misses). CT_HOT is the bitmap's
+// population; list_new lists the regions this mark added (CT_HOTNEW) for k_hot_gather.
 template <int Unused = 0>
-__global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint32_t RC, int slack16,
-                                                  const uint32_t* rcnt, uint32_t* hot, uint32_t* hot_list,
-                                                  unsigned long long* ctr, int allow_new) {
+__global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint32_t RC, int slack16, int sample_shift,
+                                                  const uint32_t* counts, uint32_t* hot, uint32_t* hot_list,
+                                                  unsigned long long* ctr, int allow_new, int list_new) {
     const uint32_t NR = nreg(p);
     const uint32_t r = blockIdx.x * 256u + threadIdx.x;
-    bool h = false;
+    bool h = false, hn = false;
     if (r < NR) {
         const uint32_t S = (uint32_t)(region_lo(r + 1, cap, p) - region_lo(r, cap, p));
-        const uint32_t T = min(RC, S - (slack16 ? S / 16u : 0u));
-        h = ((hot[r >> 5] >> (r & 31u)) & 1u) || (allow_new && rcnt[r] > T);
+        const uint64_t T = min(RC, S - (slack16 ? S / 16u : 0u));
+        const bool old = (hot[r >> 5] >> (r & 31u)) & 1u;
+        const bool over = sample_shift ? ((uint64_t)counts[r] << sample_shift) > 2 * T : counts[r] > T;
+        hn = allow_new && !old && over;
+        h = old || hn;
     }
     const uint64_t m = __ballot(h);
     const uint32_t lane = lane_id();
     const uint32_t r0 = r - lane;  // the wave's 64 regions: two bitmap words
     if (r0 < NR && (lane == 0 || lane == 32)) hot[(r0 >> 5) + (lane >> 5)] = (uint32_t)(m >> lane);
-    const unsigned long long i = wave_reserve(&ctr[CT_HOT], h);
-    if (h) hot_list[i] = r;
+    if (lane == 0 && m) atomicAdd(&ctr[CT_HOT], (unsigned long long)__popcll(m));
+    const unsigned long long i = wave_reserve(&ctr[CT_HOTNEW], list_new && hn);
+    if (list_new && hn) hot_list[i] = r;
+}
+
+// A 1-in-256 sample of routed words (the sharded path's first stage / one-shot insert): region
+// counts for the sampled mark, so a hot family is placed by key hash in pass 1 already.
+template <int W>
+__global__ __launch_bounds__(256) void k_sample_regions(KParams p, const uint64_t* __restrict__ words, uint64_t m,
+                                                        uint32_t* counts) {
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) << 8; i < m; i += ((uint64_t)gridDim.x * 256) << 8) {
+        const uint64_t w0 = words[i * W], w1 = W == 2 ? words[i * W + 1] : 0ull;
+        (void)wave_count_add(counts, mini_region(word_mini_window(w0, w1, p), p), true);
+    }
 }
 
 template <int W>
@@ -1203,7 +1253,7 @@ __global__ __launch_bounds__(256) void k_hot_gather(uint32_t RC, uint32_t* rcnt,
                                                     const uint64_t* __restrict__ buf2, uint64_t* ovf, uint64_t ovf_cap,
                                                     unsigned long long* ctr, unsigned long long* stats) {
     __shared__ unsigned long long base;
-    const uint64_t nh = ctr[CT_HOT];
+    const uint64_t nh = ctr[CT_HOTNEW];
     for (uint64_t i = blockIdx.x; i < nh; i += gridDim.x) {
         const uint32_t r = hot_list[i];
         const uint32_t m = min(rcnt[r], RC);
@@ -1270,7 +1320,8 @@ static void hot_fixup(const KParams& p, uint64_t cap, uint32_t RC, bool allow_ne
                       hipStream_t s) {
     KParams q = p;
     q.hot = B.hot;
-    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, B.rcnt, B.hot, B.hot_list, ctr, allow_new ? 1 : 0);
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 0, B.rcnt, B.hot, B.hot_list, ctr,
+                                                     allow_new ? 1 : 0, 1);
     k_hot_gather<W><<<1024, 256, 0, s>>>(RC, B.rcnt, B.hot_list, B.buf2, B.overflow, ovf_cap, ctr, stats);
     k_ovf_scatter<W><<<2048, 256, 0, s>>>(q, RC, B.rcnt, B.overflow, ovf_cap, B.buf2, B.buf1, ovf2_cap, ctr, stats);
 }
@@ -1294,8 +1345,8 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
         return e;
     const uint32_t RC = part_region_cap(p, total);
     const uint64_t ovf2_cap = part_buf1_words(p, total) / p.W;  // list B lives in buf1 (dead after pass 2)
-    if ((e = hipMemsetAsync(ctr + CT_OVF2, 0, 16, s)) != hipSuccess) return e;  // CT_OVF2, CT_HOT
-    static_assert(CT_HOT == CT_OVF2 + 1, "counter layout");
+    if ((e = hipMemsetAsync(ctr + CT_OVF2, 0, 24, s)) != hipSuccess) return e;  // CT_OVF2, CT_HOT, CT_HOTNEW
+    static_assert(CT_HOT == CT_OVF2 + 1 && CT_HOTNEW == CT_HOT + 1, "counter layout");
     hot_fixup<W>(p, t.cap, RC, table_empty, B, part_overflow_cap(total), ovf2_cap, ctr, stats, s);
     KParams q = p;  // the build and the CAS inserts place keys of remapped regions by key hash
     q.hot = B.hot;
@@ -1329,7 +1380,7 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
                               unsigned long long* ctr, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 16, s)) != hipSuccess) return e;
     if (n) {
         const unsigned grid = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
         if (p.W == 2) {
@@ -1341,8 +1392,19 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
         }
     }
     // linear probing across region boundaries: remap what would fill more than 15/16 of a slice
-    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(p, cap, 0xFFFFFFFFu, 1, rcnt, hot, hot_list, ctr, 1);
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(p, cap, 0xFFFFFFFFu, 1, 0, rcnt, hot, hot_list, ctr, 1, 0);
     return hipGetLastError();
+}
+
+// Hot regions from a 1-in-256 sample of the batch (in B.rcnt, left zeroed for pass 2).
+static hipError_t sample_mark(const KParams& p, uint64_t cap, uint32_t RC, const PartBuffers& B,
+                              unsigned long long* ctr, hipStream_t s) {
+    hipError_t e;
+    KParams q = p;
+    q.hot = B.hot;
+    if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 16, s)) != hipSuccess) return e;  // CT_HOT, CT_HOTNEW
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot, B.hot_list, ctr, 1, 0);
+    return hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s);
 }
 
 // One batch: pass 1 (records or words), pass 2, build, overflow inserts.
@@ -1361,6 +1423,15 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
     const bool rec_pass = REC && ((p.P == 13 && W == 2) || (p.P == 5 && W == 1)) && debug_flag("p1rec");
+    // empty table: a 1-in-256 sample of the batch's minimizer regions marks the hot ones before
+    // pass 1, so their keys are sorted straight into their key-hash regions (no spill storm)
+    const bool sample = table_empty && !rec_pass && !debug_flag("no_hot_sample");
+    uint32_t* samp = (REC && sample) ? rcnt : nullptr;
+    if (!REC && sample) {
+        const uint64_t ns = (n + 255) >> 8;
+        k_sample_regions<W><<<(unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024), 256, 0, s>>>(p, words, n,
+                                                                                                          rcnt);
+    }
     if (rec_pass) {
         if ((e = win1_rec_launch<W>(p, recs, n, CAP1, wcnt, B, start_mask, split_mask, ovf_cap, ctr, stats, s)) !=
             hipSuccess)
@@ -1369,17 +1440,18 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
         if (REC) {  // records -> words (input order) in buf2, which pass 2 only writes after pass 1
             const unsigned nb = (unsigned)((n + (uint64_t)T1 * PART_TILE - 1) / ((uint64_t)T1 * PART_TILE));
             if (W == 2 && p.K == 51)  // compile-time shape: aligned 8-B LDS reads, constant masks
-                k_part1_convert<W, 13, 51><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+                k_part1_convert<W, 13, 51><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask, samp);
             else if (W == 1 && p.K == 19)
-                k_part1_convert<W, 5, 19><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+                k_part1_convert<W, 5, 19><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask, samp);
             else if (p.P == 13)
-                k_part1_convert<W, 13><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+                k_part1_convert<W, 13><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask, samp);
             else if (p.P == 5)
-                k_part1_convert<W, 5><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+                k_part1_convert<W, 5><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask, samp);
             else
-                k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask);
+                k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask, samp);
             words = B.buf2;
         }
+        if (sample && (e = sample_mark(p, t.cap, RC, B, ctr, s)) != hipSuccess) return e;
         // converted records and routed words (k_route_scatter) both carry j* and the order bits
         if ((e = win1_launch<W>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, REC ? nullptr : wsplits,
                                 wsplits_cap, true)) != hipSuccess)
@@ -1398,7 +1470,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
 template <int W>
 static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
                              const PartBuffers& B, unsigned long long* ctr, unsigned long long* stats,
-                             hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap) {
+                             hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap, bool sample, uint64_t cap) {
     hipError_t e;
     if (first) {
         if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
@@ -1406,6 +1478,13 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     }
     if (m == 0) return hipSuccess;
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(p, total);
+    if (sample && !debug_flag("no_hot_sample")) {  // the first chunk's sample marks the hot regions
+        const uint64_t ns = (m + 255) >> 8;
+        k_sample_regions<W><<<(unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024), 256, 0, s>>>(p, words, m,
+                                                                                                          B.rcnt);
+        // the sample covers this chunk: scale it to the whole build (chunks are alike)
+        if ((e = sample_mark(p, cap, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess) return e;
+    }
     if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = win1_launch<W>(p, words, m, CAP1, B.wcnt, B, part_overflow_cap(total), ctr, stats, s, wsplits,
                             wsplits_cap, true)) != hipSuccess)
@@ -1417,9 +1496,9 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
 
 hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
                              const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
-                             hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap) {
-    return p.W == 1 ? part_stage<1>(p, words, m, total, first, b, ctr, stats, s, wsplits, wsplits_cap)
-                    : part_stage<2>(p, words, m, total, first, b, ctr, stats, s, wsplits, wsplits_cap);
+                             hipStream_t s, uint64_t* wsplits, uint64_t wsplits_cap, bool sample, uint64_t cap) {
+    return p.W == 1 ? part_stage<1>(p, words, m, total, first, b, ctr, stats, s, wsplits, wsplits_cap, sample, cap)
+                    : part_stage<2>(p, words, m, total, first, b, ctr, stats, s, wsplits, wsplits_cap, sample, cap);
 }
 
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,

@@ -1016,7 +1016,7 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
         KH_HIP(kh::launch_part_stage(coll ? mseg_params(t) : t->kp, (const uint64_t*)words, m, t->stage_total, false, b,
                                      t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(),
                                      t->stream, coll ? t->splits.as<uint64_t>() : nullptr,
-                                     coll ? t->splits_cap : 0));
+                                     coll ? t->splits_cap : 0, t->stage_fresh && t->stage_n == 0, t->cap));
     } else {
         if (t->stage_n == 0)
             if (int rc = cas_hot_prepass(t, nullptr, words, m)) return rc;

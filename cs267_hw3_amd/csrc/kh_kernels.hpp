@@ -36,7 +36,8 @@ enum CtrIdx : int {
     CT_OVF2 = 8,       // partitioned build: keys left for the global CAS insert (full windows, probe
                        // runs that left their slice) after the hot-region fixup
     CT_HOT = 9,        // remapped ("hot") placement regions of the table (kh_build.hip k_hot_mark)
-    CT_NUM = 10
+    CT_HOTNEW = 10,    // regions the last exact mark remapped (their window words move: k_hot_gather)
+    CT_NUM = 11
 };
 
 // Chunk of appended bases: 8 words x 32 bases (2 bits each) = 256 bases.
@@ -304,7 +305,8 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
 // region_slots_fit and buffers from ensure_part(total).
 hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m, uint64_t total, bool first,
                              const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
-                             hipStream_t s, uint64_t* word_splits = nullptr, uint64_t word_splits_cap = 0);
+                             hipStream_t s, uint64_t* word_splits = nullptr, uint64_t word_splits_cap = 0,
+                             bool sample = false, uint64_t cap = 0);
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
                               const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
                               hipStream_t s);

@@ -372,9 +372,10 @@ def test_gpu_hot_minimizers_vs_oracle(monkeypatch, mode, k, n, lmax, hot, motifs
 
 
 def test_gpu_hot_remap_off_is_not_needed_for_random_sets():
-    """Random (non-repetitive) C3-shape input: no region is remapped, nothing takes the CAS path."""
+    """Random (non-repetitive) C3-shape input: no region is remapped; only probe runs that leave
+    their slice near its end take the CAS path (a few per 10^4 keys at this table size)."""
     g = kh.SyntheticKmers(51, 4_000_000, 8, 200, 0, seed=51)
     t, got, _ = run(51, g.records())
     assert got == g.truth()
     s = t.stats()
-    assert s["n_hot_regions"] == 0 and s["n_overflow"] == 0
+    assert s["n_hot_regions"] == 0 and s["n_overflow"] < len(g.records()) // 1000
