@@ -94,7 +94,17 @@ uint64_t part_buf2_words(const KParams& p, uint64_t n) {
     return (w > n ? w : n) * p.W;
 }
 
-static uint64_t region_max_slots(const KParams& p, uint64_t cap) { return cap / nreg(p) + 1; }
+// Largest region slice a build holds in LDS. Equal ranges: cap / 2^rbits (+1). Balanced bounds
+// (p.rb): as much as three 512-thread blocks per CU leave (~53 KB: 3,260 16-B slots), so a region
+// may take up to that many slots (k_bounds falls back to equal ranges when one would not fit).
+static uint64_t region_max_slots(const KParams& p, uint64_t cap) {
+    const uint64_t eq = cap / nreg(p) + 1;
+    if (!p.rb) return eq;
+    // LDS per block = 8 W sm + (sm / 8 + 32) * 2 + 16 <= LDS_BYTES / 3
+    uint64_t sm = ((LDS_BYTES / 3 - 96) * 4) / (32ull * p.W + 1);
+    if (p.chain && sm >= (1ull << (58 - p.idx_lo)) - 1) sm = (1ull << (58 - p.idx_lo)) - 2;
+    return sm > eq ? sm : eq;
+}
 // build LDS: the slice, plus the chain head list (<= slots/8 + 32 entries, part_head_cap) when
 // chains are built (successors live in the slots' own index fields)
 static uint64_t build_lds(const KParams& p, uint64_t cap, bool chains) {
@@ -433,8 +443,7 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
     const uint32_t NR = nreg(p);
     for (uint32_t r = blockIdx.x; r < NR; r += gridDim.x) {
         if (threadIdx.x == 0) hcnt = 0;
-        const uint64_t lo = mulhi64((uint64_t)r << (64 - p.rbits), cap);
-        const uint64_t hi = (r + 1 < NR) ? mulhi64((uint64_t)(r + 1) << (64 - p.rbits), cap) : cap;
+        const uint64_t lo = region_lo(r, cap, p), hi = region_lo(r + 1, cap, p);
         const uint32_t S = (uint32_t)(hi - lo);
         if (W == 2) {
             ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
@@ -549,8 +558,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
     load(r, fill(r), a, b);
     const uint32_t NR = nreg(p);
     for (; r < NR; r += gridDim.x) {
-        const uint64_t lo = mulhi64((uint64_t)r << (64 - p.rbits), cap);
-        const uint64_t hi = (r + 1 < NR) ? mulhi64((uint64_t)(r + 1) << (64 - p.rbits), cap) : cap;
+        const uint64_t lo = region_lo(r, cap, p), hi = region_lo(r + 1, cap, p);
         const uint32_t S = (uint32_t)(hi - lo);
         const uint32_t m_next = fill(r + gridDim.x);  // in flight during this region
         if (threadIdx.x == 0) hcnt = 0;
@@ -1194,6 +1202,76 @@ static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n
     });
 }
 
+// ---- balanced region bounds (tables above load ~0.6) ---------------------------------------------
+// A region's key count is a sum of minimizer runs (sd ~14 % of the mean at C3 sizes), so equal
+// slices at load 0.85 overflow one region in ten: the overflow probes linearly across full slices
+// (C3 at 0.85: 193 ms/step). Balanced bounds give region r a slice proportional to its count
+// (plus a 1/8-mean prior, so no slice is empty): every region builds at the table's load. The
+// bounds come from the first build after a clear and stay until the next clear; lookups read
+// them from rb (two adjacent words per region). When a slice would exceed the LDS slice
+// (region_max_slots), equal ranges are written instead.
+template <int Unused = 0>
+__global__ __launch_bounds__(1024) void k_bounds(KParams p, uint64_t cap, const uint32_t* counts, uint32_t RC,
+                                                 uint64_t smax, uint64_t* rb) {
+    __shared__ unsigned long long wsum[16];
+    __shared__ int bad;
+    const uint32_t NR = nreg(p);
+    const uint32_t per = (NR + 1023) / 1024;
+    const uint32_t r0 = threadIdx.x * per;
+    uint64_t loc = 0;
+    for (uint32_t r = r0; r < r0 + per && r < NR; ++r) loc += counts ? min(counts[r], RC) : 0u;
+    // exclusive scan of loc over the block (16 waves)
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if ((int)lane >= o) x += y;
+    }
+    if (threadIdx.x == 0) bad = 0;
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint64_t pre = 0, N = 0;
+    for (uint32_t i = 0; i < 16; ++i) {
+        pre += i < w ? wsum[i] : 0ull;
+        N += wsum[i];
+    }
+    pre += x - loc;
+    const double beta = (double)N / NR / 8.0 + 1.0;  // prior: no region gets an empty slice
+    const double scale = (double)cap / ((double)N + beta * NR);
+    auto bound = [&](uint32_t r, uint64_t P) -> uint64_t {
+        const uint64_t b = (uint64_t)(((double)P + beta * r) * scale);
+        return r == 0 ? 0ull : (r >= NR || b > cap ? cap : b);
+    };
+    uint64_t P = pre, prev = bound(r0, pre);
+    for (uint32_t r = r0; r < r0 + per && r < NR; ++r) {
+        P += counts ? min(counts[r], RC) : 0u;
+        const uint64_t nx = bound(r + 1, P);
+        if (nx - prev > smax) bad = 1;
+        prev = nx;
+    }
+    __syncthreads();
+    const bool eq = bad || !counts || N == 0;
+    P = pre;
+    for (uint32_t r = r0; r < r0 + per && r < NR; ++r) {
+        rb[r] = eq ? (r ? mulhi64((uint64_t)r << (64 - p.rbits), cap) : 0ull) : bound(r, P);
+        P += counts ? min(counts[r], RC) : 0u;
+    }
+    if (threadIdx.x == 0) rb[NR] = cap;
+}
+
+void launch_bounds(const KParams& p, uint64_t cap, const uint32_t* counts, uint32_t RC, hipStream_t s) {
+    k_bounds<<<1, 1024, 0, s>>>(p, cap, counts, RC, region_max_slots(p, cap), const_cast<uint64_t*>(p.rb));
+}
+
+// Hot threshold with balanced bounds: the count whose proportional slice fills the LDS slice
+// (3 % margin for the prior and rounding); 0 = equal ranges (the slice's own size).
+static uint32_t balanced_T(const KParams& p, uint64_t cap, uint64_t n) {
+    if (!p.rb || !cap) return 0u;
+    const double t = 0.97 * (double)region_max_slots(p, cap) * (double)n / (double)cap;
+    return t < 1.0 ? 1u : (t > 4.0e9 ? 0xFFFFFFFFu : (uint32_t)t);
+}
+
 // ---- hot regions ---------------------------------------------------------------------------------
 // A minimizer window shared by far more k-mers than a region holds (a repeat family, a low-complexity
 // run; the C5 hot-bucket set) would pile its whole family into one ~3K-slot slice: the window
@@ -1216,12 +1294,13 @@ static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n
 template <int Unused = 0>
 __global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint32_t RC, int slack16, int sample_shift,
                                                   const uint32_t* counts, uint32_t* hot, uint32_t* hot_list,
-                                                  unsigned long long* ctr, int allow_new, int list_new) {
+                                                  unsigned long long* ctr, int allow_new, int list_new, uint32_t Tfix) {
     const uint32_t NR = nreg(p);
     const uint32_t r = blockIdx.x * 256u + threadIdx.x;
     bool h = false, hn = false;
     if (r < NR) {
-        const uint32_t S = (uint32_t)(region_lo(r + 1, cap, p) - region_lo(r, cap, p));
+        // equal ranges: what the slice holds; balanced bounds (Tfix): what the largest slice holds
+        const uint32_t S = Tfix ? Tfix : (uint32_t)(region_lo(r + 1, cap, p) - region_lo(r, cap, p));
         const uint64_t T = min(RC, S - (slack16 ? S / 16u : 0u));
         const bool old = (hot[r >> 5] >> (r & 31u)) & 1u;
         const bool over = sample_shift ? ((uint64_t)counts[r] << sample_shift) > 2 * T : counts[r] > T;
@@ -1315,13 +1394,13 @@ __global__ __launch_bounds__(256) void k_ovf_scatter(KParams p, uint32_t RC, uin
 }
 
 template <int W>
-static void hot_fixup(const KParams& p, uint64_t cap, uint32_t RC, bool allow_new, const PartBuffers& B,
+static void hot_fixup(const KParams& p, uint64_t cap, uint64_t n, uint32_t RC, bool allow_new, const PartBuffers& B,
                       uint64_t ovf_cap, uint64_t ovf2_cap, unsigned long long* ctr, unsigned long long* stats,
                       hipStream_t s) {
     KParams q = p;
     q.hot = B.hot;
     k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 0, B.rcnt, B.hot, B.hot_list, ctr,
-                                                     allow_new ? 1 : 0, 1);
+                                                     allow_new ? 1 : 0, 1, balanced_T(p, cap, n));
     k_hot_gather<W><<<1024, 256, 0, s>>>(RC, B.rcnt, B.hot_list, B.buf2, B.overflow, ovf_cap, ctr, stats);
     k_ovf_scatter<W><<<2048, 256, 0, s>>>(q, RC, B.rcnt, B.overflow, ovf_cap, B.buf2, B.buf1, ovf2_cap, ctr, stats);
 }
@@ -1347,9 +1426,11 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
     const uint64_t ovf2_cap = part_buf1_words(p, total) / p.W;  // list B lives in buf1 (dead after pass 2)
     if ((e = hipMemsetAsync(ctr + CT_OVF2, 0, 24, s)) != hipSuccess) return e;  // CT_OVF2, CT_HOT, CT_HOTNEW
     static_assert(CT_HOT == CT_OVF2 + 1 && CT_HOTNEW == CT_HOT + 1, "counter layout");
-    hot_fixup<W>(p, t.cap, RC, table_empty, B, part_overflow_cap(total), ovf2_cap, ctr, stats, s);
+    hot_fixup<W>(p, t.cap, total, RC, table_empty, B, part_overflow_cap(total), ovf2_cap, ctr, stats, s);
     KParams q = p;  // the build and the CAS inserts place keys of remapped regions by key hash
     q.hot = B.hot;
+    // balanced bounds: an empty table's build sizes every region slice from its final count
+    if (p.rb && table_empty) launch_bounds(p, t.cap, B.rcnt, RC, s);
     launch_build_windows<W>(q, B, t, table_empty, ovf2_cap, ctr, stats, RC,
                             reinterpret_cast<const uint32_t*>(B.rcnt), lds, s);
     k_insert_overflow<W><<<1024, PB, 0, s>>>(q, B.buf1, ovf2_cap, ctr, t.slots, t.cap, stats);
@@ -1359,19 +1440,22 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
 // ---- CAS-path hot prepass --------------------------------------------------------------------------
 template <int W, bool REC>
 __global__ __launch_bounds__(256) void k_region_count(KParams p, const uint8_t* __restrict__ recs,
-                                                      const uint64_t* __restrict__ words, uint64_t n, uint32_t* rcnt) {
+                                                      const uint64_t* __restrict__ words, uint64_t n, uint32_t* rcnt,
+                                                      int remapped) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         uint32_t win;
+        Key k;
         if (REC) {
-            Key k;
             uint32_t ext;
             parse_record(recs + i * (uint64_t)p.R, p, k, ext);
             win = mini_window(k, mini_scan(k, p), p);
         } else {
             const uint64_t w0 = words[i * W], w1 = W == 2 ? words[i * W + 1] : 0ull;
+            k = slot_key(w0, w1, p);
             win = word_mini_window(w0, w1, p);
         }
-        (void)wave_count_add(rcnt, mini_region(win, p), true);
+        // remapped: the region the insert will use (hot regions by key hash)
+        (void)wave_count_add(rcnt, remapped ? place_w(win, k, p).r : mini_region(win, p), true);
     }
 }
 
@@ -1384,26 +1468,44 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
     if (n) {
         const unsigned grid = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
         if (p.W == 2) {
-            if (recs) k_region_count<2, true><<<grid, 256, 0, s>>>(p, recs, nullptr, n, rcnt);
-            else k_region_count<2, false><<<grid, 256, 0, s>>>(p, nullptr, words, n, rcnt);
+            if (recs) k_region_count<2, true><<<grid, 256, 0, s>>>(p, recs, nullptr, n, rcnt, 0);
+            else k_region_count<2, false><<<grid, 256, 0, s>>>(p, nullptr, words, n, rcnt, 0);
         } else {
-            if (recs) k_region_count<1, true><<<grid, 256, 0, s>>>(p, recs, nullptr, n, rcnt);
-            else k_region_count<1, false><<<grid, 256, 0, s>>>(p, nullptr, words, n, rcnt);
+            if (recs) k_region_count<1, true><<<grid, 256, 0, s>>>(p, recs, nullptr, n, rcnt, 0);
+            else k_region_count<1, false><<<grid, 256, 0, s>>>(p, nullptr, words, n, rcnt, 0);
         }
     }
     // linear probing across region boundaries: remap what would fill more than 15/16 of a slice
-    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(p, cap, 0xFFFFFFFFu, 1, 0, rcnt, hot, hot_list, ctr, 1, 0);
+    KParams q = p;
+    q.hot = hot;
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, 0xFFFFFFFFu, 1, 0, rcnt, hot, hot_list, ctr, 1, 0,
+                                                     balanced_T(p, cap, n));
+    if (p.rb) {  // balanced bounds from the counts after the remap (a second, hot-aware count)
+        if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
+        if (n) {
+            const unsigned grid = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+            if (p.W == 2) {
+                if (recs) k_region_count<2, true><<<grid, 256, 0, s>>>(q, recs, nullptr, n, rcnt, 1);
+                else k_region_count<2, false><<<grid, 256, 0, s>>>(q, nullptr, words, n, rcnt, 1);
+            } else {
+                if (recs) k_region_count<1, true><<<grid, 256, 0, s>>>(q, recs, nullptr, n, rcnt, 1);
+                else k_region_count<1, false><<<grid, 256, 0, s>>>(q, nullptr, words, n, rcnt, 1);
+            }
+        }
+        launch_bounds(p, cap, rcnt, 0xFFFFFFFFu, s);
+    }
     return hipGetLastError();
 }
 
 // Hot regions from a 1-in-256 sample of the batch (in B.rcnt, left zeroed for pass 2).
-static hipError_t sample_mark(const KParams& p, uint64_t cap, uint32_t RC, const PartBuffers& B,
+static hipError_t sample_mark(const KParams& p, uint64_t cap, uint64_t n, uint32_t RC, const PartBuffers& B,
                               unsigned long long* ctr, hipStream_t s) {
     hipError_t e;
     KParams q = p;
     q.hot = B.hot;
     if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 16, s)) != hipSuccess) return e;  // CT_HOT, CT_HOTNEW
-    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot, B.hot_list, ctr, 1, 0);
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot, B.hot_list, ctr, 1, 0,
+                                                     balanced_T(p, cap, n));
     return hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s);
 }
 
@@ -1451,7 +1553,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
                 k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, n, B.buf2, start_mask, split_mask, samp);
             words = B.buf2;
         }
-        if (sample && (e = sample_mark(p, t.cap, RC, B, ctr, s)) != hipSuccess) return e;
+        if (sample && (e = sample_mark(p, t.cap, n, RC, B, ctr, s)) != hipSuccess) return e;
         // converted records and routed words (k_route_scatter) both carry j* and the order bits
         if ((e = win1_launch<W>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, REC ? nullptr : wsplits,
                                 wsplits_cap, true)) != hipSuccess)
@@ -1483,7 +1585,7 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
         k_sample_regions<W><<<(unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024), 256, 0, s>>>(p, words, m,
                                                                                                           B.rcnt);
         // the sample covers this chunk: scale it to the whole build (chunks are alike)
-        if ((e = sample_mark(p, cap, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess) return e;
+        if ((e = sample_mark(p, cap, m, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess) return e;
     }
     if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = win1_launch<W>(p, words, m, CAP1, B.wcnt, B, part_overflow_cap(total), ctr, stats, s, wsplits,

@@ -101,6 +101,7 @@ struct kh_table {
     DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
     DevBuf headrec;                           // chain head records (region build -> walker)
     DevBuf hot;                               // remapped-region bitmap (KParams::hot), HOT_WORDS words
+    DevBuf rbounds;                           // balanced region bounds (KParams::rb), 2^17 + 1 words
     uint32_t hcap = 0;                        // head records per region (0 = no chains)
     bool last_insert_part = false;
     bool staging = false, stage_part = false, stage_fresh = false;  // kh_insert_words_stage_dev build
@@ -239,6 +240,13 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     return KH_OK;
 }
 
+// Balanced region bounds (kh_build.hip k_bounds) above load 0.6, where equal slices overflow:
+// KH_BALANCED=1/0 forces them on/off (A/B).
+bool balanced_bounds(const kh_table* t) {
+    if (const char* e = getenv("KH_BALANCED")) return strcmp(e, "0") != 0;
+    return t->load > 0.6;
+}
+
 // CAS-path insert into an empty table: remap the minimizer regions the batch would overfill
 // (kh_build.hip launch_hot_prepass); later batches place keys with the same bitmap.
 int cas_hot_prepass(kh_table* t, const void* recs, const void* words, uint64_t n) {
@@ -328,6 +336,12 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     if ((rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8))) return bail(rc);
     if ((rc = t->hot.ensure(kh::HOT_WORDS * 4))) return bail(rc);
     t->kp.hot = t->hot.as<uint32_t>();
+    if (balanced_bounds(t)) {
+        if ((rc = t->rbounds.ensure((kh::HOT_WORDS * 32 + 1) * 8))) return bail(rc);
+        t->kp.rb = t->rbounds.as<uint64_t>();
+        if (hipSetDevice(device) != hipSuccess) return bail(fail(KH_ERR_HIP, "hipSetDevice failed"));
+        kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->stream);  // equal ranges until the first build
+    }
     if ((rc = t->ctr.ensure(kh::CT_NUM * 8))) return bail(rc);
     if ((rc = t->stats.ensure(kh::ST_NUM * 8))) return bail(rc);
     if ((rc = kh_clear(t))) return bail(rc);
@@ -349,7 +363,7 @@ int kh_destroy(kh_table* t) {
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
-                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot};
+                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot, &t->rbounds};
     for (auto* b : bufs) b->release();
     if (t->side) (void)hipStreamSynchronize(t->side);
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_b0,
@@ -384,6 +398,7 @@ int kh_reserve(kh_table* t, uint64_t n_kmers) {
         return rc;
     }
     t->slots_stale = true;
+    if (t->kp.rb) KH_HIP((kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->stream), hipGetLastError()));
     return KH_OK;
 }
 

@@ -63,6 +63,10 @@ struct KParams {
     // whose minimizer windows bring more k-mers than its window or slice holds has all its keys
     // placed by a hash of the whole key instead (kh_build.hip k_hot_mark; place_w)
     const uint32_t* hot;
+    // balanced region bounds (tables above load ~0.6): rb[r] = first slot of region r, rb[2^rbits]
+    // = cap, sized from the build's region counts (kh_build.hip k_bounds); nullptr = 2^rbits
+    // equal ranges
+    const uint64_t* rb;
 };
 
 // Minimizer length: consecutive k-mers of a contig share their minimizer for ~(K-M+2)/2 steps on
@@ -97,6 +101,7 @@ inline KParams make_params(int K) {
     p.chain = (SCRATCH_BIT - p.idx_lo >= 8) && K >= 14 ? 1 : 0;
     p.rbits = REGION_BITS_MAX;
     p.hot = nullptr;
+    p.rb = nullptr;
     return p;
 }
 
@@ -321,6 +326,7 @@ KH_HD uint32_t mini_region(uint32_t win, const KParams& p) { return mix32(win ^ 
 // a contig (same minimizer) lands in one region: the region build links them into chains
 // (kh_build.hip) that the walker crosses in one step.
 KH_HD uint64_t region_lo(uint32_t r, uint64_t cap, const KParams& p) {
+    if (p.rb) return p.rb[r];
     return (r >> p.rbits) ? cap : mulhi64((uint64_t)r << (64 - p.rbits), cap);
 }
 KH_HD uint64_t home_in(uint64_t lo, uint64_t hi, uint32_t h) { return lo + (((hi - lo) * (uint64_t)h) >> 32); }

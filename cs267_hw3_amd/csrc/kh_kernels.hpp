@@ -282,6 +282,9 @@ struct PartBuffers {
 // Bitmap words of the remapped-region set (one bit per region, 2^17 regions at most).
 static constexpr uint32_t HOT_WORDS = (1u << 17) / 32;
 
+// Balanced region bounds (KParams::rb) from region counts (nullptr: equal ranges).
+void launch_bounds(const KParams& p, uint64_t cap, const uint32_t* counts, uint32_t RC, hipStream_t s);
+
 // CAS-path inserts into an empty table (batches too small for the partitioned build): count the
 // batch's keys per minimizer region and remap the regions that cannot hold theirs (records or
 // routed words), so a repeat family does not pile up one linear-probing run.
