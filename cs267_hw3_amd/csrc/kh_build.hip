@@ -436,14 +436,15 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
                                                               unsigned long long* ctr,
                                                               unsigned long long* stats,
                                                               uint32_t RC, const uint32_t* rcnt,
-                                                              uint64_t* headrec, uint32_t hcap, uint32_t smax) {
+                                                              uint64_t* headrec, uint32_t hcap, uint32_t smax,
+                                                              const uint64_t* __restrict__ rbt) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
     uint16_t* hlist = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
     __shared__ uint32_t hcnt;
     const uint32_t NR = nreg(p);
     for (uint32_t r = blockIdx.x; r < NR; r += gridDim.x) {
         if (threadIdx.x == 0) hcnt = 0;
-        const uint64_t lo = region_lo(r, cap, p), hi = region_lo(r + 1, cap, p);
+        const uint64_t lo = rbt[r], hi = rbt[r + 1];
         const uint32_t S = (uint32_t)(hi - lo);
         if (W == 2) {
             ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                                                                  unsigned long long* stats, uint32_t RC,
                                                                  const uint32_t* __restrict__ rcnt,
                                                                  uint64_t* headrec, uint32_t hcap, uint32_t smax,
-                                                                 int prof) {
+                                                                 int prof, const uint64_t* __restrict__ rbt) {
     const KParams p = specialize<KT>(p_in);
     extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
     uint16_t* hlist = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
@@ -558,7 +559,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
     load(r, fill(r), a, b);
     const uint32_t NR = nreg(p);
     for (; r < NR; r += gridDim.x) {
-        const uint64_t lo = region_lo(r, cap, p), hi = region_lo(r + 1, cap, p);
+        const uint64_t lo = rbt[r], hi = rbt[r + 1];
         const uint32_t S = (uint32_t)(hi - lo);
         const uint32_t m_next = fill(r + gridDim.x);  // in flight during this region
         if (threadIdx.x == 0) hcnt = 0;
@@ -590,8 +591,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             // (the order bits stay in the register copy for the link test)
             const uint64_t home = home_in(lo, hi, key_hash32(slot_key(a[j], b[j], p)));
             pos[j] = lds_insert<W>(p, lt, S, home - lo, slot_clean(a[j], p), b[j], stats);
-            const unsigned long long idx = wave_reserve(&ctr[CT_OVF2], pos[j] == LDS_OUT);
-            if (pos[j] == LDS_OUT) {
+            if (pos[j] == LDS_OUT) {  // rare after the hot remap: a per-lane atomic (no spills)
+                const unsigned long long idx = atomicAdd(&ctr[CT_OVF2], 1ull);
                 if (idx < ovf_cap) {
                     ovf[idx * W] = a[j];
                     if (W == 2) ovf[idx * W + 1] = b[j];
@@ -697,19 +698,19 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
     }
     if (debug_flag("plain_build"))  // tests: the large-window kernel at small sizes
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
-                                                         stats, RC, rcnt, B.headrec, hcap, smax);
+                                                         stats, RC, rcnt, B.headrec, hcap, smax, B.rbt);
     else if (RC <= 4u * BUILD_THREADS)
         with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 4, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
-                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
+                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
     else if (RC <= 6u * BUILD_THREADS)
         with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 6, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
-                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
+                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
     else if (RC <= 12u * BUILD_THREADS)
         with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 12, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
-                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof); });
+                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
     else
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
-                                                         stats, RC, rcnt, B.headrec, hcap, smax);
+                                                         stats, RC, rcnt, B.headrec, hcap, smax, B.rbt);
     if (prof) {
         unsigned long long v[8];
         (void)hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_build_prof), sizeof v, 0, hipMemcpyDeviceToHost, s);
@@ -1260,8 +1261,8 @@ __global__ __launch_bounds__(1024) void k_bounds(KParams p, uint64_t cap, const 
     if (threadIdx.x == 0) rb[NR] = cap;
 }
 
-void launch_bounds(const KParams& p, uint64_t cap, const uint32_t* counts, uint32_t RC, hipStream_t s) {
-    k_bounds<<<1, 1024, 0, s>>>(p, cap, counts, RC, region_max_slots(p, cap), const_cast<uint64_t*>(p.rb));
+void launch_bounds(const KParams& p, uint64_t cap, const uint32_t* counts, uint32_t RC, uint64_t* rb, hipStream_t s) {
+    k_bounds<<<1, 1024, 0, s>>>(p, cap, counts, RC, region_max_slots(p, cap), rb);
 }
 
 // Hot threshold with balanced bounds: the count whose proportional slice fills the LDS slice
@@ -1430,7 +1431,7 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
     KParams q = p;  // the build and the CAS inserts place keys of remapped regions by key hash
     q.hot = B.hot;
     // balanced bounds: an empty table's build sizes every region slice from its final count
-    if (p.rb && table_empty) launch_bounds(p, t.cap, B.rcnt, RC, s);
+    if (p.rb && table_empty) launch_bounds(p, t.cap, B.rcnt, RC, const_cast<uint64_t*>(B.rbt), s);
     launch_build_windows<W>(q, B, t, table_empty, ovf2_cap, ctr, stats, RC,
                             reinterpret_cast<const uint32_t*>(B.rcnt), lds, s);
     k_insert_overflow<W><<<1024, PB, 0, s>>>(q, B.buf1, ovf2_cap, ctr, t.slots, t.cap, stats);
@@ -1492,7 +1493,7 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
                 else k_region_count<1, false><<<grid, 256, 0, s>>>(q, nullptr, words, n, rcnt, 1);
             }
         }
-        launch_bounds(p, cap, rcnt, 0xFFFFFFFFu, s);
+        launch_bounds(p, cap, rcnt, 0xFFFFFFFFu, const_cast<uint64_t*>(p.rb), s);
     }
     return hipGetLastError();
 }

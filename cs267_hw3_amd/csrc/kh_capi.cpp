@@ -231,6 +231,7 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     b.hot_list = b.rcnt + kh::HOT_WORDS * 32;
     b.overflow = t->pb_ovf.as<uint64_t>();
     b.hot = t->hot.as<uint32_t>();
+    b.rbt = t->rbounds.as<uint64_t>();
     // chain head records: sized by the table (regions x records per region), kept across builds
     const uint32_t hcap = kh::debug_flag("no_chains") ? 0u : kh::part_head_cap(t->kp, t->cap);
     if (hcap && (rc = t->headrec.ensure((uint64_t)hcap * (1ull << t->kp.rbits) * 16))) return rc;
@@ -336,12 +337,11 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     if ((rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8))) return bail(rc);
     if ((rc = t->hot.ensure(kh::HOT_WORDS * 4))) return bail(rc);
     t->kp.hot = t->hot.as<uint32_t>();
-    if (balanced_bounds(t)) {
-        if ((rc = t->rbounds.ensure((kh::HOT_WORDS * 32 + 1) * 8))) return bail(rc);
-        t->kp.rb = t->rbounds.as<uint64_t>();
-        if (hipSetDevice(device) != hipSuccess) return bail(fail(KH_ERR_HIP, "hipSetDevice failed"));
-        kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->stream);  // equal ranges until the first build
-    }
+    // region slot ranges: equal until a balanced table's first build (lookups read them only when
+    // balanced; the build always does)
+    if ((rc = t->rbounds.ensure((kh::HOT_WORDS * 32 + 1) * 8))) return bail(rc);
+    if (balanced_bounds(t)) t->kp.rb = t->rbounds.as<uint64_t>();
+    kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->rbounds.as<uint64_t>(), t->stream);
     if ((rc = t->ctr.ensure(kh::CT_NUM * 8))) return bail(rc);
     if ((rc = t->stats.ensure(kh::ST_NUM * 8))) return bail(rc);
     if ((rc = kh_clear(t))) return bail(rc);
@@ -398,7 +398,8 @@ int kh_reserve(kh_table* t, uint64_t n_kmers) {
         return rc;
     }
     t->slots_stale = true;
-    if (t->kp.rb) KH_HIP((kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->stream), hipGetLastError()));
+    kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->rbounds.as<uint64_t>(), t->stream);
+    KH_HIP(hipGetLastError());
     return KH_OK;
 }
 

@@ -276,6 +276,7 @@ struct PartBuffers {
     uint32_t* hot_list;  // remapped regions of this build (NREG_MAX; wcnt + rcnt + hot_list = part_count_words())
     uint64_t* overflow;  // part_overflow_cap(n) * W words: words that missed their pass-1/2 window (CT_OVF)
     uint32_t* hot;       // the table's remapped-region bitmap (KParams::hot, writable)
+    const uint64_t* rbt; // region slot ranges (equal or balanced: KParams::rb), read by the build
     uint64_t* headrec = nullptr;  // 2^rbits * hcap chain head records of 2 words (null: no chains)
     uint32_t hcap = 0;
 };
@@ -283,7 +284,9 @@ struct PartBuffers {
 static constexpr uint32_t HOT_WORDS = (1u << 17) / 32;
 
 // Balanced region bounds (KParams::rb) from region counts (nullptr: equal ranges).
-void launch_bounds(const KParams& p, uint64_t cap, const uint32_t* counts, uint32_t RC, hipStream_t s);
+// rb: the table's bounds (2^rbits + 1 words); counts nullptr: equal ranges (the build kernels read
+// every region's slot range from rb, balanced or not)
+void launch_bounds(const KParams& p, uint64_t cap, const uint32_t* counts, uint32_t RC, uint64_t* rb, hipStream_t s);
 
 // CAS-path inserts into an empty table (batches too small for the partitioned build): count the
 // batch's keys per minimizer region and remap the regions that cannot hold theirs (records or
