@@ -265,6 +265,73 @@ __device__ __forceinline__ int lds_insert(const KParams& p, unsigned long long* 
     return LDS_OUT;
 }
 
+// The same with block steps: one step reads the word0s of the 4-slot block holding `loc` and takes
+// the first slot at or after `loc` that is EMPTY (CAS) or holds the key's high word (duplicate
+// test), so a probe run of d slots costs ~d/4 steps. The build's phases run the lanes' keys in
+// lockstep, so a wave waits for its longest run: this shortens exactly that tail. Slots are
+// taken in the same order (first EMPTY at or after home) as lds_insert.
+#ifndef KH_LDS_BLOCK
+#define KH_LDS_BLOCK 1
+#endif
+template <int W>
+__device__ __forceinline__ int lds_insert_blk(const KParams& p, unsigned long long* lt, uint32_t S, uint32_t loc,
+                                              uint64_t w0, uint64_t w1, unsigned long long* stats) {
+    const uint64_t want0 = slot_keybits(w0, p);
+    uint32_t spins = 0;
+    while (loc < S) {
+        const uint32_t base = loc & ~3u;
+        uint64_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = lt[W * (base + q)];  // past S: inside the LDS allocation, masked
+        int hit = -1;
+        bool key = false;
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+            const uint32_t i = base + q;
+            const bool e = v[q] == EMPTY, m = !e && slot_keybits(v[q], p) == want0;
+            if (i >= loc && i < S && (e || m)) {
+                hit = q;
+                key = m;
+            }
+        }
+        if (hit < 0) {
+            loc = base + 4;
+            continue;
+        }
+        const uint32_t i = base + (uint32_t)hit;
+        if (!key) {
+            const unsigned long long old = atomicCAS(&lt[W * i], (unsigned long long)EMPTY, w0);
+            if (old == EMPTY) {
+                if (W == 2)
+                    __hip_atomic_store(&lt[2 * i + 1], (unsigned long long)w1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                return (int)i;
+            }
+            loc = i;  // lost the slot: look at it again (the winner may hold this key)
+            continue;
+        }
+        if (W == 1) {
+            atomicAdd(&stats[ST_DUP], 1ull);
+            return LDS_DUP;
+        }
+        const unsigned long long o1 = __hip_atomic_load(&lt[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (o1 == EMPTY) {  // claimed, word1 not stored yet: look again
+            if (++spins > (1u << 24)) {
+                atomicAdd(&stats[ST_SPIN], 1ull);
+                return LDS_DUP;
+            }
+            loc = i;
+            continue;
+        }
+        if (o1 == w1) {
+            atomicAdd(&stats[ST_DUP], 1ull);
+            return LDS_DUP;
+        }
+        loc = i + 1;
+    }
+    return LDS_OUT;
+}
+
 // KH_DEBUG=build_prof: per-phase shader-clock cycles of the prefetching build (thread 0 of every
 // block, summed), printed after each build. Off: one uniform branch per phase.
 __device__ unsigned long long g_build_prof[8];
@@ -334,6 +401,34 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned 
     const uint64_t home = MTOP ? home_in(lo, lo + S, hy) : home_of(place_w(mw, y, p), cap, p);
     if (home < lo || home >= lo + S) return NO_SUCC;
     const uint64_t want0 = W == 1 ? y.lo : y.hi;
+    if (KH_LDS_BLOCK && MTOP) {  // block steps (see lds_insert_blk): ~d/4 steps for a run of d slots
+        for (uint32_t t = (uint32_t)(home - lo); t < S;) {
+            const uint32_t base = t & ~3u;
+            uint64_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = lt[W * (base + q)];
+            int hit = -1;
+            bool key = false;
+#pragma unroll
+            for (int q = 3; q >= 0; --q) {
+                const uint32_t i = base + q;
+                const bool e = v[q] == EMPTY, m = !e && slot_keybits(v[q], p) == want0;
+                if (i >= t && i < S && (e || m)) {
+                    hit = q;
+                    key = m;
+                }
+            }
+            if (hit < 0) {
+                t = base + 4;
+                continue;
+            }
+            const uint32_t i = base + (uint32_t)hit;
+            if (!key) return NO_SUCC;  // EMPTY: y is not in this slice
+            if (W == 1 || (lt[W * i + 1] & LO_MASK) == y.lo) return i;
+            t = i + 1;
+        }
+        return NO_SUCC;
+    }
     for (uint32_t t = (uint32_t)(home - lo); t < S; ++t) {
         uint64_t v0, v1 = 0;
         if (W == 2) {  // both words in one LDS read: a match needs no second round trip
@@ -590,7 +685,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             // every word of region r's window is a key of region r; the slot keeps key, ext and j*
             // (the order bits stay in the register copy for the link test)
             const uint64_t home = home_in(lo, hi, key_hash32(slot_key(a[j], b[j], p)));
-            pos[j] = lds_insert<W>(p, lt, S, home - lo, slot_clean(a[j], p), b[j], stats);
+            pos[j] = KH_LDS_BLOCK ? lds_insert_blk<W>(p, lt, S, (uint32_t)(home - lo), slot_clean(a[j], p), b[j], stats)
+                                  : lds_insert<W>(p, lt, S, home - lo, slot_clean(a[j], p), b[j], stats);
             if (pos[j] == LDS_OUT) {  // rare after the hot remap: a per-lane atomic (no spills)
                 const unsigned long long idx = atomicAdd(&ctr[CT_OVF2], 1ull);
                 if (idx < ovf_cap) {

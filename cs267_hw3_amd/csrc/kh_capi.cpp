@@ -391,12 +391,16 @@ int kh_reserve(kh_table* t, uint64_t n_kmers) {
     const uint64_t old_n = t->n_kmers;
     const int old_bits = t->kp.split_bits;
     size_table(t, n_kmers);
-    t->slots.release();
-    if (int rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8)) {
+    // the new slot array first: when it cannot be had, the table keeps its old one and old size
+    DevBuf ns;
+    if (int rc = ns.ensure(t->cap * (uint64_t)t->kp.W * 8)) {
         size_table(t, old_n);
         t->kp.split_bits = old_bits;
         return rc;
     }
+    t->slots.release();
+    t->slots = ns;
+    ns.p = nullptr;
     t->slots_stale = true;
     kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->rbounds.as<uint64_t>(), t->stream);
     KH_HIP(hipGetLastError());

@@ -142,6 +142,7 @@ class GpuShard:
         self.n_kmers = n_kmers
         self.stream = torch.cuda.Stream(device=self.dev)
         self.table.set_stream(self.stream.cuda_stream)
+        self.inserted = 0  # k-mers the shard holds since the last clear
 
     @staticmethod
     def _p(t):
@@ -152,6 +153,7 @@ class GpuShard:
 
     def clear(self):
         self.table.clear()
+        self.inserted = 0
 
     def collect_starts(self, recs):
         check(self.L.kh_collect_starts_dev(self.h, self._p(recs), recs.shape[0]))
@@ -168,15 +170,18 @@ class GpuShard:
         return words, counts
 
     def reserve(self, m):
-        """Grow the (empty) shard to hold m k-mers (kh_reserve)."""
-        check(self.L.kh_reserve(self.h, int(m)))
+        """Room for m more k-mers: an empty shard grows to them (kh_reserve); a non-empty one must
+        already have the room (kh_reserve fails otherwise: the caller's ranks agree on it)."""
+        check(self.L.kh_reserve(self.h, int(self.inserted + m)))
 
     def insert_words(self, words, m):
         check(self.L.kh_insert_words_dev(self.h, self._p(words), m))
+        self.inserted += m
 
     def stage_words(self, words, m, total):
         """Partition m received words toward one build of <= total (kh_insert_words_stage_dev)."""
         check(self.L.kh_insert_words_stage_dev(self.h, self._p(words), m, total))
+        self.inserted += m
 
     def finish_words(self):
         check(self.L.kh_insert_words_finish(self.h))

@@ -15,13 +15,19 @@
 //               k-mer is owned elsewhere, then moves there in the round's all-to-all; the bases
 //               go home in one more all-to-all; splitter segments (long chains) are stitched by
 //               distributed pointer jumping. Each rank ends with its test_<rank>.dat bytes.
-//   find        the owner's table answers (in-process peers; the RPC of hash_map.hpp:94-100)
+//   find        the owner's table answers (the RPC of hash_map.hpp:94-100): ranks that are threads
+//               of one process (a peer group) look the owner's table up directly; otherwise every
+//               find() is one collective round (all ranks' queries gathered, each owner answers its
+//               own, answers gathered), and barrier()/process_requests() keep answering rounds until
+//               every rank has reached them -- the UPC++ progress the reference's barrier makes
+//               (kmer_hash.cpp:136, hash_map.hpp:110-113) while other ranks still walk
 //
 // The same protocol has a Python host in cs267_hw3_amd/dist.py (torch.distributed).
 #pragma once
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
@@ -103,6 +109,16 @@ public:
         auto it = peers_.find(group);
         return it == peers_.end() || rank >= (int)it->second.size() ? nullptr : it->second[rank];
     }
+    // f(peer) with the registry locked, so the peer cannot be destroyed (remove) meanwhile
+    template <class F>
+    bool with_peer(const void* group, int rank, F f) {
+        std::lock_guard<std::mutex> g(m_);
+        auto it = peers_.find(group);
+        ShardedTable* t = it == peers_.end() || rank >= (int)it->second.size() ? nullptr : it->second[rank];
+        if (!t) return false;
+        f(t);
+        return true;
+    }
 
 private:
     std::mutex m_;
@@ -149,6 +165,7 @@ public:
     void clear() {
         hip_check(hipSetDevice(device_), "hipSetDevice");
         abi_check(kh_clear(t_));
+        inserted_ = 0;
     }
 
     // hash_map.hpp:55-80 insert_all (+ kmer_hash.cpp:27-31 start nodes) for this rank's block of
@@ -194,13 +211,15 @@ public:
                 m += M(q, c, rank_);
                 for (uint64_t d = 0; d < P; ++d) gmax = std::max(gmax, M(q, c, d));
             }
-        // size the shard from what it receives; every rank fails together if any rank cannot
-        const int rc = kh_reserve(t_, m);
+        // size the shard from what it holds after this insert (a non-empty shard cannot grow:
+        // kh_reserve fails); every rank fails together if any rank cannot
+        const int rc = kh_reserve(t_, inserted_ + m);
         const std::string err = rc == KH_OK ? "" : kh_last_error();
         agree(rc != KH_OK, err);
+        inserted_ += m;
         if (P == 1) {  // one rank: the routed words are this shard's
             abi_check(kh_insert_words_dev(t_, words, m));
-            return m;
+            return done_insert(m);
         }
         int64_t* recv = recv_.words(std::max<uint64_t>(m, 1) * W_);
         std::vector<uint64_t> sc(P), sd(P), rcn(P), rd(P);
@@ -219,7 +238,7 @@ public:
             plan(0, 0);
             comm_.alltoallv(words, sc.data(), sd.data(), recv, rcn.data(), rd.data(), gmax * W_, stream_);
             abi_check(kh_insert_words_dev(t_, recv, m));
-            return m;
+            return done_insert(m);
         }
         // chunk c moves on the exchange stream while chunk c-1, received, is partitioned on the
         // table's stream; one build at the end
@@ -240,7 +259,7 @@ public:
         }
         stage(recv, prev_pos, prev_m, m, events_[nch - 1]);
         abi_check(kh_insert_words_finish(t_));
-        return m;
+        return done_insert(m);
     }
 
     // kmer_hash.cpp:38-55 assemble_contigs for this rank's start k-mers, every rank at once.
@@ -305,27 +324,106 @@ public:
         return s;
     }
 
-    // Single-key find (hash_map.hpp:83-107): the owner's table answers. Keys this rank owns are
-    // looked up here; others go to the owning rank's table when it lives in this process (the
-    // ranks are threads); a one-process-per-GPU run has no RPC channel and throws.
+    // Single-key find (hash_map.hpp:83-107): the owner's table answers. Ranks of a peer group
+    // (threads of one process) look the owner's table up directly; without one (one process per
+    // GPU) every find() is one collective round, so every rank must keep calling find() or
+    // barrier() (process_requests) until all are done, as the reference's own loop does.
     bool find(const uint8_t* packed_key, uint8_t* rec_out) {
+        if (!group_ && P_ > 1) return find_round(packed_key, rec_out, false);
         const int owner = kh_key_owner(t_, packed_key, P_);
         if (owner < 0) abi_check(owner);
-        ShardedTable* o = owner == rank_ ? this : (group_ ? PeerRegistry::get().peer(group_, owner) : nullptr);
-        if (!o) throw std::runtime_error("DistributedHashMap::find: the owner rank is not in this process");
-        std::lock_guard<std::mutex> g(o->m_);
-        hip_check(hipSetDevice(o->device_), "hipSetDevice");
+        int prev = 0;
+        hip_check(hipGetDevice(&prev), "hipGetDevice");
         uint8_t found = 0;
-        abi_check(kh_find(o->t_, packed_key, 1, rec_out, &found));
+        int rc = KH_OK;
+        auto look = [&](ShardedTable* o) {
+            std::lock_guard<std::mutex> g(o->m_);
+            if (hipSetDevice(o->device_) != hipSuccess) rc = KH_ERR_HIP;
+            else rc = kh_find(o->t_, packed_key, 1, rec_out, &found);
+        };
+        bool ok = true;
+        if (owner == rank_ || !group_)
+            look(this);
+        else
+            ok = PeerRegistry::get().with_peer(group_, owner, look);  // registry locked: the peer stays
+        (void)hipSetDevice(prev);  // the caller's device, whichever table answered
+        if (!ok) throw std::runtime_error("DistributedHashMap::find: the owner rank is not in this process");
+        abi_check(rc);
         return found != 0;
     }
 
-    void barrier() { comm_.barrier(); }
+    // hash_map.hpp:110-113 process_requests (progress + barrier) / upcxx::barrier(): collective.
+    // Without a peer group it answers find rounds until every rank has arrived here.
+    void barrier() {
+        if (!group_ && P_ > 1) {
+            while (!find_round(nullptr, nullptr, true)) {
+            }
+            return;
+        }
+        comm_.barrier();
+    }
 
     static constexpr uint64_t kInsertChunks = 4;
     static constexpr uint64_t kPipelineMin = 1ull << 22;  // records per rank below: one transfer
 
 private:
+    // hash_map.hpp:79: insert_all ends in a barrier, so a find() right after it sees every
+    // rank's keys (the shard's build has finished before any rank leaves)
+    uint64_t done_insert(uint64_t m) {
+        abi_check(kh_sync(t_));
+        comm_.barrier();
+        return m;
+    }
+
+    // One collective find round: every rank contributes {flags (1 = query, 2 = done), owner, key}
+    // (4 words), each owner answers the queries it owns with one batched kh_find, and the answers
+    // {found, record} (4 words per asker) are gathered back. done: this rank only serves (barrier);
+    // returns true when every rank was done in this round. Otherwise returns `found` for the query.
+    bool find_round(const uint8_t* key, uint8_t* rec_out, bool done) {
+        hip_check(hipSetDevice(device_), "hipSetDevice");
+        const uint64_t P = (uint64_t)P_, Pk = (uint64_t)((k_ + 3) / 4);
+        std::vector<uint64_t> q(4, 0), all(4 * P);
+        if (!done) {
+            const int owner = kh_key_owner(t_, key, P_);
+            if (owner < 0) abi_check(owner);
+            q[0] = 1;
+            q[1] = (uint64_t)owner;
+            std::memcpy(&q[2], key, Pk);
+        } else {
+            q[0] = 2;
+        }
+        comm_.allgather(q.data(), 4, all.data(), stream_);
+        bool any = false, all_done = true;
+        std::vector<uint8_t> keys, recs, found;
+        std::vector<int> asker;
+        for (uint64_t r = 0; r < P; ++r) {
+            const uint64_t* a = &all[4 * r];
+            all_done = all_done && (a[0] & 2);
+            if (!(a[0] & 1)) continue;
+            any = true;
+            if (a[1] != (uint64_t)rank_) continue;
+            keys.insert(keys.end(), reinterpret_cast<const uint8_t*>(&a[2]), reinterpret_cast<const uint8_t*>(&a[2]) + Pk);
+            asker.push_back((int)r);
+        }
+        if (!any) return all_done;  // nobody asked: every rank sees the same and skips the answers
+        std::vector<uint64_t> rep(4 * P, 0), rall(4 * P * P);
+        if (!asker.empty()) {
+            recs.assign(asker.size() * R_, 0);
+            found.assign(asker.size(), 0);
+            std::lock_guard<std::mutex> g(m_);
+            abi_check(kh_find(t_, keys.data(), asker.size(), recs.data(), found.data()));
+            for (size_t i = 0; i < asker.size(); ++i) {
+                rep[4 * asker[i]] = found[i];
+                std::memcpy(&rep[4 * asker[i] + 1], &recs[i * R_], R_);
+            }
+        }
+        comm_.allgather(rep.data(), 4 * P, rall.data(), stream_);
+        if (done) return false;
+        const uint64_t* ans = &rall[(q[1] * P + (uint64_t)rank_) * 4];
+        std::memcpy(rec_out, &ans[1], R_);
+        return ans[0] != 0;
+    }
+
     struct Exchange {
         std::vector<uint64_t> send, recv;  // per peer, in items
         uint64_t send_total = 0, recv_total = 0, total_all = 0, gmax = 0;
@@ -451,6 +549,7 @@ private:
     hipStream_t stream_ = nullptr, xstream_ = nullptr;
     uint64_t W_ = 2, R_ = 15;
     int rounds_ = 0, jump_rounds_ = 0;
+    uint64_t inserted_ = 0;  // k-mers this shard holds since the last clear
     std::mutex m_;
     std::vector<hipEvent_t> events_;
     DevBuf words_, recv_, counts_, a_, b_, tout_, trecv_, lout_, lin_, qout_, qin_, rep_, rin_, sout_, sin_, recs_;

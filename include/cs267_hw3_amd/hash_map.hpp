@@ -125,7 +125,9 @@ public:
         return shard_->find(key.data, reinterpret_cast<uint8_t*>(&result));
     }
     bool find(const std::string& key, kmer_pair& result) { return find(pkmer_t(key), result); }
-    void process_requests() {}  // hash_map.hpp:110-113: nothing is left pending between calls
+    // hash_map.hpp:110-113 (upcxx::progress + barrier): collective at world_size > 1; a rank that
+    // has finished its finds answers the others' until every rank is here
+    void process_requests() { barrier(); }
 
     // kmer_hash.cpp:38-68 in one call: walk every start k-mer collected by insert_all on the
     // device and return this rank's test_<rank>.dat bytes (collective at world_size > 1).

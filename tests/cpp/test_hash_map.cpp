@@ -3,6 +3,10 @@
 //   test_hash_map_<K> refloop <kmer_file> <P> <prefix>    the reference's own initialize_kmers +
 //        assemble_contigs + output_results (kmer_hash.cpp:21-68) over DistributedHashMap, P ranks
 //        as threads on GPU 0 (kh::ThreadComm; P = 1: the single-GPU table), one find() per step
+//   test_hash_map_<K> refloopc <kmer_file> <P> <prefix>   the same without a peer group and without
+//        the caller's barriers: every find() a collective round, process_requests() serving the rest
+//   test_hash_map_<K> rccl1loop <kmer_file> <prefix>      the reference loop over a one-rank RCCL
+//        communicator without a peer group (one process per GPU)
 //   test_hash_map_<K> rccl1   <kmer_file> <prefix>        DistributedHashMap over a one-rank RCCL
 //        communicator (sharded code path, RCCL all-gathers) -> <prefix>_0.dat
 //   test_hash_map_<K> gen     <n> <P> <len_min> <len_max> kh::ShardedTable at P ranks (threads, one
@@ -83,17 +87,20 @@ int stock(const std::string& fname) {
     return 0;
 }
 
-// kmer_hash.cpp:21-68, verbatim in structure (find per step), for one rank
-void ref_rank(const std::string& fname, int rank, int world, const std::string& prefix, size_t n_kmers) {
-    DistributedHashMap hashmap(n_kmers * 2, rank, world, 0);
+// kmer_hash.cpp:21-68, verbatim in structure (find per step), for one rank. sync: the explicit
+// barriers of a careful caller; without them the map's own collective points must do (insert_all
+// ends in a barrier, hash_map.hpp:79; process_requests() answers finds until every rank is done,
+// hash_map.hpp:110-113).
+void ref_rank(const std::string& fname, DistributedHashMap& hashmap, int rank, int world, const std::string& prefix,
+              bool sync) {
     std::vector<kmer_pair> kmers = read_kmers(fname, world, rank);
-    hashmap.barrier();
+    if (sync) hashmap.barrier();
     // initialize_kmers
     std::vector<kmer_pair> start_nodes;
     hashmap.insert_all(kmers);
     for (const auto& kmer : kmers)
         if (kmer.backwardExt() == 'F') start_nodes.push_back(kmer);
-    hashmap.barrier();
+    if (sync) hashmap.barrier();
     // assemble_contigs
     std::list<std::list<kmer_pair>> contigs;
     for (const auto& start_kmer : start_nodes) {
@@ -107,28 +114,35 @@ void ref_rank(const std::string& fname, int rank, int world, const std::string& 
         }
         contigs.push_back(contig);
     }
-    hashmap.barrier();  // every rank's finds are answered before any table goes away
+    // every rank's finds are answered before any table goes away
+    if (sync) hashmap.barrier();
+    else hashmap.process_requests();
     // output_results
     std::ofstream fout(prefix + "_" + std::to_string(rank) + ".dat");
     for (const auto& contig : contigs) fout << extract_contig(contig) << std::endl;
 }
 
-int refloop(const std::string& fname, int world, const std::string& prefix) {
+// mode "refloop": ranks as threads with a peer group (finds read the owner's table directly);
+// "refloopc": no peer group and no explicit barriers -- every find is a collective round (the
+// one-process-per-GPU protocol), driven by P threads over kh::ThreadComm
+int refloop(const std::string& fname, int world, const std::string& prefix, bool collective) {
     const size_t n = line_count(fname);
     if (world == 1) {
-        ref_rank(fname, 0, 1, prefix, n);
+        DistributedHashMap hashmap(n * 2, 0, 1, 0);
+        ref_rank(fname, hashmap, 0, 1, prefix, !collective);
         return 0;
     }
     kh::ThreadComm::Group group(world);
     auto& ctx = kh::rank_contexts();
     ctx.assign(world, kh::RankContext{});
-    for (int r = 0; r < world; ++r) ctx[r] = kh::RankContext{group.comm(r), 0, &group};
+    for (int r = 0; r < world; ++r) ctx[r] = kh::RankContext{group.comm(r), 0, collective ? nullptr : &group};
     std::vector<std::thread> th;
     int failed = 0;
     for (int r = 0; r < world; ++r)
         th.emplace_back([&, r] {
             try {
-                ref_rank(fname, r, world, prefix, n);
+                DistributedHashMap hashmap(n * 2, r, world, 0);
+                ref_rank(fname, hashmap, r, world, prefix, !collective);
             } catch (const std::exception& ex) {
                 fprintf(stderr, "rank %d: %s\n", r, ex.what());
                 failed = 1;
@@ -137,6 +151,16 @@ int refloop(const std::string& fname, int world, const std::string& prefix) {
         });
     for (auto& t : th) t.join();
     return failed;
+}
+
+// the reference's find loop over an RCCL communicator without a peer group (the
+// one-process-per-GPU shape, RcclComm(rank, world, id, device)), at one rank
+int rccl1loop(const std::string& fname, const std::string& prefix) {
+    auto comms = kh::RcclComm::init_all({0});
+    const size_t n = line_count(fname);
+    DistributedHashMap hashmap(n * 2, *comms[0], 0, nullptr);
+    ref_rank(fname, hashmap, 0, 1, prefix, false);
+    return 0;
 }
 
 int rccl1(const std::string& fname, const std::string& prefix) {
@@ -215,7 +239,9 @@ int main(int argc, char** argv) {
         if (mode == "gen" && argc >= 6)
             return gen(strtoull(argv[2], nullptr, 10), atoi(argv[3]), (uint32_t)atoi(argv[4]), (uint32_t)atoi(argv[5]));
         if (mode == "stock") return stock(fname);
-        if (mode == "refloop" && argc >= 5) return refloop(fname, atoi(argv[3]), argv[4]);
+        if (mode == "refloop" && argc >= 5) return refloop(fname, atoi(argv[3]), argv[4], false);
+        if (mode == "refloopc" && argc >= 5) return refloop(fname, atoi(argv[3]), argv[4], true);
+        if (mode == "rccl1loop" && argc >= 4) return rccl1loop(fname, argv[3]);
         if (mode == "rccl1" && argc >= 4) return rccl1(fname, argv[3]);
     } catch (const std::exception& ex) {
         fprintf(stderr, "%s\n", ex.what());

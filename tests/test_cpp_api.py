@@ -58,6 +58,28 @@ def test_reference_find_loop(tmp_path, name, k, P):
     _check_ranks(tmp_path, name, P)
 
 
+@pytest.mark.parametrize("P", [1, 2, 3, 8])
+@pytest.mark.parametrize("name,k", [("tiny19", 19), ("small51", 51)])
+def test_reference_find_loop_collective(tmp_path, name, k, P):
+    """kmer_hash.cpp:38-55 without a peer group (the one-process-per-GPU protocol: every find() a
+    collective round, process_requests() answering until all ranks are done) and without the
+    caller's barriers: a find() right after insert_all relies on insert_all's own barrier."""
+    r = subprocess.run([_exe("test", k), "refloopc", os.path.join(GOLDEN, f"{name}.txt"), str(P), "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    _check_ranks(tmp_path, name, P)
+
+
+@pytest.mark.parametrize("name,k", [("tiny19", 19), ("small51", 51)])
+def test_reference_find_loop_over_rccl(tmp_path, name, k):
+    """The reference's find loop over RcclComm without a peer group, one rank (one process per GPU)."""
+    r = subprocess.run([_exe("test", k), "rccl1loop", os.path.join(GOLDEN, f"{name}.txt"), "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert open(tmp_path / "out_0.dat", "rb").read() == \
+        open(os.path.join(GOLDEN, f"{name}_test_0.dat"), "rb").read()
+
+
 @pytest.mark.parametrize("P", [2, 3, 8])
 @pytest.mark.parametrize("name,k", [("mixed19", 19), ("small51", 51), ("singles51", 51), ("k60", 60)])
 def test_driver_multirank_threads(tmp_path, name, k, P):
