@@ -28,6 +28,11 @@ WORKLOADS = {
     "c2": dict(k=19, n=10_000_000, len_min=200, len_max=1374, single=0, seed=19,
                desc="C2: k=19, 10M synthetic k-mers per GPU, contigs U[200,1374] k-mers "
                     "(test.txt-like mean 787), table load 0.5"),
+    # BASELINE.json configs[3]: k=51, 1B k-mers sharded across the GPUs (strong scaling: the
+    # block split of read_kmers.hpp:55-58 over the ranks; at one rank the whole 1B on one GPU)
+    "c4": dict(k=51, n=1_000_000_000, len_min=8, len_max=200, single=0, seed=5101, strong=True,
+               desc="C4: k=51, 1B synthetic k-mers in all, block split over the GPUs, contigs U[8,200] "
+                    "k-mers"),
     # BASELINE.json configs[4]: skewed set, 8 chains of 10^6 k-mers among
     # short contigs U[2,16], every start k-mer first in record order (the block split hands all
     # walkers to the first rank)
@@ -114,7 +119,8 @@ def cpu_baseline(w, host_recs, truth, sample_n):
 
 
 def load_traffic(workload, n_per_gpu):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (workload key: e.g. "c3", or "c3_dist" for the sharded path at one rank)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
@@ -180,6 +186,7 @@ def main():
     args = ap.parse_args()
 
     w = dict(WORKLOADS[args.workload])
+    w["name"] = args.workload
     if args.n:
         w["n"] = args.n
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,7 +196,7 @@ def main():
     if world > 1 or os.environ.get("KH_BENCH_FORCE_DIST") == "1":
         # sharded path (also forced at one rank to exercise it on a 1-GPU box)
         from cs267_hw3_amd import dist
-        return dist.bench_main(args, w, world, rank)
+        return dist.bench_main(args, w, world, rank, cpu_baseline=cpu_baseline, load_traffic=load_traffic)
 
     import numpy as np
     import cs267_hw3_amd as kh
@@ -197,6 +204,8 @@ def main():
     k, n = w["k"], w["n"]
     t = time.time()
     g = kh.SyntheticKmers(k, n, w["len_min"], w["len_max"], w["single"], seed=w["seed"], **w.get("gen", {}))
+    if w.get("strong"):
+        log("note: a strong-scaling workload on one GPU: the whole set on this GPU")
     host = g.records()
     log(f"generated {n} records ({host.nbytes / 1e9:.2f} GB) in {time.time() - t:.1f}s")
     L = kh._lib.lib()

@@ -383,7 +383,7 @@ __device__ __forceinline__ void clean_out(uint64_t& w0, uint64_t& w1, const KPar
 // y's home is this region's; a tie in the top bits counts as "no link" (never a wrong link).
 template <int W, bool MTOP>
 __device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned long long* lt, uint32_t S,
-                                               uint64_t lo, uint64_t cap, uint64_t w0, uint64_t w1) {
+                                               uint64_t lo, uint64_t cap, uint64_t w0, uint64_t w1, bool dense = false) {
     const uint32_t f = ext_fwd(slot_ext(w0));
     const uint32_t j = slot_jstar(w0) & (W == 1 ? 31u : 63u);
     if (f > 3u || (int)j >= p.K - p.M) return NO_SUCC;
@@ -401,7 +401,12 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned 
     const uint64_t home = MTOP ? home_in(lo, lo + S, hy) : home_of(place_w(mw, y, p), cap, p);
     if (home < lo || home >= lo + S) return NO_SUCC;
     const uint64_t want0 = W == 1 ? y.lo : y.hi;
-    if (KH_LDS_BLOCK && MTOP) {  // block steps (see lds_insert_blk): ~d/4 steps for a run of d slots
+#ifndef KH_LINK_MODE
+#define KH_LINK_MODE 1
+#endif
+    // block steps (see lds_insert_blk): ~d/4 steps for a run of d slots (KH_LINK_MODE: 0 slot
+    // steps, 1 block steps, 2 block steps in dense slices)
+    if (KH_LDS_BLOCK && MTOP && (KH_LINK_MODE == 1 || (KH_LINK_MODE == 2 && dense))) {
         for (uint32_t t = (uint32_t)(home - lo); t < S;) {
             const uint32_t base = t & ~3u;
             uint64_t v[4];
@@ -651,12 +656,16 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         }
     };
     uint32_t r = blockIdx.x;
-    load(r, fill(r), a, b);
+    uint32_t m_cur = fill(r);
+    load(r, m_cur, a, b);
     const uint32_t NR = nreg(p);
     for (; r < NR; r += gridDim.x) {
         const uint64_t lo = rbt[r], hi = rbt[r + 1];
         const uint32_t S = (uint32_t)(hi - lo);
         const uint32_t m_next = fill(r + gridDim.x);  // in flight during this region
+        // block-step probing (lds_insert_blk) where the slice fills above ~2/3 (balanced tables at
+        // load 0.85: build 21.3 -> 13.0 ms); slot steps below (C3 at 0.5: 3.71 vs 3.90 ms)
+        const bool dense = KH_LDS_BLOCK && 3u * m_cur > 2u * S;
         if (threadIdx.x == 0) hcnt = 0;
         if (W == 2) {
             ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
@@ -685,8 +694,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             // every word of region r's window is a key of region r; the slot keeps key, ext and j*
             // (the order bits stay in the register copy for the link test)
             const uint64_t home = home_in(lo, hi, key_hash32(slot_key(a[j], b[j], p)));
-            pos[j] = KH_LDS_BLOCK ? lds_insert_blk<W>(p, lt, S, (uint32_t)(home - lo), slot_clean(a[j], p), b[j], stats)
-                                  : lds_insert<W>(p, lt, S, home - lo, slot_clean(a[j], p), b[j], stats);
+            pos[j] = dense ? lds_insert_blk<W>(p, lt, S, (uint32_t)(home - lo), slot_clean(a[j], p), b[j], stats)
+                           : lds_insert<W>(p, lt, S, home - lo, slot_clean(a[j], p), b[j], stats);
             if (pos[j] == LDS_OUT) {  // rare after the hot remap: a per-lane atomic (no spills)
                 const unsigned long long idx = atomicAdd(&ctr[CT_OVF2], 1ull);
                 if (idx < ovf_cap) {
@@ -710,7 +719,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             // registers (no pass over empty slots) and every key knows its slot
 #pragma unroll
             for (int j = 0; j < IPT; ++j)
-                if (pos[j] >= 0) put_link<W>(lt, (uint32_t)pos[j], chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j]), p);
+                if (pos[j] >= 0)
+                    put_link<W>(lt, (uint32_t)pos[j], chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j], dense), p);
             load(r + gridDim.x, m_next, a, b);
             lds_barrier();
             BPROF(2);
@@ -754,6 +764,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         }
         lds_barrier();
         BPROF(5);
+        m_cur = m_next;
     }
 }
 
@@ -1720,9 +1731,9 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
                                                stats, s, after_records, nullptr, 0, before_build);
     }
     return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s,
-                                            nullptr, wsplits, wsplits_cap)
+                                            nullptr, wsplits, wsplits_cap, before_build)
                     : part_insert<2, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s,
-                                            nullptr, wsplits, wsplits_cap);
+                                            nullptr, wsplits, wsplits_cap, before_build);
 }
 
 }  // namespace kh

@@ -974,12 +974,14 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
         if (int rc = clean_slots(t)) return rc;
     t->slots_stale = false;
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
-    if (part)
+    t->build_timed = part;
+    if (part) {
         KH_HIP(kh::launch_part_insert(coll ? mseg_params(t) : t->kp, nullptr, (const uint64_t*)words, m, view(t),
                                       fresh, pb, nullptr, nullptr, t->ctr.as<unsigned long long>(),
                                       t->stats.as<unsigned long long>(), t->stream, nullptr,
-                                      coll ? t->splits.as<uint64_t>() : nullptr, coll ? t->splits_cap : 0));
-    else {
+                                      coll ? t->splits.as<uint64_t>() : nullptr, coll ? t->splits_cap : 0, t->ev_b0));
+        KH_HIP(hipEventRecord(t->ev_b1, t->stream));
+    } else {
         if (int rc = cas_hot_prepass(t, nullptr, words, m)) return rc;
         KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
                                        t->stats.as<unsigned long long>(), t->stream));
@@ -1051,11 +1053,14 @@ int kh_insert_words_finish(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (!t->staging) return fail(KH_ERR_STATE, "no staged insert open");
     if (int rc = set_device(t)) return rc;
+    t->build_timed = t->stage_part;
     if (t->stage_part) {
         kh::PartBuffers b{};
         if (int rc = ensure_part(t, t->stage_total, b)) return rc;
+        KH_HIP(hipEventRecord(t->ev_b0, t->stream));
         KH_HIP(kh::launch_part_finish(t->kp, t->stage_total, view(t), t->stage_fresh, b, t->ctr.as<unsigned long long>(),
                                       t->stats.as<unsigned long long>(), t->stream));
+        KH_HIP(hipEventRecord(t->ev_b1, t->stream));
         t->slots_stale = false;
     }
     KH_HIP(hipEventRecord(t->ev_ins1, t->stream));

@@ -620,8 +620,10 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
     return out
 
 
-def bench_main(args, w, world, rank):
-    """bench.py body for N > 1 ranks (torch.distributed.run, one rank per GPU)."""
+def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
+    """bench.py body for N > 1 ranks (torch.distributed.run, one rank per GPU), or forced at one
+    rank (KH_BENCH_FORCE_DIST=1). Weak scaling (n k-mers per GPU) unless the workload is strong
+    (C4: n k-mers in all, block split over the ranks, read_kmers.hpp:55-58)."""
     import json
     import os
     import sys
@@ -635,18 +637,19 @@ def bench_main(args, w, world, rank):
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     comm = TorchComm()
-    k, n_per = w["k"], w["n"]
-    n_total = n_per * world  # weak scaling: n k-mers per GPU
+    k = w["k"]
+    strong = bool(w.get("strong"))
+    n_total = w["n"] if strong else w["n"] * world
+    n_per = (n_total + world - 1) // world
     t = time.time()
     g = SyntheticKmers(k, n_total, w["len_min"], w["len_max"], w["single"], seed=w["seed"], **w.get("gen", {}))
     b, e = g.block(world, rank)
-    host = g.records(b, e)
-    recs = torch.from_numpy(host).to(torch.device("cuda", local))
-    del host
+    recs = g.records_dev(b, e, device=local)  # the rank's block, generated in its HBM
+    torch.cuda.synchronize()
     print(f"[rank {rank}] generated {e - b} records in {time.time() - t:.1f}s", file=sys.stderr,
           flush=True)
-    # each shard holds ~n_total/world keys; hash imbalance is tiny at this size, give 2% slack
-    shard = GpuShard(k, int(n_per * 1.02) + 4096, device=local)
+    # each shard holds ~n_total/world keys (it grows to what it is routed); 2 % slack
+    shard = GpuShard(k, int(n_per * 1.02) + 4096, device=local, load_factor=getattr(args, "load", 0.5))
     dm = DistributedKmerHashMap(comm, shard)
     R = record_size(k)
 
@@ -669,7 +672,7 @@ def bench_main(args, w, world, rank):
 
     for _ in range(args.warmup):
         step()
-    times = []
+    times, phases = [], []
     for _ in range(args.steps):
         dist.barrier()
         torch.cuda.synchronize()
@@ -678,13 +681,12 @@ def bench_main(args, w, world, rank):
         torch.cuda.synchronize()
         dist.barrier()
         times.append(time.perf_counter() - t0)
+        phases.append(shard.stats())
     print(f"[rank {rank}] step ms: " + " ".join(f"{1e3 * x:.2f}" for x in times), file=sys.stderr, flush=True)
     mine = sum(times) / len(times)
     tmax = comm.all_reduce_max(mine)
-    st = shard.stats()
-    nc_local = st["n_starts"]
-    look_local = st["n_lookups"]
-    tot = torch.tensor([nc_local, look_local], dtype=torch.int64, device="cuda")
+    st = phases[-1]
+    tot = torch.tensor([st["n_starts"], st["n_lookups"]], dtype=torch.int64, device="cuda")
     dist.all_reduce(tot)
     nc, nl = tot.tolist()
     ok = None
@@ -695,31 +697,52 @@ def bench_main(args, w, world, rank):
         ok = bool(okt.item())
         if not ok and rank == 0:
             print("bench: contig text differs from the generator ground truth", file=sys.stderr)
+    cpu = None
+    if rank == 0 and cpu_baseline is not None and not args.no_cpu:
+        # the CPU restatement of the reference on a bounded sample of the same generator/config
+        # (whole contigs: a rank's block of shuffled records is not a closed set), rank 0 only,
+        # after the timed region; the other ranks wait at the closing barrier
+        t = time.time()
+        sn = min(args.cpu_sample or 20_000_000, n_per)
+        gs = SyntheticKmers(k, sn, w["len_min"], w["len_max"], w["single"], seed=w["seed"], **w.get("gen", {}))
+        cpu = cpu_baseline(w, gs.records(), gs.truth(), 0)
+        cpu["sample"] = f"a {sn}-k-mer set of the same generator/config (rank 0's host share); " + cpu["sample"]
+        print(f"cpu baseline took {time.time() - t:.1f}s", file=sys.stderr, flush=True)
     if rank == 0:
         value = (n_total + nl) / tmax
-        ins_ms = st["ms_insert_kernel"]
+        avg = lambda key: sum(p[key] for p in phases) / len(phases)  # noqa: E731
+        build_ms, ins_ms = avg("ms_build"), avg("ms_insert_kernel")
+        units = st["n_inserted"]
         b_alg = 2 * R
-        achieved = shard.table.stats()["n_inserted"] * b_alg / (ins_ms / 1e3) / 1e9 if ins_ms else 0.0
+        traffic, tsrc = (load_traffic(w.get("name", "") + "_dist", n_per) if load_traffic else (None, None))
+        tb = traffic.get("k_part_build") if traffic else None
+        achieved = units * b_alg / (build_ms / 1e3) / 1e9 if build_ms else 0.0
         out = {
             "metric": "k-mer inserts+lookups/sec (k=51)" if k == 51 else f"k-mer inserts+lookups/sec (k={k})",
             "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": tmax * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": value / 72.6e6, "dtype": "u64", "data": "synthetic",
+            "scaling": "strong" if strong else "weak", "vs_baseline": value / 72.6e6, "dtype": "u64",
+            "data": "synthetic",
             "config": {"workload": w["desc"], "k": k, "n_kmers_total": n_total,
                        "n_kmers_per_gpu": n_per, "contigs": nc, "lookups": nl,
+                       "load_factor": getattr(args, "load", 0.5),
                        "parallelism": f"{world} GPUs, key space sharded by "
                                       f"{'minimizer' if os.environ.get('KH_OWNER') != 'hash' else 'hash'} owner, "
                                       f"RCCL all-to-all per migrating-walker round",
                        "walk_rounds": dm.rounds},
             "inserts_per_s": n_total / tmax, "lookups_per_s": nl / tmax,
             "contigs_per_s": nc / tmax, "verified_vs_truth": ok,
-            "roofline": {"bound": "hbm", "kernel": "insert pipeline on the received words (rank 0: "
-                                                     "k_part1_hist .. k_part_build)",
+            "phases_ms": {"insert_pipeline_rank0": ins_ms, "build_rank0": build_ms},
+            "roofline": {"bound": "hbm", "kernel": "k_part_build_pf (rank 0's region build + chains over the "
+                                                     "words it received)",
                          "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
-                         "traffic": None, "alg_bytes_per_unit": b_alg, "avg_launch_ms": ins_ms,
-                         "note": "achieved = inserts x 2*sizeof(kmer_pair) / HIP-event time of the "
-                                 "insert kernels of the last step; traffic: see profiles/pmc_traffic.json"},
-            "cpu_baseline": None,
+                         "traffic": tb, "alg_bytes_per_unit": b_alg, "units_per_launch": units,
+                         "avg_launch_ms": build_ms,
+                         "traffic_GBs": (tb / (build_ms / 1e3) / 1e9) if tb and build_ms else None,
+                         "note": "achieved = k-mers in rank 0's shard x 2*sizeof(kmer_pair) / HIP-event time of "
+                                 "the build" + (f"; traffic = PMC HBM bytes per launch from {tsrc} (sharded "
+                                                f"path at one rank)" if tb else "")},
+            "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     torch.cuda.synchronize()
@@ -727,4 +750,3 @@ def bench_main(args, w, world, rank):
     dist.destroy_process_group()
     dm.close()
     shard.table.close()
-    return 0

@@ -21,14 +21,16 @@ KERNELS = {"k_insert": ("k_insert<",), "k_walk": ("k_walk<", "k_walk_g<", "k_wal
            "k_part1_scatter": ("k_part1_scatter<",), "k_part2_hist": ("k_part2_hist<",),
            "k_part2_scatter": ("k_part2_scatter<",), "k_part2_res": ("k_part2_res<",),
            "k_part_build": ("k_part_build<", "k_part_build_pf<"), "k_insert_overflow": ("k_insert_overflow<",),
+           "k_route_own": ("k_route_own",), "k_route_scatter": ("k_route_scatter",), "k_mw_run": ("k_mw_run",),
+           "k_ovf_scatter": ("k_ovf_scatter<",),
            "membench_gather16": ("k_gather16",), "membench_chase16": ("k_chase16",),
            "membench_chase64q": ("k_chasegILi4",), "membench_chase128o": ("k_chasegILi8",)}
 # kernels of the insert pipeline (whichever of them ran)
 PIPELINE = ["k_part1_convert", "k_part1_fused", "k_win1", "k_win1_rec", "k_part1_scatter", "k_part2_hist", "k_part2_scatter",
-            "k_part2_res", "k_win2", "k_part_build", "k_insert_overflow"]
+            "k_part2_res", "k_win2", "k_ovf_scatter", "k_part_build", "k_insert_overflow", "k_route_own", "k_route_scatter"]
 # random-access kernels: FETCH_SIZE is NOT doubled (the 1/2 correction is for wide coalesced
 # streaming reads); their requests are calibrated against tools/membench (random 16-B loads)
-RANDOM = {"k_walk", "k_insert", "k_insert_overflow", "membench_gather16", "membench_chase16",
+RANDOM = {"k_walk", "k_insert", "k_insert_overflow", "k_mw_run", "membench_gather16", "membench_chase16",
           "membench_chase64q", "membench_chase128o"}
 
 

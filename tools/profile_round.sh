@@ -26,4 +26,19 @@ if [ -x tools/membench ]; then
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $PWD/$OUT/cal_WRITE_SIZE -- tools/membench calib > $OUT/cal_WRITE_SIZE.log 2>&1
   python3 tools/pmc_traffic.py membench 0 $OUT/cal_ $OUT/pmc_traffic.json > /dev/null
 fi
+# the sharded path at one rank (KH_BENCH_FORCE_DIST: route, routed-word build, migrating walk):
+# its PMC traffic goes in as workload "c3_dist" (the N > 1 bench line reads it). The env makes
+# rank 0 of a one-rank process group without the torchrun launcher (the profiler runs python).
+if [ -z "${NO_DIST:-}" ]; then
+  D="python3 bench.py --steps 3 --warmup 1 --no-cpu --e2e-steps 0 --no-verify ${BARGS:-}"
+  export KH_BENCH_FORCE_DIST=1 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$OUT/dtrace -- $D > $OUT/dtrace.log 2>&1
+  python3 tools/kstats.py $OUT/dtrace > $OUT/kernel_stats_dist.txt
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 400 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $PWD/$OUT/dpmc_$c -- $D > $OUT/dpmc_$c.log 2>&1
+  done
+  python3 tools/pmc_traffic.py c3_dist 200000000 $OUT/dpmc_ $OUT/pmc_traffic.json > /dev/null
+  grep '"metric"' $OUT/dtrace.log > $OUT/bench_dist_under_trace.json || true
+  unset KH_BENCH_FORCE_DIST RANK WORLD_SIZE LOCAL_RANK MASTER_ADDR MASTER_PORT
+fi
 echo "profile $TAG done"
