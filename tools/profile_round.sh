@@ -17,6 +17,10 @@ for c in FETCH_SIZE WRITE_SIZE TCC_EA0_ATOMIC_sum; do
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum --output-format csv -d $PWD/$OUT/pmc_RDREQ -- $B > $OUT/pmc_RDREQ.log 2>&1
 python3 tools/pmc_traffic.py c3 200000000 $OUT/pmc_ $OUT/pmc_traffic.json > /dev/null
+# one pass of the 8 SQ counters behind DESIGN's bound statements (wave parking, VALU, LDS conflicts)
+SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
+timeout -k 10 400 rocprofv3 --kernel-trace --pmc $SQ --output-format csv -d $PWD/$OUT/pmc_SQ -- $B > $OUT/pmc_SQ.log 2>&1
+python3 tools/sq_summary.py $OUT/pmc_SQ > $OUT/sq_counters.json
 grep '"metric"' $OUT/trace.log > $OUT/bench_under_trace.json || true
 if [ -x tools/membench ]; then
   for c in FETCH_SIZE; do
