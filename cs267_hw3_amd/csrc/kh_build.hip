@@ -1711,6 +1711,56 @@ hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m
                     : part_stage<2>(p, words, m, total, first, b, ctr, stats, s, wsplits, wsplits_cap, sample, cap);
 }
 
+// Staged build from reference records (kh_insert's chunked host upload): the chunk is converted
+// (start / splitter bits into its slice of the masks, words into words_tmp), then partitioned like
+// a routed chunk; first: counters of the build; sample: this chunk's 1-in-256 sample marks the hot
+// regions before its pass 1.
+template <int W>
+static hipError_t part_stage_recs(const KParams& p, const uint8_t* recs, uint64_t m, uint64_t total, bool first,
+                                  const PartBuffers& B, uint64_t* words_tmp, uint64_t* start_mask, uint64_t* split_mask,
+                                  unsigned long long* ctr, unsigned long long* stats, hipStream_t s, bool sample,
+                                  uint64_t cap) {
+    hipError_t e;
+    if (first) {
+        if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
+    }
+    if (m == 0) return hipSuccess;
+    const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(p, total);
+    const bool samp_on = sample && !debug_flag("no_hot_sample");
+    uint32_t* samp = samp_on ? B.rcnt : nullptr;
+    const unsigned nb = (unsigned)((m + (uint64_t)T1 * PART_TILE - 1) / ((uint64_t)T1 * PART_TILE));
+    if (W == 2 && p.K == 51)
+        k_part1_convert<W, 13, 51><<<nb, PB, 0, s>>>(p, recs, m, words_tmp, start_mask, split_mask, samp);
+    else if (W == 1 && p.K == 19)
+        k_part1_convert<W, 5, 19><<<nb, PB, 0, s>>>(p, recs, m, words_tmp, start_mask, split_mask, samp);
+    else if (p.P == 13)
+        k_part1_convert<W, 13><<<nb, PB, 0, s>>>(p, recs, m, words_tmp, start_mask, split_mask, samp);
+    else if (p.P == 5)
+        k_part1_convert<W, 5><<<nb, PB, 0, s>>>(p, recs, m, words_tmp, start_mask, split_mask, samp);
+    else
+        k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, m, words_tmp, start_mask, split_mask, samp);
+    if (samp_on && (e = sample_mark(p, cap, m, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess)
+        return e;
+    if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
+    if ((e = win1_launch<W>(p, words_tmp, m, CAP1, B.wcnt, B, part_overflow_cap(total), ctr, stats, s, nullptr, 0,
+                            true)) != hipSuccess)
+        return e;
+    if ((e = win2_launch<W>(p, B, m, RC, B.rcnt, part_overflow_cap(total), ctr, stats, CAP1, B.wcnt, s)) != hipSuccess)
+        return e;
+    return hipGetLastError();
+}
+
+hipError_t launch_part_stage_recs(const KParams& p, const uint8_t* recs, uint64_t m, uint64_t total, bool first,
+                                  const PartBuffers& b, uint64_t* words_tmp, uint64_t* start_mask,
+                                  uint64_t* split_mask, unsigned long long* ctr, unsigned long long* stats,
+                                  hipStream_t s, bool sample, uint64_t cap) {
+    return p.W == 1 ? part_stage_recs<1>(p, recs, m, total, first, b, words_tmp, start_mask, split_mask, ctr, stats, s,
+                                         sample, cap)
+                    : part_stage_recs<2>(p, recs, m, total, first, b, words_tmp, start_mask, split_mask, ctr, stats, s,
+                                         sample, cap);
+}
+
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
                               const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
                               hipStream_t s) {

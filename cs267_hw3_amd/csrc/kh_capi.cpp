@@ -505,11 +505,92 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     return KH_OK;
 }
 
+// kh_insert of a large batch into an empty table (the reference's boundary: records in host
+// memory, kmer_hash.cpp:129): the records go up in chunks on the side stream while the table's
+// stream converts and partitions each chunk that has landed (passes 1-2 into the region windows);
+// one build after the last chunk. The upload is the bound (~55 GB/s over PCIe for 3 GB at C3);
+// all device work but the last chunk's passes, the build and the walk hides behind it.
+static int insert_chunked_upload(kh_table* t, const uint8_t* host_recs, uint64_t n) {
+    const uint64_t R = (uint64_t)t->kp.R, W = (uint64_t)t->kp.W;
+    // chunks of a multiple of 8192 records (the convert pass's tiles; start-mask words stay whole)
+    uint64_t nch = 8;
+    uint64_t chunk = ((n + nch - 1) / nch + 8191) & ~8191ull;
+    nch = (n + chunk - 1) / chunk;
+    int rc;
+    if ((rc = t->stage.ensure(n * R + 16))) return rc;
+    if ((rc = t->stage2.ensure(chunk * W * 8 + 16))) return rc;
+    const uint64_t nw = (n + 63) / 64;
+    const bool split = t->kp.split_bits > 0;
+    if ((rc = t->mask.ensure(nw * 8 * (split ? 2 : 1)))) return rc;
+    if ((rc = t->mask_off.ensure(nw * 8))) return rc;
+    if ((rc = t->scratch.ensure(kh::scan_scratch_words(nw > n ? nw : n) * 8 + 64))) return rc;
+    if ((rc = ensure_starts(t, n))) return rc;
+    if (split && (rc = ensure_list(t, t->splits, t->splits_cap, n))) return rc;
+    uint64_t* start_mask = t->mask.as<uint64_t>();
+    uint64_t* split_mask = split ? start_mask + nw : nullptr;
+    kh::PartBuffers pb{};
+    if ((rc = ensure_part(t, n, pb))) return rc;
+    struct Events {  // one per chunk: its upload landed
+        std::vector<hipEvent_t> e;
+        ~Events() {
+            for (auto x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } ev;
+    ev.e.assign(nch, nullptr);
+    for (auto& e : ev.e) KH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    uint8_t* d = t->stage.as<uint8_t>();
+    unsigned long long* ctr = t->ctr.as<unsigned long long>();
+    unsigned long long* stats = t->stats.as<unsigned long long>();
+    auto upload = [&](uint64_t c) -> hipError_t {
+        const uint64_t b = c * chunk, m = (b + chunk < n ? chunk : n - b);
+        hipError_t e = hipMemcpyAsync(d + b * R, host_recs + b * R, m * R, hipMemcpyHostToDevice, t->side);
+        return e != hipSuccess ? e : hipEventRecord(ev.e[c], t->side);
+    };
+    // the side stream starts after everything already queued on the table's stream; chunk c + 1's
+    // upload is queued after chunk c's passes, so a pageable (host-synchronous) copy overlaps too
+    KH_HIP(hipEventRecord(t->ev_side, t->stream));
+    KH_HIP(hipStreamWaitEvent(t->side, t->ev_side, 0));
+    KH_HIP(upload(0));
+    KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
+    t->slots_stale = false;  // the build of an empty table writes every slot
+    for (uint64_t c = 0; c < nch; ++c) {
+        const uint64_t b = c * chunk, m = (b + chunk < n ? chunk : n - b);
+        KH_HIP(hipStreamWaitEvent(t->stream, ev.e[c], 0));
+        KH_HIP(kh::launch_part_stage_recs(t->kp, d + b * R, m, n, c == 0, pb, t->stage2.as<uint64_t>(),
+                                          start_mask + b / 64, split ? split_mask + b / 64 : nullptr, ctr, stats,
+                                          t->stream, c == 0, t->cap));
+        KH_HIP(kh::launch_collect_starts(t->kp, d + b * R, m, start_mask + b / 64, t->mask_off.as<uint64_t>(),
+                                         t->scratch.as<uint64_t>(), t->starts.as<uint64_t>(), ctr, t->stream));
+        if (split)
+            KH_HIP(kh::launch_collect_starts(t->kp, d + b * R, m, split_mask + b / 64, t->mask_off.as<uint64_t>(),
+                                             t->scratch.as<uint64_t>(), t->splits.as<uint64_t>(), ctr, t->stream,
+                                             kh::CT_N_SPLIT));
+        if (c + 1 < nch) KH_HIP(upload(c + 1));
+    }
+    KH_HIP(hipEventRecord(t->ev_b0, t->stream));
+    KH_HIP(kh::launch_part_finish(t->kp, n, view(t), true, pb, ctr, stats, t->stream));
+    KH_HIP(hipEventRecord(t->ev_b1, t->stream));
+    KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
+    KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
+    t->build_timed = t->ins_timed = true;
+    t->last_insert_part = true;
+    t->n_inserted += n;
+    t->assembled = false;
+    KH_HIP(hipStreamSynchronize(t->stream));
+    return check_stats(t);
+}
+
 int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (n == 0) return KH_OK;
     if (!host_recs) return fail(KH_ERR_ARG, "null records");
     if (int rc = set_device(t)) return rc;
+    if (t->n_inserted + n > t->n_kmers)
+        return fail(KH_ERR_FULL, "inserting %llu k-mers into a table created for %llu (%llu in)",
+                    (unsigned long long)n, (unsigned long long)t->n_kmers, (unsigned long long)t->n_inserted);
+    if (t->n_inserted == 0 && n >= (1ull << 24) && use_part_build(t, n) && !kh::debug_flag("whole_upload"))
+        return insert_chunked_upload(t, host_recs, n);
     const uint64_t bytes = n * (uint64_t)t->kp.R;
     if (int rc = t->stage.ensure(bytes)) return rc;
     KH_HIP(hipMemcpyAsync(t->stage.p, host_recs, bytes, hipMemcpyHostToDevice, t->stream));

@@ -313,6 +313,12 @@ hipError_t launch_part_stage(const KParams& p, const uint64_t* words, uint64_t m
                              const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
                              hipStream_t s, uint64_t* word_splits = nullptr, uint64_t word_splits_cap = 0,
                              bool sample = false, uint64_t cap = 0);
+// The same from reference records (converted into words_tmp, chunk records' start / splitter
+// bits into start_mask / split_mask): kh_insert's chunked upload.
+hipError_t launch_part_stage_recs(const KParams& p, const uint8_t* recs, uint64_t m, uint64_t total, bool first,
+                                  const PartBuffers& b, uint64_t* words_tmp, uint64_t* start_mask,
+                                  uint64_t* split_mask, unsigned long long* ctr, unsigned long long* stats,
+                                  hipStream_t s, bool sample, uint64_t cap);
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
                               const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
                               hipStream_t s);

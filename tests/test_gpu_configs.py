@@ -1,6 +1,7 @@
 """Every BASELINE.json config at the size it names, on the GPU:
 
-  C2  k=19, 10M k-mers, one GPU                 -> test_gpu_parity.py (generator truth, 10M)
+  C2  k=19, 10M k-mers, one GPU                 -> byte-compared to the oracle (device and host
+      inserts); test_gpu_parity.py (generator truth, 10M)
   C3  k=51, 200M k-mers, one GPU, load 0.5      -> byte-compared to the generator's ground truth;
       a C3-shape 20M sample byte-compared to the oracle (oracle/kmer_oracle.c, ~7 s)
   C4  k=51, 1B k-mers sharded over 8 ranks      -> 8 logical ranks on one GPU (ThreadComm): each
@@ -80,6 +81,56 @@ def test_c3_shape_20m_vs_oracle():
     text, st = _single_gpu(g, n)
     assert st["n_contigs"] == nc
     assert text == want
+
+
+def _host_insert(g, recs, n, load=0.5):
+    """The reference boundary: records in host memory through kh_insert (>= 2^24 records into an
+    empty table: the chunked upload, H2D overlapped with the partition passes)."""
+    with kh.KmerHashTable(g.k, n, load) as t:
+        t.insert_all(recs)
+        t.assemble()
+        st = t.stats()
+        assert st["n_dup"] == 0 and st["n_full"] == 0 and st["n_missing"] == 0
+        return t.contigs_text(), st
+
+
+@pytest.mark.parametrize("load", [0.5, 0.85])
+def test_c3_shape_20m_host_insert_vs_oracle(load):
+    """kh_insert from host records (chunked upload) == the oracle on the 20M C3-shape set."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_bind as ob
+    n = 20_000_000
+    g = _gen(C3, n)
+    recs = g.records()
+    rc, want, nc, _, _, _ = ob.assemble(51, recs)
+    assert rc == 0
+    text, st = _host_insert(g, recs, n, load)
+    assert st["n_contigs"] == nc and text == want
+
+
+def test_c2_10m_vs_oracle():
+    """BASELINE configs[1] (k=19, 10M) byte-compared to the oracle, device and host inserts."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_bind as ob
+    n = 10_000_000
+    g = _gen(dict(C3, k=19, seed=19, len_min=200, len_max=1374), n)
+    recs = g.records()
+    rc, want, nc, _, _, _ = ob.assemble(19, recs)
+    assert rc == 0
+    text, st = _single_gpu(g, n)
+    assert st["n_contigs"] == nc and text == want
+    text, st = _host_insert(g, recs, n)
+    assert st["n_contigs"] == nc and text == want
+
+
+def test_chunked_upload_hot_bucket_vs_truth():
+    """The chunked upload samples hot regions from its first chunk only: the C5 hot-bucket set at
+    40M through kh_insert still assembles to the truth with the hot regions found."""
+    n = 40_000_000
+    g = _gen(C5H, n)
+    text, st = _host_insert(g, g.records(), n)
+    assert st["n_contigs"] == g.num_contigs and st["n_hot_regions"] >= 8
+    assert text == g.truth()
 
 
 @pytest.mark.parametrize("load", [0.5, 0.85])
