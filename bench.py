@@ -148,22 +148,49 @@ def end_to_end(table, host, n, nl, truth, steps):
     nb = ctypes.c_uint64(0)
     nco = ctypes.c_uint64(0)
 
-    def step():
+    def step(ph=None):
+        t0 = time.perf_counter()
         table.clear()
         kh._lib.check(L.kh_insert(table._h, ctypes.c_void_p(pin.data_ptr()), n))
+        t1 = time.perf_counter()
         kh._lib.check(L.kh_assemble(table._h, ctypes.byref(nco), ctypes.byref(nb)))
+        t2 = time.perf_counter()
         kh._lib.check(L.kh_contigs_text(table._h, ctypes.c_void_p(tpin.data_ptr()), tb + 64))
+        t3 = time.perf_counter()
+        if ph is not None:
+            ph.append(((t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3))
 
     step()
-    times = []
+    times, ph = [], []
     for _ in range(steps):
         t = time.perf_counter()
-        step()
+        step(ph)
         times.append((time.perf_counter() - t) * 1e3)
     ok = nb.value == tb and bytes(tpin.numpy()[:tb]) == truth
     med = sorted(times)[len(times) // 2]
+    # the PCIe floor of the same bytes: the pinned records alone up, the text alone down
+    dev = torch.empty(host.nbytes, dtype=torch.uint8, device="cuda")
+    dtext = torch.empty(tb, dtype=torch.uint8, device="cuda")
+    h2d, d2h = [], []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        dev.copy_(pin, non_blocking=True)
+        torch.cuda.synchronize()
+        h2d.append((time.perf_counter() - t) * 1e3)
+        t = time.perf_counter()
+        tpin[:tb].copy_(dtext, non_blocking=True)
+        torch.cuda.synchronize()
+        d2h.append((time.perf_counter() - t) * 1e3)
+    del dev, dtext
+    hot = table.stats()["n_hot_regions"]
+    h2d_ms, d2h_ms = min(h2d), min(d2h)
     return {"value": (n + nl) / (med / 1e3), "unit": "ops/s", "ms_per_step_median": med, "step_ms": times,
-            "h2d_bytes": int(host.nbytes), "d2h_bytes": tb, "verified_vs_truth": ok,
+            "phases_ms_median": {k: sorted(p[i] for p in ph)[len(ph) // 2]
+                                 for i, k in enumerate(("kh_insert", "kh_assemble", "kh_contigs_text"))},
+            "pcie_floor_ms": {"h2d_records": h2d_ms, "d2h_text": d2h_ms, "sum": h2d_ms + d2h_ms,
+                              "h2d_GBs": host.nbytes / h2d_ms / 1e6, "d2h_GBs": tb / d2h_ms / 1e6},
+            "h2d_bytes": int(host.nbytes), "d2h_bytes": tb, "verified_vs_truth": ok, "hot_regions": hot,
             "note": "reference boundary (kmer_hash.cpp:129-137): kh_insert from pinned host records "
                     "(H2D + insert), kh_assemble, kh_contigs_text D2H into pinned host memory"}
 

@@ -1397,7 +1397,7 @@ static uint32_t balanced_T(const KParams& p, uint64_t cap, uint64_t n) {
 // regions and for windows that were full.
 // counts: exact region counts (sample_shift 0) or a 1-in-2^sample_shift sample of the batch
 // (k_part1_convert / k_sample_regions); a sampled region counts as hot only above twice the
-// threshold (the exact mark after pass 2 catches what the sample misses). CT_HOT is the bitmap's
+// threshold and with >= 16 samples (the exact mark after pass 2 catches what the sample misses). CT_HOT is the bitmap's
 // population; list_new lists the regions this mark added (CT_HOTNEW) for k_hot_gather.
 template <int Unused = 0>
 __global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint32_t RC, int slack16, int sample_shift,
@@ -1411,7 +1411,10 @@ __global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint3
         const uint32_t S = Tfix ? Tfix : (uint32_t)(region_lo(r + 1, cap, p) - region_lo(r, cap, p));
         const uint64_t T = min(RC, S - (slack16 ? S / 16u : 0u));
         const bool old = (hot[r >> 5] >> (r & 31u)) & 1u;
-        const bool over = sample_shift ? ((uint64_t)counts[r] << sample_shift) > 2 * T : counts[r] > T;
+        // sampled: also at least 16 samples, so a small sample (the first of 16 upload chunks: 0.4
+        // samples per region on average) cannot mark a region on Poisson noise alone
+        const bool over = sample_shift ? counts[r] >= 16u && ((uint64_t)counts[r] << sample_shift) > 2 * T
+                                       : counts[r] > T;
         hn = allow_new && !old && over;
         h = old || hn;
     }

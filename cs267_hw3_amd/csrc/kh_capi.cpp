@@ -513,7 +513,8 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
 static int insert_chunked_upload(kh_table* t, const uint8_t* host_recs, uint64_t n) {
     const uint64_t R = (uint64_t)t->kp.R, W = (uint64_t)t->kp.W;
     // chunks of a multiple of 8192 records (the convert pass's tiles; start-mask words stay whole)
-    uint64_t nch = 8;
+    const char* ce = getenv("KH_UPLOAD_CHUNKS");
+    uint64_t nch = ce && atoi(ce) > 0 ? (uint64_t)atoi(ce) : 16;
     uint64_t chunk = ((n + nch - 1) / nch + 8191) & ~8191ull;
     nch = (n + chunk - 1) / chunk;
     int rc;
