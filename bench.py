@@ -48,6 +48,7 @@ WORKLOADS = {
                 desc="C5 hot-bucket: k=51, 200M synthetic k-mers per GPU, contigs U[8,200], 30% of "
                      "them built around one of 8 shared minimizer motifs"),
 }
+RANDOM_REQ_CEILING = 49e9
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 BEST_PUBLISHED_OPS = 72.6e6    # k=51, 4 nodes x 128 ranks (512 CPU ranks)
 
@@ -297,9 +298,17 @@ def main():
     kw = kernel_roof("k_walk_q (contig walk, chain hops)", nl, walkk_ms, "k_walk", "lookups")
     rq = ((traffic or {}).get("requests") or {}).get("TCC_EA0_RDREQ_sum", {}).get("k_walk")
     kw["requests_per_lookup"] = rq / nl if rq else None  # 64-B HBM read requests (PMC) per lookup
+    # the walk in what it moves: PMC bytes (traffic_GBs above) and random 64-B requests per second
+    # against the measured random-request ceiling (tools/membench.hip: ~49 G random 16-B loads/s
+    # = 64-B requests/s at a 6.4 GB table, profiles/r01/membench.jsonl)
+    kw["requests_per_s"] = rq / (walkk_ms / 1e3) if rq else None
+    kw["request_ceiling_per_s"] = RANDOM_REQ_CEILING
+    kw["request_frac"] = kw["requests_per_s"] / RANDOM_REQ_CEILING if rq else None
     roof = dict(kb if build_ms >= walkk_ms else kw)
     roof["kernels"] = {"k_part_build_pf": kb, "k_walk_q": kw}
-    insert_pipe = {"kernels": "k_part1_convert (records -> words + minimizer), k_win1, k_win2, k_part_build_pf, "
+    insert_pipe = {"kernels": "k_win1_rec (records -> parse + minimizer + bucket sort), k_win2, k_part_build_pf, "
+                              "k_insert_overflow" if k in (51, 19) else
+                              "k_part1_convert (records -> words + minimizer), k_win1, k_win2, k_part_build_pf, "
                               "k_insert_overflow",
                    "ms": ins_ms, "achieved_alg_GBs": n * b_alg / (ins_ms / 1e3) / 1e9,
                    "inserts_per_s": n / (ins_ms / 1e3),

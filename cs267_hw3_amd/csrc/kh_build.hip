@@ -1108,12 +1108,13 @@ __device__ __forceinline__ void load_record16(const uint8_t* __restrict__ recs, 
     }
 }
 
-template <int W, int TB, int TILE, int PK>
-__global__ __launch_bounds__(TB) void k_win1_rec(KParams p, const uint8_t* __restrict__ recs, uint64_t n,
+template <int W, int TB, int TILE, int PK, int KT>
+__global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __restrict__ recs, uint64_t n,
                                                  uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1,
                                                  uint64_t* start_mask, uint64_t* split_mask, uint64_t* ovf,
                                                  uint64_t ovf_cap, unsigned long long* ctr,
                                                  unsigned long long* stats) {
+    const KParams p = specialize<KT>(p_in);
     constexpr int IPT = TILE / TB;
     const bool hot_on = p.hot && ctr[CT_HOT];
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -1282,15 +1283,18 @@ static hipError_t win1_rec_launch(const KParams& p, const uint8_t* recs, uint64_
                                   uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats,
                                   hipStream_t s) {
     constexpr int PK = W == 2 ? 13 : 5;
-    hipError_t e;
-    if ((e = allow_lds(k_win1_rec<W, 512, WIN_TILE, PK>, WIN_LDS)) != hipSuccess) return e;
     uint64_t grid = ((uint64_t)cu_count() + S1 - 1) / S1 * S1;
     const uint64_t ntiles = (n + WIN_TILE - 1) / WIN_TILE;
     if (grid > ntiles) grid = (ntiles + S1 - 1) / S1 * S1;
     if (grid == 0) grid = S1;
-    k_win1_rec<W, 512, WIN_TILE, PK><<<(unsigned)grid, 512, WIN_LDS, s>>>(
-        p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask, B.overflow, ovf_cap, ctr, stats);
-    return hipSuccess;
+    return with_kt<W>(p.K, [&](auto kt) {
+        constexpr int KT = decltype(kt)::value;
+        hipError_t e;
+        if ((e = allow_lds(k_win1_rec<W, 512, WIN_TILE, PK, KT>, WIN_LDS)) != hipSuccess) return e;
+        k_win1_rec<W, 512, WIN_TILE, PK, KT><<<(unsigned)grid, 512, WIN_LDS, s>>>(
+            p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask, B.overflow, ovf_cap, ctr, stats);
+        return hipSuccess;
+    });
 }
 
 // pass 2: bucket -> region windows (RC words each)
@@ -1435,6 +1439,22 @@ __global__ __launch_bounds__(256) void k_sample_regions(KParams p, const uint64_
     for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) << 8; i < m; i += ((uint64_t)gridDim.x * 256) << 8) {
         const uint64_t w0 = words[i * W], w1 = W == 2 ? words[i * W + 1] : 0ull;
         (void)wave_count_add(counts, mini_region(word_mini_window(w0, w1, p), p), true);
+    }
+}
+
+// The same sample read straight from the reference records (the records pass 1, k_win1_rec, has
+// no earlier pass to count in): record 256 i, one aligned 16-B pair of loads each.
+template <int W, int KT>
+__global__ __launch_bounds__(256) void k_sample_records(KParams p_in, const uint8_t* __restrict__ recs, uint64_t n,
+                                                        uint32_t* counts) {
+    const KParams p = specialize<KT>(p_in);
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) << 8; i < n; i += ((uint64_t)gridDim.x * 256) << 8) {
+        uint64_t x0, x1;
+        load_record_regs(recs, i, (uint32_t)p.R, x0, x1);
+        Key k;
+        uint32_t ext;
+        parse_record_regs(x0, x1, p, k, ext);
+        (void)wave_count_add(counts, mini_region(mini_window(k, mini_scan(k, p), p), p), true);
     }
 }
 
@@ -1609,6 +1629,16 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
 }
 
 // Hot regions from a 1-in-256 sample of the batch (in B.rcnt, left zeroed for pass 2).
+template <int W>
+static hipError_t sample_records(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t* counts, hipStream_t s) {
+    const uint64_t ns = (n + 255) >> 8;
+    const unsigned nb = (unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024);
+    return with_kt<W>(p.K, [&](auto kt) {
+        k_sample_records<W, decltype(kt)::value><<<nb, 256, 0, s>>>(p, recs, n, counts);
+        return hipGetLastError();
+    });
+}
+
 static hipError_t sample_mark(const KParams& p, uint64_t cap, uint64_t n, uint32_t RC, const PartBuffers& B,
                               unsigned long long* ctr, hipStream_t s) {
     hipError_t e;
@@ -1618,6 +1648,11 @@ static hipError_t sample_mark(const KParams& p, uint64_t cap, uint64_t n, uint32
     k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot, B.hot_list, ctr, 1, 0,
                                                      balanced_T(p, cap, n));
     return hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s);
+}
+
+template <int W>
+static bool rec_pass_ok(const KParams& p) {
+    return ((p.P == 13 && W == 2) || (p.P == 5 && W == 1)) && !debug_flag("p1conv");
 }
 
 // One batch: pass 1 (records or words), pass 2, build, overflow inserts.
@@ -1635,11 +1670,17 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
-    const bool rec_pass = REC && ((p.P == 13 && W == 2) || (p.P == 5 && W == 1)) && debug_flag("p1rec");
+    // records of a compiled shape (k=51 / k=19 packed sizes): pass 1 reads them itself, no
+    // record -> word copy (KH_DEBUG=p1conv: the convert pass + pass 1 on its words)
+    const bool rec_pass = REC && rec_pass_ok<W>(p);
     // empty table: a 1-in-256 sample of the batch's minimizer regions marks the hot ones before
     // pass 1, so their keys are sorted straight into their key-hash regions (no spill storm)
-    const bool sample = table_empty && !rec_pass && !debug_flag("no_hot_sample");
+    const bool sample = table_empty && !debug_flag("no_hot_sample");
     uint32_t* samp = (REC && sample) ? rcnt : nullptr;
+    if (rec_pass && sample) {
+        if ((e = sample_records<W>(p, recs, n, rcnt, s)) != hipSuccess) return e;
+        if ((e = sample_mark(p, t.cap, n, RC, B, ctr, s)) != hipSuccess) return e;
+    }
     if (!REC && sample) {
         const uint64_t ns = (n + 255) >> 8;
         k_sample_regions<W><<<(unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024), 256, 0, s>>>(p, words, n,
@@ -1731,6 +1772,20 @@ static hipError_t part_stage_recs(const KParams& p, const uint8_t* recs, uint64_
     if (m == 0) return hipSuccess;
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(p, total);
     const bool samp_on = sample && !debug_flag("no_hot_sample");
+    if (rec_pass_ok<W>(p)) {
+        if (samp_on) {
+            if ((e = sample_records<W>(p, recs, m, B.rcnt, s)) != hipSuccess) return e;
+            if ((e = sample_mark(p, cap, m, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess) return e;
+        }
+        if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
+        if ((e = win1_rec_launch<W>(p, recs, m, CAP1, B.wcnt, B, start_mask, split_mask, part_overflow_cap(total), ctr,
+                                    stats, s)) != hipSuccess)
+            return e;
+        if ((e = win2_launch<W>(p, B, m, RC, B.rcnt, part_overflow_cap(total), ctr, stats, CAP1, B.wcnt, s)) !=
+            hipSuccess)
+            return e;
+        return hipGetLastError();
+    }
     uint32_t* samp = samp_on ? B.rcnt : nullptr;
     const unsigned nb = (unsigned)((m + (uint64_t)T1 * PART_TILE - 1) / ((uint64_t)T1 * PART_TILE));
     if (W == 2 && p.K == 51)
