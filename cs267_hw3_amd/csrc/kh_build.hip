@@ -55,6 +55,8 @@ static constexpr uint64_t LDS_BYTES = 160 * 1024;
 static constexpr int WIN_TILE = 8192;
 constexpr size_t sort_lds(int tile) { return (size_t)tile * 16 + tile * 2 + 2 * NB1 * 4 + NB1 * 8; }
 static_assert(sort_lds(WIN_TILE) + 64 <= 160 * 1024, "k_win LDS");
+static constexpr int REC_TILE = 3584;  // records pass 1 (k_win1_rec): two blocks per CU
+static_assert(2 * (sort_lds(REC_TILE) + 64) <= 160 * 1024, "k_win1_rec LDS");
 static uint64_t win_blocks1(uint64_t n) { return (n + (uint64_t)T1 * WIN_TILE - 1) / ((uint64_t)T1 * WIN_TILE); }
 // pass-2 blocks per bucket
 static uint64_t win_G(uint64_t n) {
@@ -1283,18 +1285,32 @@ static hipError_t win1_rec_launch(const KParams& p, const uint8_t* recs, uint64_
                                   uint64_t ovf_cap, unsigned long long* ctr, unsigned long long* stats,
                                   hipStream_t s) {
     constexpr int PK = W == 2 ? 13 : 5;
-    uint64_t grid = ((uint64_t)cu_count() + S1 - 1) / S1 * S1;
-    const uint64_t ntiles = (n + WIN_TILE - 1) / WIN_TILE;
-    if (grid > ntiles) grid = (ntiles + S1 - 1) / S1 * S1;
-    if (grid == 0) grid = S1;
-    return with_kt<W>(p.K, [&](auto kt) {
-        constexpr int KT = decltype(kt)::value;
-        hipError_t e;
-        if ((e = allow_lds(k_win1_rec<W, 512, WIN_TILE, PK, KT>, WIN_LDS)) != hipSuccess) return e;
-        k_win1_rec<W, 512, WIN_TILE, PK, KT><<<(unsigned)grid, 512, WIN_LDS, s>>>(
-            p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask, B.overflow, ovf_cap, ctr, stats);
-        return hipSuccess;
-    });
+    // tiles of REC_TILE records: two blocks per CU (4 waves per SIMD) for the VALU-heavy parse and
+    // minimizer scan (C3: 2.49 ms at 8192-record tiles and one block per CU, 2.30 at 3584; the
+    // words pass 2 keeps 8192: 1.60 vs 1.87 ms at 3584). KH_REC_TILE=8192 for A/B runs.
+    static const bool big = [] {
+        const char* e = getenv("KH_REC_TILE");
+        return e && atoi(e) == WIN_TILE;
+    }();
+    auto go = [&](auto tile_c) -> hipError_t {
+        constexpr int TILE = decltype(tile_c)::value;
+        constexpr size_t lds = sort_lds(TILE);
+        const uint64_t bpc = LDS_BYTES / (lds + 64);  // resident blocks per CU
+        uint64_t grid = ((uint64_t)cu_count() * bpc + S1 - 1) / S1 * S1;
+        const uint64_t ntiles = (n + TILE - 1) / TILE;
+        if (grid > ntiles) grid = (ntiles + S1 - 1) / S1 * S1;
+        if (grid == 0) grid = S1;
+        return with_kt<W>(p.K, [&](auto kt) {
+            constexpr int KT = decltype(kt)::value;
+            hipError_t e;
+            if ((e = allow_lds(k_win1_rec<W, 512, TILE, PK, KT>, lds)) != hipSuccess) return e;
+            k_win1_rec<W, 512, TILE, PK, KT><<<(unsigned)grid, 512, lds, s>>>(
+                p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask, B.overflow, ovf_cap, ctr, stats);
+            return hipSuccess;
+        });
+    };
+    if (big) return go(std::integral_constant<int, WIN_TILE>{});
+    return go(std::integral_constant<int, REC_TILE>{});
 }
 
 // pass 2: bucket -> region windows (RC words each)

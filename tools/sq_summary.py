@@ -12,7 +12,7 @@ import json
 import sys
 
 d = sys.argv[1]
-pats = sys.argv[2:] or ["k_part_build_pf", "k_part1_convert", "k_win1", "k_win2", "k_walk_q"]
+pats = sys.argv[2:] or ["k_part_build_pf", "k_part1_convert", "k_win1_rec", "k_win1<", "k_win2", "k_walk_q"]
 files = glob.glob(f"{d}/**/*_counter_collection.csv", recursive=True)
 acc = {}
 for r in csv.DictReader(open(files[0])):
