@@ -77,6 +77,7 @@ _SIGS = {
     "kh_collect_starts_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_route_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.c_int, c_vp, c_vp]),
     "kh_route_starts_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.c_int, c_vp, c_vp]),
+    "kh_route_starts_win_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.c_int, c_vp, c_u64, c_vp]),
     "kh_insert_words_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_insert_words_stage_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_u64]),
     "kh_insert_words_finish": (ctypes.c_int, [c_vp]),

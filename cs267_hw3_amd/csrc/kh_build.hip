@@ -54,6 +54,7 @@ static constexpr uint64_t LDS_BYTES = 160 * 1024;
 // bin gets per tile (C3 pass 1: 16 words = 256 B instead of 128 B) in 152 KiB of LDS
 static constexpr int WIN_TILE = 8192;
 constexpr size_t sort_lds(int tile) { return (size_t)tile * 16 + tile * 2 + 2 * NB1 * 4 + NB1 * 8; }
+constexpr size_t sort_lds_nb(int tile, int nb) { return (size_t)tile * 16 + tile * 2 + 2 * nb * 4 + nb * 8; }
 static_assert(sort_lds(WIN_TILE) + 64 <= 160 * 1024, "k_win LDS");
 static constexpr int REC_TILE = 3584;  // records pass 1 (k_win1_rec): two blocks per CU
 static_assert(2 * (sort_lds(REC_TILE) + 64) <= 160 * 1024, "k_win1_rec LDS");
@@ -1110,23 +1111,27 @@ __device__ __forceinline__ void load_record16(const uint8_t* __restrict__ recs, 
     }
 }
 
-template <int W, int TB, int TILE, int PK, int KT>
+// ROUTE: the sharded path's one-pass route instead (kh_route_starts_win_dev): bins are the owner
+// ranks (P <= MAX_RANKS), owner q's run of each tile goes to its window buf1 + q * CAP1 words
+// (CAP1 = the caller's window size, >= the records routed), wcnt[q] counts them.
+template <int W, int TB, int TILE, int PK, int KT, bool ROUTE = false>
 __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __restrict__ recs, uint64_t n,
                                                  uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1,
                                                  uint64_t* start_mask, uint64_t* split_mask, uint64_t* ovf,
                                                  uint64_t ovf_cap, unsigned long long* ctr,
-                                                 unsigned long long* stats) {
+                                                 unsigned long long* stats, uint32_t P = 1) {
     const KParams p = specialize<KT>(p_in);
+    constexpr int NB = ROUTE ? MAX_RANKS : NB1;
     constexpr int IPT = TILE / TB;
-    const bool hot_on = p.hot && ctr[CT_HOT];
+    const bool hot_on = !ROUTE && p.hot && ctr[CT_HOT];
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* items = smem;
     uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + TILE * 2);
     uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + TILE);
-    uint32_t* start = hist + NB1;
-    uint32_t* gpos = start + NB1;
+    uint32_t* start = hist + NB;
+    uint32_t* gpos = start + NB;
     __shared__ uint32_t wsum[TB / 64];
-    const uint32_t sub = blockIdx.x % S1;
+    const uint32_t sub = ROUTE ? 0u : blockIdx.x % S1;
     // persistent blocks: tile t, t + gridDim.x, ...; the next tile's loads are always in flight
     const uint64_t ntiles = (n + TILE - 1) / TILE;
     // a wave's 64 records are one contiguous run of 64 * R bytes: lane l loads the run's l-th
@@ -1189,14 +1194,18 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
             }
             a[j] = valid ? part_word0(slot_w0(k, ext, p), mn, p) : EMPTY;
             b[j] = (valid && W == 2) ? k.lo : 0;
-            bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on) >> (p.rbits - B1);
+            if (ROUTE)
+                bin[j] = P == 1 ? 0u
+                                : (p.owner_mode == 1 ? owner_key(k, p, P) : owner_of_mini(mini_window(k, mn, p), P));
+            else
+                bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on) >> (p.rbits - B1);
         }
         const uint64_t nt = t + gridDim.x, nbase = nt * TILE;
-        sort_reserve_write<W, TB, NB1, TILE>(
+        sort_reserve_write<W, TB, NB, TILE>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
-            [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
-            [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
-            [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
+            [&](uint32_t q) { return &wcnt[q * (ROUTE ? 1u : S1) + sub]; },
+            [&](uint32_t q) { return (uint64_t)(q * (ROUTE ? 1u : S1) + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr,
+            stats, [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
     }
 }
 
@@ -1311,6 +1320,49 @@ static hipError_t win1_rec_launch(const KParams& p, const uint8_t* recs, uint64_
     };
     if (big) return go(std::integral_constant<int, WIN_TILE>{});
     return go(std::integral_constant<int, REC_TILE>{});
+}
+
+// One-pass route (sharded insert): records -> owner windows, start bits in the same pass.
+template <int U = 0>
+__global__ void k_route_win_counts(const uint32_t* cnt, uint32_t P, uint64_t n, uint64_t* counts) {
+    const uint32_t q = threadIdx.x;
+    if (q < P) counts[q] = cnt[q];
+    if (q == 0) counts[P] = n;
+}
+
+template <int W>
+static hipError_t route_win_launch(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
+                                   uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
+                                   unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+    constexpr int PK = W == 2 ? 13 : 5;
+    constexpr size_t lds = sort_lds_nb(REC_TILE, MAX_RANKS);
+    hipError_t e;
+    if ((e = hipMemsetAsync(cnt, 0, (size_t)MAX_RANKS * 4, s)) != hipSuccess) return e;
+    if (n) {
+        const uint64_t bpc = LDS_BYTES / (lds + 64);
+        uint64_t grid = (uint64_t)cu_count() * bpc;
+        const uint64_t ntiles = (n + REC_TILE - 1) / REC_TILE;
+        if (grid > ntiles) grid = ntiles;
+        e = with_kt<W>(p.K, [&](auto kt) {
+            constexpr int KT = decltype(kt)::value;
+            hipError_t x;
+            if ((x = allow_lds(k_win1_rec<W, 512, REC_TILE, PK, KT, true>, lds)) != hipSuccess) return x;
+            k_win1_rec<W, 512, REC_TILE, PK, KT, true><<<(unsigned)grid, 512, lds, s>>>(
+                p, recs, n, (uint32_t)win, cnt, words, start_mask, nullptr, nullptr, 0, ctr, stats, P);
+            return hipGetLastError();
+        });
+        if (e != hipSuccess) return e;
+    }
+    k_route_win_counts<<<1, MAX_RANKS, 0, s>>>(cnt, P, n, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_win(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
+                            uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
+                            unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+    if (win < n || win >= (1ull << 32)) return hipErrorInvalidValue;
+    return p.W == 1 ? route_win_launch<1>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s)
+                    : route_win_launch<2>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s);
 }
 
 // pass 2: bucket -> region windows (RC words each)

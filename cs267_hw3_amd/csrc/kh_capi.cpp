@@ -1035,6 +1035,36 @@ int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nrank
     return KH_OK;
 }
 
+int kh_route_starts_win_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* words_out,
+                            uint64_t win, void* counts_out) {
+    if (!t) return fail(KH_ERR_ARG, "null table");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
+    if (!counts_out || (n && (!dev_recs || !words_out))) return fail(KH_ERR_ARG, "null buffer");
+    if (!aligned16(dev_recs) || !aligned16(words_out)) return fail(KH_ERR_ARG, "device buffers must be 16-byte aligned");
+    if (win < n || win >= (1ull << 32))
+        return fail(KH_ERR_ARG, "window of %llu words for %llu records (need n <= win < 2^32)", (unsigned long long)win,
+                    (unsigned long long)n);
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, n, nranks)) return rc;
+    const uint64_t nw = (n + 63) / 64;
+    int rc;
+    if ((rc = t->mask.ensure(nw * 8 + 8))) return rc;
+    if ((rc = t->mask_off.ensure(nw * 8 + 8))) return rc;
+    if ((rc = t->scratch.ensure(kh::scan_scratch_words(nw) * 8 + 64))) return rc;
+    if ((rc = t->route_own.ensure(kh::MAX_RANKS * 4 + 64))) return rc;
+    if ((rc = ensure_starts(t, t->collected_n + n))) return rc;
+    KH_HIP(kh::launch_route_win(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks, (uint64_t*)words_out, win,
+                                t->route_own.as<uint32_t>(), (uint64_t*)counts_out, n ? t->mask.as<uint64_t>() : nullptr,
+                                t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(), t->stream));
+    if (n)
+        KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
+                                         t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
+                                         t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(), t->stream));
+    t->collected_n += n;
+    t->assembled = false;
+    return KH_OK;
+}
+
 int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (m == 0) return KH_OK;

@@ -319,6 +319,11 @@ hipError_t launch_part_stage_recs(const KParams& p, const uint8_t* recs, uint64_
                                   const PartBuffers& b, uint64_t* words_tmp, uint64_t* start_mask,
                                   uint64_t* split_mask, unsigned long long* ctr, unsigned long long* stats,
                                   hipStream_t s, bool sample, uint64_t cap);
+// One-pass route of the sharded insert: owner q's words at words + q * win * W (win >= n, < 2^32),
+// counts[q] = their number, counts[P] = n; start bits into start_mask (kh_build.hip).
+hipError_t launch_route_win(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
+                            uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
+                            unsigned long long* ctr, unsigned long long* stats, hipStream_t s);
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
                               const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
                               hipStream_t s);

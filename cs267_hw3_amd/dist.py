@@ -57,6 +57,17 @@ class TorchComm:
             raise NotImplementedError
         self.dist.all_to_all(outs, inps, group=self.group)
 
+    def all_to_all_views_async(self, outs, inps):
+        """Per-peer input views (not back to back: the one-pass route's owner windows) into
+        per-peer output views. RCCL: grouped send/recv straight from the views; other backends:
+        packed through one all_to_all_single, unpacked at wait()."""
+        if self.backend == "nccl":
+            return self.dist.all_to_all(outs, inps, group=self.group, async_op=True)
+        send, recv = _pack_views(inps, outs)
+        w = self.dist.all_to_all_single(recv, send, [o.numel() for o in outs], [i.numel() for i in inps],
+                                        group=self.group, async_op=True)
+        return _UnpackOnWait(w, recv, outs)
+
     def barrier(self):
         self.dist.barrier(group=self.group)
 
@@ -66,6 +77,27 @@ class TorchComm:
             t = t.cuda()
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
+
+
+def _pack_views(inps, outs):
+    like = inps[0] if inps else outs[0]
+    send = torch.cat(list(inps)) if len(inps) > 1 else inps[0].contiguous()
+    recv = torch.empty(sum(o.numel() for o in outs), dtype=like.dtype, device=like.device)
+    return send, recv
+
+
+class _UnpackOnWait:
+    def __init__(self, work, recv, outs):
+        self.work, self.recv, self.outs = work, recv, outs
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+        pos = 0
+        for o in self.outs:
+            if o.numel():
+                o.copy_(self.recv[pos:pos + o.numel()])
+            pos += o.numel()
 
 
 class ThreadComm:
@@ -98,6 +130,12 @@ class ThreadComm:
     def _sync(self, t):
         if t.is_cuda:
             torch.cuda.current_stream(t.device).synchronize()
+
+    def all_to_all_views_async(self, outs, inps):
+        send, recv = _pack_views(inps, outs)
+        self.all_to_all(recv, send, [o.numel() for o in outs], [i.numel() for i in inps])
+        _UnpackOnWait(None, recv, outs).wait()
+        return ThreadComm._Done()
 
     def all_to_all(self, out, inp, out_splits, in_splits):
         self._sync(inp)
@@ -168,6 +206,16 @@ class GpuShard:
         f = self.L.kh_route_starts_dev if starts else self.L.kh_route_dev
         check(f(self.h, self._p(recs), n, nranks, self._p(words), self._p(counts)))
         return words, counts
+
+    route_windows = True  # route_win: one pass over the records into per-owner windows
+
+    def route_win(self, recs, nranks, words, win):
+        """Records -> owner q's words at words[q * win * W ...] (one pass, kh_route_starts_win_dev;
+        win >= the records routed) + this block's start k-mers; returns the [P+1] counts."""
+        counts = self.zeros(nranks + 1, torch.int64)
+        check(self.L.kh_route_starts_win_dev(self.h, self._p(recs), recs.shape[0], nranks, self._p(words), int(win),
+                                             self._p(counts)))
+        return counts
 
     def reserve(self, m):
         """Room for m more k-mers: an empty shard grows to them (kh_reserve); a non-empty one must
@@ -301,8 +349,11 @@ class DistributedKmerHashMap:
         mx = counts[:P].max().reshape(1)
         send = torch.stack([counts[:P], counts[P:P + 1].expand(P), mx.expand(P)], 1)
         send = send.contiguous().view(-1)
-        recv = torch.empty_like(send)
-        self.comm.all_to_all(recv, send, [3] * P, [3] * P)
+        if P == 1 and not self.SELF_EXCHANGE:
+            recv = send  # one rank: the exchange is the identity (no collective launch)
+        else:
+            recv = torch.empty_like(send)
+            self.comm.all_to_all(recv, send, [3] * P, [3] * P)
         host = torch.cat([send, recv]).cpu().view(2, P, 3)
         send_splits = host[0, :, 0].tolist()
         recv_splits = host[1, :, 0].tolist()
@@ -310,20 +361,27 @@ class DistributedKmerHashMap:
         gmax = int(host[1, :, 2].max())
         return send_splits, recv_splits, totals, gmax
 
-    def _all_to_all(self, out, inp, out_splits, in_splits, gmax_elems):
+    def _all_to_all(self, out, inp, out_splits, in_splits, gmax_elems, in_off=None):
         """all_to_all_single in chunks of at most A2A_CHUNK_BYTES per peer. gmax_elems is the
-        largest per-peer split over ALL ranks, so every rank runs the same number of calls."""
+        largest per-peer split over ALL ranks, so every rank runs the same number of calls.
+        in_off: where each peer's input starts (the route's owner windows; default back to back)."""
         limit = max(1, self.A2A_CHUNK_BYTES // inp.element_size())
         rounds = (gmax_elems + limit - 1) // limit
-        if rounds <= 1:
+        P = self.P
+        if rounds <= 1 and in_off is None:
             self.comm.all_to_all(out, inp, out_splits, in_splits)
             return
-        P = self.P
-        in_off = [0] * P
         out_off = [0] * P
         for q in range(1, P):
-            in_off[q] = in_off[q - 1] + in_splits[q - 1]
             out_off[q] = out_off[q - 1] + out_splits[q - 1]
+        if in_off is None:
+            in_off = [0] * P
+            for q in range(1, P):
+                in_off[q] = in_off[q - 1] + in_splits[q - 1]
+        if rounds <= 1:
+            self.comm.all_to_all_views_async([out[out_off[q]:out_off[q] + out_splits[q]] for q in range(P)],
+                                             [inp[in_off[q]:in_off[q] + in_splits[q]] for q in range(P)]).wait()
+            return
         if getattr(self.comm, "backend", None) == "nccl":
             # views straight into the packed buffers: no staging copies
             for r in range(rounds):
@@ -351,6 +409,7 @@ class DistributedKmerHashMap:
     # pipelined insert: chunk c-1, received, is partitioned while chunk c is on the wire
     # (KH_INSERT_CHUNKS=1: one transfer)
     INSERT_CHUNKS = int(os.environ.get("KH_INSERT_CHUNKS", "4"))
+    ROUTE_WINDOW_BYTES = int(os.environ.get("KH_ROUTE_WINDOW_GB", "64")) << 30
     PIPELINE_MIN = 1 << 22  # records per rank below which the insert is one chunk
 
     def _exchange_count_matrix(self, counts):
@@ -361,8 +420,11 @@ class DistributedKmerHashMap:
         mat = torch.stack([c[:P] for c in counts])            # [nch, P]
         mx = mat.max().reshape(1)
         send = torch.cat([mat.t(), mx.expand(P).reshape(P, 1)], 1).contiguous().view(-1)  # [P, nch+1]
-        recv = torch.empty_like(send)
-        self.comm.all_to_all(recv, send, [nch + 1] * P, [nch + 1] * P)
+        if P == 1 and not self.SELF_EXCHANGE:
+            recv = send
+        else:
+            recv = torch.empty_like(send)
+            self.comm.all_to_all(recv, send, [nch + 1] * P, [nch + 1] * P)
         host = torch.cat([send, recv]).cpu().view(2, P, nch + 1)
         send_c = [[int(host[0, q, c]) for q in range(P)] for c in range(nch)]
         recv_c = [[int(host[1, q, c]) for q in range(P)] for c in range(nch)]
@@ -393,11 +455,29 @@ class DistributedKmerHashMap:
             nch = max(self.INSERT_CHUNKS, -(-n * W * 8 // self.A2A_CHUNK_BYTES))
         # chunk starts at multiples of 16 records: every chunk's records stay 16-B aligned
         bounds = [min(n, (n * c // nch) & ~15) for c in range(nch)] + [n]
-        words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
+        # one-pass route into per-owner windows (each sized for the whole chunk, so any skew fits)
+        # while P windows of the block fit the budget; the two-pass route packs back to back
+        windows = getattr(sh, "route_windows", False) and P * n * W * 8 <= self.ROUTE_WINDOW_BYTES
+        if windows:
+            # one-pass route: chunk c's owner windows of (c1 - c0) words each at P * c0 words
+            words = self._grow("_ins_words", max(P * n, 1) * W, torch.int64, recs.device)
+        else:
+            words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
         counts = []
         for c in range(nch):
             c0, c1 = bounds[c], bounds[c + 1]
-            counts.append(sh.route(recs[c0:c1], P, words[c0 * W:max(c1, c0 + 1) * W], starts=True)[1])
+            if windows:
+                counts.append(sh.route_win(recs[c0:c1], P, words[P * c0 * W:], max(c1 - c0, 1)))
+            else:
+                counts.append(sh.route(recs[c0:c1], P, words[c0 * W:max(c1, c0 + 1) * W], starts=True)[1])
+
+        def views(c, send):  # chunk c's per-peer input (window starts, or back to back)
+            c0, c1 = bounds[c], bounds[c + 1]
+            if windows:
+                offs = [(P * c0 + q * max(c1 - c0, 1)) * W for q in range(P)]
+            else:
+                offs = [c0 * W + sum(send[:q]) * W for q in range(P)]
+            return [words[offs[q]:offs[q] + send[q] * W] for q in range(P)], offs
         send_c, recv_c, gmax = self._exchange_count_matrix(counts)
         m = sum(sum(r) for r in recv_c)
         err = None
@@ -411,16 +491,18 @@ class DistributedKmerHashMap:
             return m
         recv = self._grow("_ins_recv", max(m, 1) * W, torch.int64, recs.device)
         if nch == 1:
-            self._all_to_all(recv[:m * W], words[:n * W], [x * W for x in recv_c[0]],
-                             [x * W for x in send_c[0]], gmax * W)
+            self._all_to_all(recv[:m * W], words, [x * W for x in recv_c[0]],
+                             [x * W for x in send_c[0]], gmax * W, in_off=views(0, send_c[0])[1])
             sh.insert_words(recv, m)
             return m
         works, spans, pos = [], [], 0
         for c in range(nch):
-            c0, c1 = bounds[c], bounds[c + 1]
             mc = sum(recv_c[c])
-            works.append(self.comm.all_to_all_async(recv[pos * W:(pos + mc) * W], words[c0 * W:c1 * W],
-                                                    [x * W for x in recv_c[c]], [x * W for x in send_c[c]]))
+            outs, o = [], pos
+            for q in range(P):
+                outs.append(recv[o * W:(o + recv_c[c][q]) * W])
+                o += recv_c[c][q]
+            works.append(self.comm.all_to_all_views_async(outs, views(c, send_c[c])[0]))
             spans.append((pos, mc))
             pos += mc
             if c > 0:  # previous chunk received: partition it while this one is on the wire

@@ -136,6 +136,12 @@ int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void
  * come from the route's owner pass); successive calls append starts in call order. */
 int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
                         void* dev_counts_out);
+/* kh_route_starts_dev in ONE pass over the records (no owner pre-pass): owner q's words land in
+ * the window dev_words_out + q * win words-per-k-mer (win >= n, < 2^32: a window holds every record,
+ * whatever the skew), dev_counts_out[q] = their count, [nranks] = n. The all-to-all sends each
+ * window's first counts[q] words. Replaces the same hash_map.hpp:28-30,64-77 routing. */
+int kh_route_starts_win_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
+                            uint64_t win, void* dev_counts_out);
 /* dev_words: internal words as kh_route_dev / kh_route_starts_dev emit them (they carry the
  * k-mer's placement bits: minimizer window, order bits). */
 int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);

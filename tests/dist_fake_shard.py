@@ -67,6 +67,17 @@ class FakeShard:
             return words, counts
         return enc, counts
 
+    def route_win(self, recs, nranks, words, win):
+        """The one-pass route's layout (kh_route_starts_win_dev): owner q's words in the window at
+        words[q * win * W ...]; enabled per instance with route_windows = True."""
+        enc, counts = self.route(recs, nranks, starts=True)
+        pos = 0
+        for q in range(nranks):
+            c = int(counts[q])
+            words[q * win * self.W:(q * win + c) * self.W].copy_(enc[pos * self.W:(pos + c) * self.W])
+            pos += c
+        return counts
+
     def reserve(self, m):
         """kh_reserve: the shard grows to what it receives (fails like the GPU on NOMEM)."""
         if m > self.max_kmers:

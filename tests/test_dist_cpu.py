@@ -21,7 +21,8 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, insert_chunks=None, max_kmers=None):
+def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, insert_chunks=None, max_kmers=None,
+               windows=False):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -35,6 +36,7 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, insert_chunks=
     k = MANIFEST[name]["k"]
     recs = kh.read_kmers(os.path.join(GOLDEN, f"{name}.txt"), k, world, rank)
     shard = FakeShard(k) if max_kmers is None else FakeShard(k, max_kmers=max_kmers if rank == 0 else 1 << 24)
+    shard.route_windows = windows          # the one-pass route's owner-window layout
     dm = DistributedKmerHashMap(TorchComm(), shard)
     if insert_chunks:                      # pipelined insert: chunked route/exchange + staged build
         dm.INSERT_CHUNKS = insert_chunks
@@ -103,3 +105,19 @@ def test_sharded_shard_full_fails_on_every_rank(tmp_path):
     errs = [open(tmp_path / f"err_{r}").read() for r in range(world)]
     assert "cannot hold" in errs[0]
     assert "another rank" in errs[1]
+
+
+@pytest.mark.parametrize("name,world,chunk,chunks", [("small51", 2, None, None), ("mixed19", 3, 1000, None),
+                                                     ("small51", 3, None, 3), ("mixed19", 2, None, 4)])
+def test_sharded_route_windows_gloo(tmp_path, name, world, chunk, chunks):
+    """The one-pass route's layout (each owner's words in its own window, not back to back):
+    single and chunked all-to-all, and the pipelined insert, over gloo."""
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), chunk, chunks, None, True),
+                       nprocs=world, join=True, start_method="spawn")
+    import cs267_hw3_amd as kh
+    m = MANIFEST[name]
+    g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"],
+                          seed=m["seed"])
+    for r in range(world):
+        b, e = g.block(world, r)
+        assert open(tmp_path / f"test_{r}.dat", "rb").read() == g.truth(b, e)
