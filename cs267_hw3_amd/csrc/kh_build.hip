@@ -927,7 +927,8 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
 // Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
 // with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
 // out[window(bin) + reserved + rank] (positions past cap -> overflow list).
-template <int W, int TB, int NB, int TILE, class CtrF, class WinF, class NextF>
+// WRANK: ranks by wave_rank_all (few bins: the route's owners) instead of one LDS atomic per item
+template <int W, int TB, int NB, int TILE, bool WRANK = false, class CtrF, class WinF, class NextF>
 __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, const uint32_t* bin, uint64_t* items,
                                                    uint16_t* sbin, uint32_t* hist, uint32_t* start, uint32_t* gpos,
                                                    uint32_t* wsum, CtrF counter, WinF window, uint32_t cap,
@@ -941,7 +942,12 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
     lds_barrier();
     uint32_t rank[IPT];
 #pragma unroll
-    for (int j = 0; j < IPT; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
+    for (int j = 0; j < IPT; ++j) {
+        if (WRANK)
+            rank[j] = wave_rank_all(hist, bin[j], a[j] != EMPTY);
+        else
+            rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
+    }
     lds_barrier();
     const uint32_t hv = threadIdx.x < NB ? hist[threadIdx.x] : 0u;
     uint32_t total;
@@ -1137,7 +1143,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
     // a wave's 64 records are one contiguous run of 64 * R bytes: lane l loads the run's l-th
     // aligned 16-B block (coalesced, no straddling), and each lane later gathers the two blocks
     // holding its record by cross-lane shuffles
-    constexpr uint32_t R = PK + 2;
+    const uint32_t R = PK ? (uint32_t)(PK + 2) : (uint32_t)p.R;  // PK = 0: any record of <= 15 bytes
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nbytes = n * (uint64_t)R;
     uint64_t a[IPT], b[IPT];  // raw 16-B blocks until parsed, then the words
@@ -1179,7 +1185,12 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
                     w2 = q1;
                 }
                 const uint32_t sh = (o & 7u) * 8u;
-                if (valid) parse_record_regs_t<PK>(funnel64(w0, w1, sh), funnel64(w1, w2, sh), p.pad, k, ext);
+                if (valid) {
+                    if constexpr (PK != 0)
+                        parse_record_regs_t<PK>(funnel64(w0, w1, sh), funnel64(w1, w2, sh), p.pad, k, ext);
+                    else
+                        parse_record_regs(funnel64(w0, w1, sh), funnel64(w1, w2, sh), p, k, ext);
+                }
             }
             const uint32_t mn = mini_scan(k, p);
             if (s0 < n) {  // uniform: one start / splitter word per 64 consecutive records
@@ -1201,11 +1212,39 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
                 bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on) >> (p.rbits - B1);
         }
         const uint64_t nt = t + gridDim.x, nbase = nt * TILE;
-        sort_reserve_write<W, TB, NB, TILE>(
-            a, b, bin, items, sbin, hist, start, gpos, wsum,
-            [&](uint32_t q) { return &wcnt[q * (ROUTE ? 1u : S1) + sub]; },
-            [&](uint32_t q) { return (uint64_t)(q * (ROUTE ? 1u : S1) + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr,
-            stats, [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
+        if constexpr (ROUTE) {
+            // owner runs need no LDS staging: ranks per (tile, owner) by wave-aggregated LDS
+            // atomics, one reservation per (tile, owner), then every lane stores its word at its
+            // run position (a tile's run of an owner is contiguous: L2 merges the 16-B stores)
+            __shared__ uint32_t rh[MAX_RANKS], rg[MAX_RANKS];
+            if (threadIdx.x < MAX_RANKS) rh[threadIdx.x] = 0;
+            lds_barrier();
+            uint32_t rank[IPT];
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) rank[j] = wave_rank_all(rh, bin[j], a[j] != EMPTY);
+            lds_barrier();
+            if (threadIdx.x < P) {
+                const uint32_t h = rh[threadIdx.x];
+                rg[threadIdx.x] = h ? atomicAdd(&wcnt[threadIdx.x], h) : 0u;
+            }
+            lds_barrier();
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                if (a[j] == EMPTY) continue;
+                const uint64_t d = (uint64_t)bin[j] * CAP1 + rg[bin[j]] + rank[j];
+                if (W == 2)
+                    *reinterpret_cast<ulonglong2*>(buf1 + d * 2) = make_ulonglong2(a[j], b[j]);
+                else
+                    buf1[d] = a[j];
+            }
+            load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase);
+            lds_barrier();  // every lane has read rg before the next tile's counts
+        } else {
+            sort_reserve_write<W, TB, NB, TILE>(
+                a, b, bin, items, sbin, hist, start, gpos, wsum, [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
+                [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
+                [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
+        }
     }
 }
 
@@ -1330,17 +1369,15 @@ __global__ void k_route_win_counts(const uint32_t* cnt, uint32_t P, uint64_t n, 
     if (q == 0) counts[P] = n;
 }
 
-template <int W>
+template <int W, int PK>
 static hipError_t route_win_launch(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
                                    uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
                                    unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
-    constexpr int PK = W == 2 ? 13 : 5;
-    constexpr size_t lds = sort_lds_nb(REC_TILE, MAX_RANKS);
+    constexpr size_t lds = 0;  // the route stages nothing in LDS (k_win1_rec ROUTE)
     hipError_t e;
     if ((e = hipMemsetAsync(cnt, 0, (size_t)MAX_RANKS * 4, s)) != hipSuccess) return e;
     if (n) {
-        const uint64_t bpc = LDS_BYTES / (lds + 64);
-        uint64_t grid = (uint64_t)cu_count() * bpc;
+        uint64_t grid = (uint64_t)cu_count() * 4;  // resident blocks loop over the tiles
         const uint64_t ntiles = (n + REC_TILE - 1) / REC_TILE;
         if (grid > ntiles) grid = ntiles;
         e = with_kt<W>(p.K, [&](auto kt) {
@@ -1360,9 +1397,12 @@ static hipError_t route_win_launch(const KParams& p, const uint8_t* recs, uint64
 hipError_t launch_route_win(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
                             uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
                             unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
-    if (win < n || win >= (1ull << 32)) return hipErrorInvalidValue;
-    return p.W == 1 ? route_win_launch<1>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s)
-                    : route_win_launch<2>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s);
+    if (win < n || win >= (1ull << 32) || p.R > 15) return hipErrorInvalidValue;  // 64 records in 62 blocks
+    if (p.W == 1)
+        return p.P == 5 ? route_win_launch<1, 5>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s)
+                        : route_win_launch<1, 0>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s);
+    return p.P == 13 ? route_win_launch<2, 13>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s)
+                     : route_win_launch<2, 0>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s);
 }
 
 // pass 2: bucket -> region windows (RC words each)

@@ -1044,6 +1044,7 @@ int kh_route_starts_win_dev(kh_table* t, const void* dev_recs, uint64_t n, int n
     if (win < n || win >= (1ull << 32))
         return fail(KH_ERR_ARG, "window of %llu words for %llu records (need n <= win < 2^32)", (unsigned long long)win,
                     (unsigned long long)n);
+    if (t->kp.R > 15) return fail(KH_ERR_ARG, "the one-pass route takes records of <= 15 bytes (k <= 52)");
     if (int rc = set_device(t)) return rc;
     if (int rc = ensure_route(t, n, nranks)) return rc;
     const uint64_t nw = (n + 63) / 64;

@@ -65,6 +65,25 @@ __device__ __forceinline__ uint32_t wave_count_add(uint32_t* cnt, uint32_t key, 
     return want ? atomicAdd(&cnt[key], 1u) : 0u;
 }
 
+// Rank of each wanting lane among all lanes (of any wave) that add to cnt[key]: one atomic per
+// distinct key in the wave (a loop over the wave's keys), so few keys (the route's owner ranks,
+// one at P = 1) cost no same-address LDS atomic storm.
+__device__ __forceinline__ uint32_t wave_rank_all(uint32_t* cnt, uint32_t key, bool want) {
+    uint64_t act = __ballot(want);
+    uint32_t r = 0;
+    while (act) {  // uniform
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint32_t lk = __shfl(key, leader, 64);
+        const uint64_t grp = __ballot(want && key == lk);
+        uint32_t old = 0;
+        if ((int)lane_id() == leader) old = atomicAdd(&cnt[lk], (uint32_t)__popcll(grp));
+        old = __shfl(old, leader, 64);
+        if ((grp >> lane_id()) & 1ull) r = old + mbcnt64(grp);
+        act &= ~grp;
+    }
+    return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Block-wide exclusive scan of one uint64 per thread (256 threads = 4 waves of 64).
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its

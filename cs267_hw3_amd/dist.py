@@ -118,6 +118,7 @@ class ThreadComm:
         self.sh = shared
         self.rank = rank
         self.world = shared.world
+        self.ranks_per_device = shared.world  # every logical rank shares the one GPU
 
     class _Done:
         def wait(self):
@@ -207,7 +208,9 @@ class GpuShard:
         check(f(self.h, self._p(recs), n, nranks, self._p(words), self._p(counts)))
         return words, counts
 
-    route_windows = True  # route_win: one pass over the records into per-owner windows
+    @property
+    def route_windows(self):  # route_win: one pass over records of <= 15 bytes into owner windows
+        return self.R <= 15
 
     def route_win(self, recs, nranks, words, win):
         """Records -> owner q's words at words[q * win * W ...] (one pass, kh_route_starts_win_dev;
@@ -458,9 +461,14 @@ class DistributedKmerHashMap:
         # one-pass route into per-owner windows (each sized for the whole chunk, so any skew fits)
         # while P windows of the block fit the budget; the two-pass route packs back to back
         windows = getattr(sh, "route_windows", False) and P * n * W * 8 <= self.ROUTE_WINDOW_BYTES
+        if windows and recs.is_cuda:  # and a third of this rank's share of what is free
+            have = getattr(self, "_ins_words", None)
+            have = have.numel() * 8 if have is not None and have.device == recs.device else 0
+            share = getattr(self.comm, "ranks_per_device", 1)  # P logical ranks on one GPU
+            windows = P * n * W * 8 <= have + torch.cuda.mem_get_info(recs.device)[0] // (3 * share)
         if windows:
             # one-pass route: chunk c's owner windows of (c1 - c0) words each at P * c0 words
-            words = self._grow("_ins_words", max(P * n, 1) * W, torch.int64, recs.device)
+            words = self._grow("_ins_words", max(P * n, 1) * W, torch.int64, recs.device, slack=1.0)
         else:
             words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
         counts = []
@@ -519,10 +527,13 @@ class DistributedKmerHashMap:
         """Walk this rank's start k-mers (collective); returns the number of rounds."""
         return self._assemble_migrate(total_kmers)
 
-    def _grow(self, name, n, dtype, device):
+    def _grow(self, name, n, dtype, device, slack=1.25):
         t = getattr(self, name, None)
         if t is None or t.numel() < n or t.dtype != dtype or t.device != device:
-            t = torch.empty(max(int(n * 1.25), 16), dtype=dtype, device=device)
+            if t is not None:
+                setattr(self, name, None)
+                del t  # the old buffer goes back to the allocator before the new one is taken
+            t = torch.empty(max(int(n * slack), 16), dtype=dtype, device=device)
             setattr(self, name, t)
         return t
 

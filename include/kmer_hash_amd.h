@@ -139,7 +139,8 @@ int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nrank
 /* kh_route_starts_dev in ONE pass over the records (no owner pre-pass): owner q's words land in
  * the window dev_words_out + q * win words-per-k-mer (win >= n, < 2^32: a window holds every record,
  * whatever the skew), dev_counts_out[q] = their count, [nranks] = n. The all-to-all sends each
- * window's first counts[q] words. Replaces the same hash_map.hpp:28-30,64-77 routing. */
+ * window's first counts[q] words. Records of <= 15 bytes (k <= 52; KH_ERR_ARG otherwise: use
+ * kh_route_starts_dev). Replaces the same hash_map.hpp:28-30,64-77 routing. */
 int kh_route_starts_win_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* dev_words_out,
                             uint64_t win, void* dev_counts_out);
 /* dev_words: internal words as kh_route_dev / kh_route_starts_dev emit them (they carry the
