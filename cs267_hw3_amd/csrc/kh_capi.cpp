@@ -114,7 +114,9 @@ struct kh_table {
     bool words_split = true;   // every routed word since the last clear went through splitter collection
     bool ms_on = false;        // the current migrating walk uses splitter segments
     uint64_t ms_ns = 0, ms_nsp = 0, ms_cap2 = 0, ms_nq = 0;
-    uint64_t mw_store_n = 0;   // text records in mw_store
+    uint64_t mw_store_n = 0;   // text records in mw_store (valid when mw_store_known)
+    uint64_t mw_store_bound = 0;  // upper bound of the store's records (its device count: mw_misc[2])
+    bool mw_store_known = true;
     uint32_t mw_P = 0, mw_rank = 0;
     bool mw_live = false, mw_stepped = false;
     bool mw_hot = true;        // the shard has remapped regions (the walk reads the bitmap)
@@ -1217,6 +1219,17 @@ static kh::MSegState mseg_state(kh_table* t) {
     return st;
 }
 
+// The text store's record count (one host read after the rounds, not one per round).
+static int mw_store_count(kh_table* t) {
+    if (t->mw_store_known) return KH_OK;
+    unsigned long long v = 0;
+    KH_HIP(hipMemcpyAsync(&v, t->mw_misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    t->mw_store_n = v;
+    t->mw_store_known = true;
+    return KH_OK;
+}
+
 int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t* n_walkers) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (nranks < 1 || nranks > kh::MAX_RANKS || rank < 0 || rank >= nranks)
@@ -1224,16 +1237,18 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     if (int rc = set_device(t)) return rc;
     if (int rc = clean_slots(t)) return rc;
     int rc;
-    uint64_t ns = 0, nhot = 0;
-    if ((rc = read_ctr(t, kh::CT_N_STARTS, &ns)) || (rc = read_ctr(t, kh::CT_HOT, &nhot))) return rc;
-    t->mw_hot = nhot != 0;
+    unsigned long long cv[kh::CT_NUM];  // one read of the counters (starts, hot regions, splitters)
+    KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipStreamSynchronize(t->stream));
+    const uint64_t ns = cv[kh::CT_N_STARTS];
+    t->mw_hot = cv[kh::CT_HOT] != 0;
     if (ns >= (1ull << 31)) return fail(KH_ERR_ARG, "%llu start k-mers on one rank (max 2^31)", (unsigned long long)ns);
     // splitter segments: every splitter this shard owns seeds a walker too (kh_mseg.hip)
     // on or off the same way on every rank (walkers stop before splitters owned anywhere)
     uint64_t nsp = 0;
     t->ms_on = mseg_enabled(t) && t->words_split;
     if (t->ms_on && t->splits.p) {
-        if ((rc = read_ctr(t, kh::CT_N_SPLIT, &nsp))) return rc;
+        nsp = cv[kh::CT_N_SPLIT];
         if (nsp > t->splits_cap)
             return fail(KH_ERR_FULL, "%llu splitter k-mers exceed the list (%llu)", (unsigned long long)nsp,
                         (unsigned long long)t->splits_cap);
@@ -1263,6 +1278,9 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     t->rw_n = ns;
     t->rw_total = total_kmers > ns ? total_kmers : ns;
     t->mw_store_n = 0;
+    t->mw_store_bound = 0;
+    t->mw_store_known = true;
+    KH_HIP(hipMemsetAsync(t->mw_misc.as<unsigned long long>() + 2, 0, 8, t->stream));
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
     t->wk_timed = false;
     KH_HIP(kh::launch_mw_init(t->kp, t->starts.as<uint64_t>(), ns, (uint32_t)rank, t->mw_init.as<uint64_t>(),
@@ -1436,16 +1454,21 @@ int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, vo
     kh::KParams kp = t->kp;
     if (!t->mw_hot) kp.hot = nullptr;
     KH_HIP(kh::launch_mw_run(kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
-    // text records of this round -> the rank-local store (the host needs their count to size it)
-    unsigned long long* tot = t->mw_misc.as<unsigned long long>();
-    KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), tot, t->stream));
-    uint64_t m = 0;
-    KH_HIP(hipMemcpyAsync(&m, tot, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
-    if ((rc = grow_keep(t->mw_store, (t->mw_store_n + m) * 16, t->mw_store_n * 16, t->stream))) return rc;
-    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>() + t->mw_store_n * 2,
-                                 t->stream));
-    t->mw_store_n += m;
+    // text records of this round -> the rank-local store at offsets continuing its device-side
+    // count: the store is sized from an upper bound (MW_REC_SLOTS per walker and round), so no
+    // host round trip per round; past a few GB of bound the actual count is read once
+    unsigned long long* store_n = t->mw_misc.as<unsigned long long>() + 2;
+    const uint64_t add = n * (uint64_t)kh::MW_REC_SLOTS;
+    if (t->mw_store_bound + add > (1ull << 28) && !t->mw_store_known) {
+        if ((rc = mw_store_count(t))) return rc;
+        t->mw_store_bound = t->mw_store_n;
+    }
+    if ((rc = grow_keep(t->mw_store, (t->mw_store_bound + add) * 16 + 16, t->mw_store_bound * 16, t->stream)))
+        return rc;
+    KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), store_n, t->stream));
+    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>(), t->stream));
+    t->mw_store_bound += add;
+    t->mw_store_known = false;
     KH_HIP(kh::launch_mw_group(mw, t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
                                t->route_scratch.as<uint64_t>(), (uint64_t*)out, (uint64_t*)counts, t->stream));
     t->mw_stepped = true;
@@ -1455,12 +1478,14 @@ int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, vo
 int kh_mwalk_text_count(kh_table* t, uint64_t* n_records) {
     if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
     if (!n_records) return fail(KH_ERR_ARG, "null output");
+    if (int rc = mw_store_count(t)) return rc;
     *n_records = t->mw_store_n;
     return KH_OK;
 }
 
 int kh_mwalk_text_dev(kh_table* t, void* out, void* counts) {
     if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (int rc = mw_store_count(t)) return rc;
     if (!counts || (t->mw_store_n && !out)) return fail(KH_ERR_ARG, "null buffer");
     if (int rc = set_device(t)) return rc;
     if (int rc = ensure_route(t, t->mw_store_n, (int)t->mw_P)) return rc;

@@ -192,8 +192,9 @@ hipError_t launch_mseg_words(int K, const uint64_t* recs, uint64_t n, const uint
                              const MSegState& st, const uint64_t* off, char* out, hipStream_t s);
 hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
                          hipStream_t s);
+// text records of this round: absolute store offsets continuing *store_n (device counter, updated)
 hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
-                                  unsigned long long* total, hipStream_t s);
+                                  unsigned long long* store_n, hipStream_t s);
 hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, hipStream_t s);
 hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, uint64_t* scratch,
                            uint64_t* out, uint64_t* counts, hipStream_t s);

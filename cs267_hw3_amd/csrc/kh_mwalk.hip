@@ -320,9 +320,10 @@ hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, un
 }
 
 hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
-                                  unsigned long long* total, hipStream_t s) {
-    if (mw.n_in == 0) return hipMemsetAsync(total, 0, 8, s);
-    return scan_exclusive(NrecF{mw.nrec}, mw.n_in, off, scratch, (unsigned long long*)nullptr, total, s);
+                                  unsigned long long* store_n, hipStream_t s) {
+    if (mw.n_in == 0) return hipSuccess;
+    // offsets continue the store's running count (store_n, on the device: no host round trip)
+    return scan_exclusive(NrecF{mw.nrec}, mw.n_in, off, scratch, store_n, (unsigned long long*)nullptr, s);
 }
 
 hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, hipStream_t s) {
