@@ -65,6 +65,24 @@ __device__ __forceinline__ uint32_t wave_count_add(uint32_t* cnt, uint32_t key, 
     return want ? atomicAdd(&cnt[key], 1u) : 0u;
 }
 
+// Quad (4-lane) exchanges by DPP: the walkers' transposed block probes (k_walk_q, k_mw_run).
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int J>
+__device__ __forceinline__ uint64_t qbcast64(uint64_t v) {  // value of quad lane J
+    constexpr int C = J * 0x55;  // quad_perm [J,J,J,J]
+    return ((uint64_t)qperm32<C>((uint32_t)(v >> 32)) << 32) | qperm32<C>((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t qor32(uint32_t v) {
+    v |= qperm32<0xB1>(v);  // [1,0,3,2]
+    v |= qperm32<0x4E>(v);  // [2,3,0,1]
+    return v;
+}
+static constexpr uint64_t WQ_REC = 1ull << 63;  // walker's next load is a head record (index below)
+static constexpr uint64_t WQ_IDLE = ~0ull;
+
 // Rank of each wanting lane among all lanes (of any wave) that add to cnt[key]: one atomic per
 // distinct key in the wave (a loop over the wave's keys), so few keys (the route's owner ranks,
 // one at P = 1) cost no same-address LDS atomic storm.

@@ -315,23 +315,6 @@ __device__ __forceinline__ uint64_t walk_splits(const WalkBuffers& wb) {
 // k-mer (tail) whose low 2*links bits ARE those bases — and continues from the tail's extension.
 // A C3 contig (~104 k-mers) costs ~6 such hops of two dependent requests instead of ~104 lookups.
 // Every walker starts by looking up its own start k-mer (to find its record).
-template <int CTRL>
-__device__ __forceinline__ uint32_t qperm32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-template <int J>
-__device__ __forceinline__ uint64_t qbcast64(uint64_t v) {  // value of quad lane J
-    constexpr int C = J * 0x55;  // quad_perm [J,J,J,J]
-    return ((uint64_t)qperm32<C>((uint32_t)(v >> 32)) << 32) | qperm32<C>((uint32_t)v);
-}
-__device__ __forceinline__ uint32_t qor32(uint32_t v) {
-    v |= qperm32<0xB1>(v);  // [1,0,3,2]
-    v |= qperm32<0x4E>(v);  // [2,3,0,1]
-    return v;
-}
-
-static constexpr uint64_t WQ_REC = 1ull << 63;  // walker's next load is a head record (index below)
-static constexpr uint64_t WQ_IDLE = ~0ull;
 
 template <int W, int KT>
 __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* __restrict__ slots,

@@ -34,6 +34,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                                                   MWalkRound mw, unsigned long long* stats) {
     const KParams p = specialize<KT>(p_in);
     const bool chains = p.chain && mw.hcap != 0;
+    const uint32_t q4 = lane_id() & 3u, ql4 = lane_id() & ~3u;  // quad member, quad's first lane
     uint32_t reg = 0;  // region of the k-mer being probed (its head records live there)
     // append n bases (base i at bits 2i of piece, n <= room in the current word) to the walker's
     // buffer, flushing a finished 32-base word as a text record
@@ -149,13 +150,54 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                 j += stride;
             }
         }
+        // quad-transposed block probe (as k_walk_q): lane q of a quad loads slot q of each member's
+        // 64-B block (one request per block), the members learn their first hit / EMPTY by ballot
+        const uint64_t sp = (active && probing) ? s : WQ_IDLE;
+        uint64_t sj[4], w0[4], w1[4];
+        sj[0] = qbcast64<0>(sp);
+        sj[1] = qbcast64<1>(sp);
+        sj[2] = qbcast64<2>(sp);
+        sj[3] = qbcast64<3>(sp);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            w0[jj] = EMPTY;
+            w1[jj] = 0;
+            const uint64_t my = (sj[jj] & ~3ull) + q4;
+            if (sj[jj] != WQ_IDLE && my < cap) load_slot_nt<W>(slots, my, w0[jj], w1[jj]);
+        }
+        uint64_t kh_[4], kl_[4];
+        kh_[0] = qbcast64<0>(k.hi);
+        kh_[1] = qbcast64<1>(k.hi);
+        kh_[2] = qbcast64<2>(k.hi);
+        kh_[3] = qbcast64<3>(k.hi);
+        kl_[0] = qbcast64<0>(k.lo);
+        kl_[1] = qbcast64<1>(k.lo);
+        kl_[2] = qbcast64<2>(k.lo);
+        kl_[3] = qbcast64<3>(k.lo);
+        uint32_t myfh = 4, myfe = 4, myext = 0;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const uint64_t my = (sj[jj] & ~3ull) + q4;
+            const bool valid = sj[jj] != WQ_IDLE && my >= sj[jj] && my < cap;
+            const bool empty = w0[jj] == EMPTY;
+            const bool hit = !empty & (slot_keybits(w0[jj], p) == ((W == 1) ? kl_[jj] : kh_[jj])) &
+                             ((W == 1) | (w1[jj] == kl_[jj]));
+            const uint32_t bh = (uint32_t)(__ballot(valid && hit) >> ql4) & 0xFu;
+            const uint32_t be = (uint32_t)(__ballot(valid && empty) >> ql4) & 0xFu;
+            const uint32_t fh = bh ? (uint32_t)__builtin_ctz(bh) : 4u;
+            const uint32_t fe = be ? (uint32_t)__builtin_ctz(be) : 4u;
+            // hit slot: ext | found flag | head-record index << 7
+            const uint32_t ext =
+                qor32(q4 == fh ? (slot_ext(w0[jj]) | 0x40u | ((chains ? slot_hidx(w0[jj], p) : 0u) << 7)) : 0u);
+            if (q4 == (uint32_t)jj) {
+                myfh = fh;
+                myfe = fe;
+                myext = ext;
+            }
+        }
         if (active && probing) {
-            uint64_t w0, w1;
-            load_slot<W>(slots, s, w0, w1);
-            const bool empty = w0 == EMPTY;
-            const bool hit = !empty & (slot_keybits(w0, p) == ((W == 1) ? k.lo : k.hi)) & ((W == 1) | (w1 == k.lo));
-            if (hit) {
-                const uint32_t hidx = chains ? slot_hidx(w0, p) : 0u;
+            if (myfh < myfe) {
+                const uint32_t hidx = myext >> 7;
                 if (hidx && nwords + 3 <= MW_RUN_WORDS) {  // the run's <= 2 words fit this round
                     const ulonglong2 rv =
                         *reinterpret_cast<const ulonglong2*>(mw.headrec + ((uint64_t)reg * mw.hcap + hidx - 1) * 2);
@@ -174,10 +216,10 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                         n -= m;
                     }
                 } else {
-                    st = ext_fwd(slot_ext(w0));
+                    st = ext_fwd(myext & 63u);
                 }
                 probing = false;
-            } else if (empty) {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
+            } else if (myfe < 4u) {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
                 atomicAdd(&stats[ST_MISSING], 1ull);
                 if (steps & 31) {
                     rec[2 * nrec] = rec_tag(origin, false, steps >> 5, idx);
@@ -192,7 +234,8 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                 active = false;
                 j += stride;
             } else {
-                s = (s + 1 == cap) ? 0 : s + 1;
+                const uint64_t nx = (s & ~3ull) + 4;
+                s = nx >= cap ? 0 : nx;
             }
         }
     }
