@@ -413,7 +413,7 @@ class DistributedKmerHashMap:
     # (KH_INSERT_CHUNKS=1: one transfer)
     INSERT_CHUNKS = int(os.environ.get("KH_INSERT_CHUNKS", "4"))
     ROUTE_WINDOW_BYTES = int(os.environ.get("KH_ROUTE_WINDOW_GB", "64")) << 30
-    PIPELINE_MIN = 1 << 22  # records per rank below which the insert is one chunk
+    PIPELINE_MIN = int(os.environ.get("KH_PIPELINE_MIN", 1 << 22))  # records per rank below which one chunk
 
     def _exchange_count_matrix(self, counts):
         """counts: list over chunks of [P+1] int64 device tensors (per-destination, total) ->

@@ -43,10 +43,17 @@ def test_driver_rejects_wrong_k(tmp_path):
 
 
 @pytest.mark.gpu
-def test_dist_launcher_one_rank(tmp_path):
-    """cs267_hw3_amd.kmer_hash_dist under torchrun (1 rank, RCCL): same test_0.dat."""
+@pytest.mark.parametrize("mode", ["plain", "self_exchange", "self_exchange_pipelined"])
+def test_dist_launcher_one_rank(tmp_path, mode):
+    """cs267_hw3_amd.kmer_hash_dist under torchrun (1 rank, RCCL): same test_0.dat. The
+    self-exchange modes run every exchange through RCCL anyway (the per-peer window views of the
+    one-pass route, count exchanges, walker rounds; pipelined: chunked async all-to-alls)."""
     import sys
     env = dict(os.environ, PYTHONPATH=ROOT)
+    if mode != "plain":
+        env["KH_DIST_SELF_EXCHANGE"] = "1"
+    if mode == "self_exchange_pipelined":
+        env["KH_PIPELINE_MIN"] = "0"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
                         "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port",
                         "29533", "-m", "cs267_hw3_amd.kmer_hash_dist",
