@@ -202,7 +202,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--n", type=int, default=0, help="override k-mers per GPU")
+    ap.add_argument("--n", "--kmers", dest="n", type=int, default=0,
+                    help="override k-mers per GPU (--kmers under torchrun: its argparse takes --n "
+                         "for an abbreviation of its own options)")
     ap.add_argument("--load", type=float, default=0.5,
                     help="table load factor (kmer_hash.cpp:109 uses 0.5; SURVEY C5 names a 0.85 variant)")
     ap.add_argument("--cpu-sample", type=int, default=20_000_000,

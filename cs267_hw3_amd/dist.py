@@ -34,6 +34,22 @@ from ._lib import check
 
 # --------------------------------------------------------------------------------------------
 # Communicators
+def init_rank_process_group():
+    """One process per GPU: LOCAL_RANK's device, RCCL (backend "nccl") over xGMI. Returns the
+    device index. Rehearsal of the multi-process path on a box with fewer GPUs than ranks:
+    KH_DIST_DEVICE=<d> puts every local rank on device d and KH_DIST_BACKEND=gloo moves the
+    exchanges through gloo (RCCL refuses two ranks on one GPU); the kernels, the SPMD protocol
+    and its collectives are the same."""
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    shared = os.environ.get("KH_DIST_DEVICE")
+    dev = int(shared) if shared else local
+    torch.cuda.set_device(dev)
+    backend = os.environ.get("KH_DIST_BACKEND", "nccl")
+    dist.init_process_group(backend, device_id=torch.device("cuda", dev) if backend == "nccl" else None)
+    return dev
+
+
 class TorchComm:
     """torch.distributed process group (nccl = RCCL over xGMI on MI355X, or gloo on CPU)."""
 
@@ -44,6 +60,9 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        # processes sharing one GPU (KH_DIST_DEVICE rehearsals) split its free memory
+        self.ranks_per_device = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) if os.environ.get(
+            "KH_DIST_DEVICE") else 1
 
     def all_to_all_async(self, out, inp, out_splits, in_splits):
         return self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=True)
@@ -726,9 +745,7 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
     import torch.distributed as dist
     from .hashmap import SyntheticKmers, record_size
 
-    local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    local = init_rank_process_group()
     comm = TorchComm()
     k = w["k"]
     strong = bool(w.get("strong"))

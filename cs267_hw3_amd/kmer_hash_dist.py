@@ -27,7 +27,7 @@ def main(argv):
     import torch  # noqa: F401  (before the C ABI library: one HIP runtime)
     import torch.distributed as dist
 
-    from .dist import DistributedKmerHashMap, GpuShard, TorchComm
+    from .dist import DistributedKmerHashMap, GpuShard, TorchComm, init_rank_process_group
     from .hashmap import kmer_size, read_kmer_lines, record_size
 
     if len(argv) < 1:
@@ -36,10 +36,7 @@ def main(argv):
     fname = argv[0]
     run_type = argv[1] if len(argv) >= 2 else ""
     prefix = argv[2] if run_type == "test" and len(argv) >= 3 else "test"
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    backend = os.environ.get("KH_DIST_BACKEND", "nccl")
-    dist.init_process_group(backend, device_id=torch.device("cuda", local) if backend == "nccl" else None)
+    local = init_rank_process_group()
     rank, world = dist.get_rank(), dist.get_world_size()
     k = kmer_size(fname)
     n_total = os.path.getsize(fname) // (k + 4)

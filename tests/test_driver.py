@@ -62,3 +62,45 @@ def test_dist_launcher_one_rank(tmp_path, mode):
     assert r.returncode == 0, r.stderr[-3000:]
     got = open(tmp_path / "out_0.dat", "rb").read()
     assert got == open(os.path.join(GOLDEN, "small51_test_0.dat"), "rb").read()
+
+
+def _torchrun(P, port, args, cwd, env, timeout=300):
+    import sys
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+                           "--nproc-per-node", str(P), "--master-addr", "127.0.0.1", "--master-port",
+                           str(port)] + args, cwd=cwd, capture_output=True, text=True, timeout=timeout,
+                          env=env)
+
+
+def _shared_gpu_env():
+    """P processes on the one GPU of the test box (KH_DIST_DEVICE=0), exchanging over gloo: RCCL
+    refuses two ranks on one device, everything else (kernels, SPMD protocol, collectives, the
+    launcher and bench's timing bracket) is the multi-GPU code path."""
+    return dict(os.environ, PYTHONPATH=ROOT, KH_DIST_BACKEND="gloo", KH_DIST_DEVICE="0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,P", [("small51", 2), ("small51", 4), ("verysmall19", 3)])
+def test_dist_launcher_multiprocess(tmp_path, name, P):
+    """P real processes (torchrun), one shard each: every rank writes its block's contigs in its
+    start-node order (kmer_hash.cpp:60-68), so out_0.dat + ... + out_{P-1}.dat is the one-rank
+    solution byte for byte (read_kmers.hpp:55-58 block split)."""
+    r = _torchrun(P, 29541 + P, ["-m", "cs267_hw3_amd.kmer_hash_dist", os.path.join(GOLDEN, f"{name}.txt"),
+                                 "test", "out"], tmp_path, _shared_gpu_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = b"".join(open(tmp_path / f"out_{q}.dat", "rb").read() for q in range(P))
+    assert got == open(os.path.join(GOLDEN, f"{name}_test_0.dat"), "rb").read()
+    assert f"Rank 0 reconstructed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_bench_multiprocess(tmp_path):
+    """bench.py's N > 1 line from 2 real processes: barrier + sync bracket, max over ranks, the
+    ground-truth check on every rank, roofline and phases from rank 0."""
+    import json
+    r = _torchrun(2, 29551, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--kmers", "2000000", "--steps", "2",
+                             "--warmup", "1", "--no-cpu", "--e2e-steps", "0"], tmp_path, _shared_gpu_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert line["n_gpus"] == 2 and line["verified_vs_truth"] is True
+    assert line["config"]["n_kmers_total"] == 4_000_000 and line["value"] > 0
