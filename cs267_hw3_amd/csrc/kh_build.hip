@@ -39,7 +39,6 @@ static constexpr int B1 = 9, B2 = 8;              // radix bits per pass (pass 2
 static constexpr int NB1 = 1 << B1, NB2 = 1 << B2;
 static constexpr uint32_t NREG_MAX = 1u << (B1 + B2);
 static_assert(B1 == REGION_BITS_MIN && B1 + B2 == REGION_BITS_MAX, "regions of the placement hash");
-__host__ __device__ inline uint32_t nreg(const KParams& p) { return 1u << p.rbits; }
 static constexpr int BUILD_THREADS = 512;
 static constexpr int T1 = 2;                      // consecutive tiles per pass-1 block
 static constexpr uint32_t S1 = 8;                 // pass-1 windows (atomic counters) per bucket
@@ -478,6 +477,8 @@ __device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long
                                             uint32_t r, bool fresh, uint64_t* headrec, uint32_t hcap,
                                             const uint32_t* hcnt) {
     const uint32_t nh = min(*hcnt, hcap);
+    // the region's record count (after the records: k_rec_succ resolves only these)
+    if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(headrec + (uint64_t)nreg(p) * hcap * 2)[r] = nh;
     for (uint32_t id = threadIdx.x; id < nh; id += TB) {
         const uint32_t i = hlist[id];
         const uint64_t w0 = lt[W * i];
@@ -501,7 +502,7 @@ __device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long
         }
         const uint64_t tw1 = W == 2 ? lt[W * t + 1] & LO_MASK : 0ull;
         *reinterpret_cast<ulonglong2*>(headrec + ((uint64_t)r * hcap + id) * 2) =
-            make_ulonglong2(with_hidx(slot_clean(tw0, p) & (W == 1 ? ~PRED : ~0ull), links, p), tw1);
+            make_ulonglong2(with_hidx(tw0 & ((1ull << p.idx_lo) - 1), links, p), tw1);  // succ 0
         lt[W * i] = with_hidx(slot_clean(w0, p), id + 1, p);
     }
 }

@@ -236,7 +236,13 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     b.rbt = t->rbounds.as<uint64_t>();
     // chain head records: sized by the table (regions x records per region), kept across builds
     const uint32_t hcap = kh::debug_flag("no_chains") ? 0u : kh::part_head_cap(t->kp, t->cap);
-    if (hcap && (rc = t->headrec.ensure((uint64_t)hcap * (1ull << t->kp.rbits) * 16))) return rc;
+    if (hcap) {
+        // + the per-region record counts the build writes after the records (k_rec_succ reads them)
+        const uint64_t recb = (uint64_t)hcap * (1ull << t->kp.rbits) * 16, cntb = (1ull << t->kp.rbits) * 4;
+        const void* before = t->headrec.p;
+        if ((rc = t->headrec.ensure(recb + cntb))) return rc;
+        if (t->headrec.p != before) KH_HIP(hipMemsetAsync((char*)t->headrec.p + recb, 0, cntb, t->stream));
+    }
     t->hcap = hcap;
     b.headrec = hcap ? t->headrec.as<uint64_t>() : nullptr;
     b.hcap = hcap;
@@ -752,7 +758,30 @@ int kh_assemble_dev(kh_table* t) {
     for (int attempt = 0;; ++attempt) {
         KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
         KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
+        // Successor runs of the head records (k_rec_succ). A record read before its successor is
+        // resolved still says 0 (the walker probes, as without), so the resolve runs on the side
+        // stream beside the walk (request-bound beside a latency-bound walker); the table stream
+        // waits for it after the walk (the next build rewrites the records).
+        bool succ_side = false;
+        if (attempt == 0 && wb.hcap && !kh::debug_flag("no_rec_succ") && kh::rec_succ_fits(kp, wb.hcap)) {
+            const char* ce = getenv("KH_SUCC_CONC");  // 0: before the walk on the table stream
+            const char* be = getenv("KH_SUCC_BLOCKS");
+            const bool conc = !ce || atoi(ce) != 0;
+            // beside the walk: 1024 blocks (C3 walk + resolve 1.28 ms; the full 8192-block grid
+            // 1.32-1.34, 256 blocks 1.85: the resolve then lags the walkers; no resolve 1.46)
+            const unsigned blocks = be ? (unsigned)atoi(be) : (conc ? 1024u : 0u);
+            hipStream_t rs = t->stream;
+            if (conc && t->side) {
+                KH_HIP(hipEventRecord(t->ev_side, t->stream));
+                KH_HIP(hipStreamWaitEvent(t->side, t->ev_side, 0));
+                rs = t->side;
+                succ_side = true;
+            }
+            KH_HIP(kh::launch_rec_succ(kp, view(t), t->headrec.as<uint64_t>(), wb.hcap, rs, blocks));
+            if (succ_side) KH_HIP(hipEventRecord(t->ev_conv, t->side));
+        }
         KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, 0, t->stream));
+        if (succ_side) KH_HIP(hipStreamWaitEvent(t->stream, t->ev_conv, 0));
         KH_HIP(hipEventRecord(t->ev_wk1, t->stream));
         t->wk_timed = true;
         if (kp.split_bits) KH_HIP(kh::launch_segments(kp, wb, sb, stats, t->stream));

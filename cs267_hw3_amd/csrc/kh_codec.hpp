@@ -403,6 +403,16 @@ KH_HD uint64_t with_hidx(uint64_t w0, uint32_t v, const KParams& p) {
     const uint64_t f = ((1ull << (SCRATCH_BIT - p.idx_lo)) - 1) << p.idx_lo;
     return (w0 & ~f) | (((uint64_t)v << p.idx_lo) & f);
 }
+// placement regions of the table (2^rbits)
+KH_HD uint32_t nreg(const KParams& p) { return 1u << p.rbits; }
+
+// Head records (kh_build.hip chain_heads): word 0 = the run's tail k-mer word 0 (key + ext), the
+// link count in the low 6 bits of the index field and, from bit idx_lo + 6 up, the head-record
+// index + 1 (within its region) of the run that follows the tail, 0 = none: the walker then looks
+// the next k-mer up. The build writes 0 there; k_rec_succ resolves it before a walk.
+KH_HD uint32_t rec_links(uint64_t r0, const KParams& p) { return (uint32_t)(r0 >> p.idx_lo) & 63u; }
+KH_HD int rec_succ_shift(const KParams& p) { return p.idx_lo + 6; }
+KH_HD uint32_t rec_succ(uint64_t r0, const KParams& p) { return (uint32_t)(r0 >> rec_succ_shift(p)); }
 // key + ext + j* only (head index and scratch cleared)
 KH_HD uint64_t slot_clean(uint64_t w0, const KParams& p) {
     return p.chain ? (w0 & (((1ull << p.idx_lo) - 1) | (63ull << JSTAR_SHIFT))) : w0;

@@ -338,6 +338,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
     uint32_t reg = 0;  // region of the k-mer being looked up (its head records live there)
     Key k{0, 0};
     uint32_t fwd = 0, steps = 0, chunk = 0;
+    uint32_t nrec = 0;  // the last record's successor run (head-record index + 1 in its region)
     // look up key k: s = its home slot (the hit may carry a head-record index)
     auto lookup = [&]() {
         const Place pl = place(k, p);
@@ -397,6 +398,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                         fwd = ext_fwd(slot_ext(x0));
                         steps = 0;
                         buf = 0;
+                        nrec = 0;
                         active = true;
                         entry = chains;
                         if (chains)
@@ -426,6 +428,12 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                 wb.seg_key[2 * c] = k.hi;
                 wb.seg_key[2 * c + 1] = k.lo;
                 active = false;
+            } else if (nrec) {
+                // the record named the run that starts at k (k_rec_succ): read it, no probe
+                reg = place(k, p).r;
+                s = WQ_REC | ((uint64_t)reg * wb.hcap + nrec - 1);
+                resolved = false;
+                nrec = 0;
             } else {
                 lookup();
             }
@@ -491,7 +499,8 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                 // head record: jump to the run's tail, appending the bases of its links
                 k = slot_key(r0, r1, p);
                 fwd = ext_fwd(slot_ext(r0));
-                const uint32_t links = slot_hidx(r0, p);
+                const uint32_t links = rec_links(r0, p);
+                nrec = rec_succ(r0, p);
                 append_key_tail(o, c, k, links, steps, chunk, buf, ctr, stats);
                 resolved = true;
                 if (steps > wb.max_steps) {
@@ -530,6 +539,50 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
             }
         }
     }
+}
+
+// Successor of every head record of the last build: the run after the tail starts at
+// y = next_kmer(tail); when y's slot carries a head-record index (y heads a run with a record),
+// that index goes into the record (rec_succ), so the walker reads y's record straight after this
+// one instead of probing y's slot first (one dependent request per run instead of two). One wave
+// per region over its records (count after the records, written by the build). Splitters need no
+// test here: the walker checks the next k-mer for one before it follows a successor.
+template <int W, int KT>
+__global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
+                                                    uint64_t* headrec, uint32_t hcap) {
+    const KParams p = specialize<KT>(p_in);
+    const uint32_t NR = nreg(p);
+    const uint32_t* hn = reinterpret_cast<const uint32_t*>(headrec + (uint64_t)NR * hcap * 2);
+    const int sh = rec_succ_shift(p);
+    const uint32_t lane = lane_id(), waves = gridDim.x * (BLOCK / 64);
+    for (uint32_t r = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; r < NR; r += waves) {
+        const uint32_t n = min(hn[r], hcap);
+        for (uint32_t id = lane; id < n; id += 64) {
+            uint64_t* rec = headrec + ((uint64_t)r * hcap + id) * 2;
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(rec);
+            const uint32_t f = ext_fwd(slot_ext(v.x));
+            uint32_t succ = 0;
+            uint64_t w0 = 0;
+            if (f <= 3u && probe<W>(key_next(slot_key(v.x, v.y, p), f, p), p, slots, cap, w0))
+                succ = slot_hidx(w0, p);
+            rec[0] = (v.x & ((1ull << sh) - 1)) | ((uint64_t)succ << sh);
+        }
+    }
+}
+
+bool rec_succ_fits(const KParams& p, uint32_t hcap) {
+    return p.chain && hcap && rec_succ_shift(p) < 64 && (uint64_t)hcap + 1 < (1ull << (64 - rec_succ_shift(p)));
+}
+
+hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uint32_t hcap, hipStream_t s,
+                           unsigned blocks) {
+    if (!rec_succ_fits(p, hcap)) return hipSuccess;
+    const unsigned grid = blocks ? blocks : (unsigned)hmin((nreg(p) + BLOCK / 64 - 1) / (BLOCK / 64), 8192);
+    if (p.W == 1)
+        with_kt<1>(p.K, [&](auto kt) { k_rec_succ<1, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, headrec, hcap); });
+    else
+        with_kt<2>(p.K, [&](auto kt) { k_rec_succ<2, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, headrec, hcap); });
+    return hipGetLastError();
 }
 
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,

@@ -92,6 +92,10 @@ struct WalkBuffers {
 
 // Persistent per-lane walker (single GPU): every lane walks whole contigs, pulling start k-mers
 // from a wave-batched work queue.
+// head records' successor runs (before a walk; KH_REC_SUCC=0 skips it: the walker then probes)
+bool rec_succ_fits(const KParams& p, uint32_t hcap);
+hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uint32_t hcap, hipStream_t s,
+                           unsigned blocks = 0);
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s);
 

@@ -203,7 +203,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                         *reinterpret_cast<const ulonglong2*>(mw.headrec + ((uint64_t)reg * mw.hcap + hidx - 1) * 2);
                     k = slot_key(rv.x, rv.y, p);
                     st = ext_fwd(slot_ext(rv.x));
-                    uint32_t n = slot_hidx(rv.x, p);  // links: the last n bases of the tail key
+                    uint32_t n = rec_links(rv.x, p);  // links: the last n bases of the tail key
                     while (n) {
                         const uint32_t room = 32u - (steps & 31u), m = n < room ? n : room;
                         const int sh = 2 * (int)(n - m);  // bits [sh, sh + 2m) of V, oldest base first

@@ -172,6 +172,27 @@ def test_generated_vs_oracle(k, n, lmin, lmax, single, seed):
     assert got == want and gnc == nc
 
 
+@pytest.mark.parametrize("succ", ["side", "inline", "off"])
+@pytest.mark.parametrize("k", [19, 51])
+def test_record_successors(monkeypatch, k, succ):
+    """Head records name the record of the run after their tail (k_rec_succ): resolved beside the
+    walk (records read before their successor is resolved still say 0), before it, or not at all;
+    the text is the oracle's in every case, and a second walk of the same table reads resolved
+    records only."""
+    if succ == "off":
+        monkeypatch.setenv("KH_DEBUG", "no_rec_succ")
+    monkeypatch.setenv("KH_SUCC_CONC", "0" if succ == "inline" else "1")
+    g = kh.SyntheticKmers(k, 1_000_000, 8, 400, 10, seed=k + 7)
+    recs = g.records()
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0
+    with kh.KmerHashTable(k, len(recs), device=0) as t:
+        t.insert_all(recs)
+        for _ in range(2):
+            got_nc, _ = t.assemble()
+            assert got_nc == nc and t.contigs_text() == want
+
+
 def test_c2_full_size_vs_truth():
     # BASELINE configs[1]: k=19, 10M synthetic k-mers, bit-exact (vs generator ground truth,
     # which the oracle matches at every smaller size above)
