@@ -296,8 +296,10 @@ def main():
     # 16-B word in and two 16-B slots out per k-mer (load 0.5), 48 B
     kb = kernel_roof("k_part_build_pf (region build + chains)", n, build_ms, "k_part_build", "inserts")
     kb["inherent_bytes_per_unit"] = 48
-    # contig walk: one lookup per k-mer but, with chains, ~2 random requests per run of ~19 k-mers
-    kw = kernel_roof("k_walk_q (contig walk, chain hops)", nl, walkk_ms, "k_walk", "lookups")
+    # contig walk: one lookup per k-mer but, with chains, ~1 random request per run of ~19 k-mers
+    # (the record of the next run, named by k_rec_succ beside the walk: both in the HIP-event bracket
+    # and in the PMC sums)
+    kw = kernel_roof("k_walk_q + k_rec_succ (contig walk, chain hops)", nl, walkk_ms, "k_walk", "lookups")
     rq = ((traffic or {}).get("requests") or {}).get("TCC_EA0_RDREQ_sum", {}).get("k_walk")
     kw["requests_per_lookup"] = rq / nl if rq else None  # 64-B HBM read requests (PMC) per lookup
     # the walk in what it moves: PMC bytes (traffic_GBs above) and random 64-B requests per second

@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-KERNELS = {"k_insert": ("k_insert<",), "k_walk": ("k_walk<", "k_walk_g<", "k_walk_q<"),
+KERNELS = {"k_insert": ("k_insert<",), "k_walk": ("k_walk<", "k_walk_g<", "k_walk_q<", "k_rec_succ<"),
            "k_win1": ("k_win1<",), "k_win1_rec": ("k_win1_rec<",), "k_win2": ("k_win2<",),
            "k_part1_convert": ("k_part1_convert<",), "k_part1_fused": ("k_part1_fused<",),
            "k_part1_scatter": ("k_part1_scatter<",), "k_part2_hist": ("k_part2_hist<",),
