@@ -100,6 +100,7 @@ struct kh_table {
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
     DevBuf headrec;                           // chain head records (region build -> walker)
+    DevBuf start_rec;                         // each walker's own head record (k_start_rec)
     DevBuf hot;                               // remapped-region bitmap (KParams::hot), HOT_WORDS words
     DevBuf rbounds;                           // balanced region bounds (KParams::rb), 2^17 + 1 words
     uint32_t hcap = 0;                        // head records per region (0 = no chains)
@@ -371,9 +372,9 @@ int kh_destroy(kh_table* t) {
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
-                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot, &t->rbounds};
+                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot, &t->rbounds, &t->start_rec};
+    if (t->side) (void)hipStreamSynchronize(t->side);  // k_rec_succ may still read the table
     for (auto* b : bufs) b->release();
-    if (t->side) (void)hipStreamSynchronize(t->side);
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_b0,
                         t->ev_b1, t->ev_wk1, t->ev_conv,
                         t->ev_side};
@@ -719,6 +720,12 @@ int kh_assemble_dev(kh_table* t) {
     wb.max_steps = n;
     wb.headrec = t->headrec.as<uint64_t>();
     wb.hcap = t->headrec.p ? t->hcap : 0u;
+    // the walkers' own head records, found before the walk (KH_DEBUG=no_start_rec: looked up)
+    if (wb.hcap && kp.chain && !kh::debug_flag("no_start_rec") &&
+        (uint64_t)wb.hcap * (1ull << kp.rbits) < 0xFFFFFFFFull) {
+        if ((rc = t->start_rec.ensure((nseg + 1) * 4))) return rc;
+        wb.start_rec = t->start_rec.as<uint32_t>();
+    }
     kh::SegBuffers sb{};
     if (kp.split_bits) {
         // walkers may stop before a splitter k-mer even when none was collected (then the link
@@ -762,6 +769,7 @@ int kh_assemble_dev(kh_table* t) {
         // resolved still says 0 (the walker probes, as without), so the resolve runs on the side
         // stream beside the walk (request-bound beside a latency-bound walker); the table stream
         // waits for it after the walk (the next build rewrites the records).
+        if (attempt == 0 && wb.start_rec) KH_HIP(kh::launch_start_rec(kp, view(t), wb, t->stream));
         bool succ_side = false;
         if (attempt == 0 && wb.hcap && !kh::debug_flag("no_rec_succ") && kh::rec_succ_fits(kp, wb.hcap)) {
             const char* ce = getenv("KH_SUCC_CONC");  // 0: before the walk on the table stream

@@ -88,6 +88,9 @@ struct WalkBuffers {
     // chain head records of the last region build (kh_build.hip region_chains); hcap 0 = none
     const uint64_t* headrec = nullptr;
     uint32_t hcap = 0;
+    // per walker (start, then walked splitter): its own head record's global index + 1, 0 = look
+    // the k-mer up (k_start_rec; null = every walker looks its k-mer up)
+    uint32_t* start_rec = nullptr;
 };
 
 // Persistent per-lane walker (single GPU): every lane walks whole contigs, pulling start k-mers
@@ -98,6 +101,8 @@ hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uin
                            unsigned blocks = 0);
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s);
+// the walkers' own head records (wb.start_rec), before the walk
+hipError_t launch_start_rec(const KParams& p, TableView t, const WalkBuffers& wb, hipStream_t s);
 
 static constexpr uint32_t SEG_NONE = 0xFFFFFFFFu, SEG_AT_SPLIT = 0xFFFFFFFEu;
 
