@@ -121,6 +121,7 @@ struct kh_table {
     uint32_t mw_P = 0, mw_rank = 0;
     bool mw_live = false, mw_stepped = false;
     bool mw_hot = true;        // the shard has remapped regions (the walk reads the bitmap)
+    bool succ_pending = false; // k_rec_succ of the migrating walk still queued on the side stream
     uint64_t rw_n = 0, rw_total = 0;  // migrating walk: local walkers, bound on contig length
     uint64_t starts_cap = 0;                 // start entries the starts buffer holds
     uint64_t splits_cap = 0, splits_w_cap = 0;
@@ -206,6 +207,15 @@ int clean_slots(kh_table* t) {
     if (!t->slots_stale) return KH_OK;
     KH_HIP(hipMemsetAsync(t->slots.p, 0xff, t->cap * (uint64_t)t->kp.W * 8, t->stream));
     t->slots_stale = false;
+    return KH_OK;
+}
+
+// The migrating walk resolves record successors on the side stream beside its rounds: the
+// table's stream waits for it before anything rewrites the records (end of the walk, clear).
+int join_succ(kh_table* t) {
+    if (!t->succ_pending) return KH_OK;
+    KH_HIP(hipStreamWaitEvent(t->stream, t->ev_conv, 0));
+    t->succ_pending = false;
     return KH_OK;
 }
 
@@ -419,6 +429,7 @@ int kh_reserve(kh_table* t, uint64_t n_kmers) {
 int kh_clear(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
     t->slots_stale = true;
     KH_HIP(hipMemsetAsync(t->ctr.p, 0, kh::CT_NUM * 8, t->stream));
     KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
@@ -458,6 +469,7 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
                     (unsigned long long)n, (unsigned long long)t->n_kmers,
                     (unsigned long long)t->n_inserted);
     if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
     int rc;
     const uint64_t nw = (n + 63) / 64;
     const bool split = t->kp.split_bits > 0;
@@ -658,6 +670,7 @@ int kh_set_starts(kh_table* t, const uint8_t* recs, uint64_t n) {
 int kh_assemble_dev(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
     if (int rc = clean_slots(t)) return rc;
     int rc;
     // The start count decides buffer sizes and the grid (the reference also knows
@@ -774,7 +787,7 @@ int kh_assemble_dev(kh_table* t) {
         if (attempt == 0 && wb.hcap && !kh::debug_flag("no_rec_succ") && kh::rec_succ_fits(kp, wb.hcap)) {
             const char* ce = getenv("KH_SUCC_CONC");  // 0: before the walk on the table stream
             const char* be = getenv("KH_SUCC_BLOCKS");
-            const bool conc = !ce || atoi(ce) != 0;
+            const bool conc = (!ce || atoi(ce) != 0) && kh::rec_succ_side(kp);
             // beside the walk: 1024 blocks (C3 walk + resolve 1.28 ms; the full 8192-block grid
             // 1.32-1.34, 256 blocks 1.85: the resolve then lags the walkers; no resolve 1.46)
             const unsigned blocks = be ? (unsigned)atoi(be) : (conc ? 1024u : 0u);
@@ -1114,6 +1127,7 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
                     (unsigned long long)m, (unsigned long long)t->n_kmers,
                     (unsigned long long)t->n_inserted);
     if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
     t->split_ok = false;  // routed words carry no splitter marks: walks on this table use none
     const bool part = use_part_build(t, m);
     const bool coll = part && mseg_enabled(t) && t->words_split;
@@ -1151,6 +1165,7 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (m && !words) return fail(KH_ERR_ARG, "null words");
     if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
     if (!t->staging) {
         if (total_hint < m) total_hint = m;
         if (t->n_inserted + total_hint > t->n_kmers)
@@ -1272,6 +1287,7 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     if (nranks < 1 || nranks > kh::MAX_RANKS || rank < 0 || rank >= nranks)
         return fail(KH_ERR_ARG, "bad rank %d of %d", rank, nranks);
     if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
     if (int rc = clean_slots(t)) return rc;
     int rc;
     unsigned long long cv[kh::CT_NUM];  // one read of the counters (starts, hot regions, splitters)
@@ -1320,10 +1336,30 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     KH_HIP(hipMemsetAsync(t->mw_misc.as<unsigned long long>() + 2, 0, 8, t->stream));
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
     t->wk_timed = false;
-    KH_HIP(kh::launch_mw_init(t->kp, t->starts.as<uint64_t>(), ns, (uint32_t)rank, t->mw_init.as<uint64_t>(),
-                              t->stream));
+    // chain records: every walker whose k-mer heads a record starts from it (k_mw_init), and the
+    // records' successor runs are resolved beside the first round (k_rec_succ, as on one GPU)
+    kh::KParams ikp = t->kp;
+    if (!t->mw_hot) ikp.hot = nullptr;
+    const uint32_t hcap = (t->headrec.p && t->kp.chain && !kh::debug_flag("no_start_rec") &&
+                           (uint64_t)t->hcap * (1ull << t->kp.rbits) < 0xFFFFFFFFull)
+                              ? t->hcap
+                              : 0u;
+    KH_HIP(kh::launch_mw_init(ikp, view(t), hcap, t->starts.as<uint64_t>(), ns, (uint32_t)rank,
+                              t->mw_init.as<uint64_t>(), t->stream));
+    if (t->headrec.p && t->hcap && !kh::debug_flag("no_rec_succ") && kh::rec_succ_fits(ikp, t->hcap)) {
+        hipStream_t rs = t->stream;
+        if (kh::rec_succ_side(ikp) && t->side) {
+            KH_HIP(hipEventRecord(t->ev_side, t->stream));
+            KH_HIP(hipStreamWaitEvent(t->side, t->ev_side, 0));
+            rs = t->side;
+            t->succ_pending = true;
+        }
+        KH_HIP(kh::launch_rec_succ(ikp, view(t), t->headrec.as<uint64_t>(), t->hcap, rs,
+                                   t->succ_pending ? 1024u : 0u));
+        if (t->succ_pending) KH_HIP(hipEventRecord(t->ev_conv, t->side));
+    }
     if (t->ms_on) {
-        KH_HIP(kh::launch_mw_init(t->kp, t->splits.as<uint64_t>(), nsp, (uint32_t)rank,
+        KH_HIP(kh::launch_mw_init(ikp, view(t), hcap, t->splits.as<uint64_t>(), nsp, (uint32_t)rank,
                                   t->mw_init.as<uint64_t>() + ns * kh::MSG_WORDS, t->stream, ns));
         KH_HIP(kh::launch_mseg_init(ns, nseg, (uint32_t)rank, mseg_state(t), t->stream));
         KH_HIP(kh::launch_mseg_stab(t->kp, t->splits.as<uint64_t>(), nsp, t->ms_stab.as<uint64_t>(),
@@ -1522,6 +1558,7 @@ int kh_mwalk_text_count(kh_table* t, uint64_t* n_records) {
 
 int kh_mwalk_text_dev(kh_table* t, void* out, void* counts) {
     if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (int rc = join_succ(t)) return rc;
     if (int rc = mw_store_count(t)) return rc;
     if (!counts || (t->mw_store_n && !out)) return fail(KH_ERR_ARG, "null buffer");
     if (int rc = set_device(t)) return rc;

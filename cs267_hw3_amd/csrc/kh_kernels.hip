@@ -571,7 +571,10 @@ __global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t
             uint64_t w0 = 0;
             if (f <= 3u && probe<W>(key_next(slot_key(v.x, v.y, p), f, p), p, slots, cap, w0))
                 succ = slot_hidx(w0, p);
-            rec[0] = (v.x & ((1ull << sh) - 1)) | ((uint64_t)succ << sh);
+            // one 64-bit store; walkers may read the record concurrently (side stream), which
+            // is only allowed when the successor field lies in the upper dword (rec_succ_side)
+            __hip_atomic_store(rec, (v.x & ((1ull << sh) - 1)) | ((uint64_t)succ << sh), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -622,6 +625,12 @@ hipError_t launch_start_rec(const KParams& p, TableView t, const WalkBuffers& wb
 bool rec_succ_fits(const KParams& p, uint32_t hcap) {
     return p.chain && hcap && rec_succ_shift(p) < 64 && (uint64_t)hcap + 1 < (1ull << (64 - rec_succ_shift(p)));
 }
+
+// The resolve may run beside walkers that read records with 16-B vector loads only when the
+// successor field lies entirely in the upper dword of word 0: a load that sees half of the
+// resolve's 64-bit store then still reads either 0 or the whole index (the lower dword is
+// rewritten with its own value). Below that (W=2 at k <= 40) it runs before the walk.
+bool rec_succ_side(const KParams& p) { return rec_succ_shift(p) >= 32; }
 
 hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uint32_t hcap, hipStream_t s,
                            unsigned blocks) {

@@ -97,6 +97,7 @@ struct WalkBuffers {
 // from a wave-batched work queue.
 // head records' successor runs (before a walk; KH_REC_SUCC=0 skips it: the walker then probes)
 bool rec_succ_fits(const KParams& p, uint32_t hcap);
+bool rec_succ_side(const KParams& p);
 hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uint32_t hcap, hipStream_t s,
                            unsigned blocks = 0);
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
@@ -159,8 +160,9 @@ struct MWalkRound {
     const uint64_t* headrec = nullptr;  // chain head records of this shard's build (hcap 0 = none)
     uint32_t hcap = 0;
 };
-hipError_t launch_mw_init(const KParams& p, const uint64_t* starts, uint64_t n, uint32_t rank, uint64_t* msgs,
-                          hipStream_t s, uint64_t idx0 = 0);
+// initial messages; hcap > 0: a walker whose own k-mer heads a chain record starts by reading it
+hipError_t launch_mw_init(const KParams& p, TableView t, uint32_t hcap, const uint64_t* starts, uint64_t n,
+                          uint32_t rank, uint64_t* msgs, hipStream_t s, uint64_t idx0 = 0);
 
 // ---- splitter segments of the migrating walk (kh_mseg.hip) ----------------------------------
 struct MSegState {       // per local segment: starts [0, ns), splitter segments [ns, ns + nsp)

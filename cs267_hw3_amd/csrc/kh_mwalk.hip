@@ -16,19 +16,23 @@
 
 namespace kh {
 
-static constexpr uint32_t MW_LOOKUP = 0xFF;  // message state: key must be looked up by its owner
-static constexpr uint8_t MW_NONE = 0xFF;     // destination: walker finished this round
+static constexpr uint32_t MW_LOOKUP = 0xFF;   // message state: key must be looked up by its owner
+static constexpr uint32_t MW_READREC = 0xFE;  // message state: read head record (m[4] >> 32) - 1 of this
+                                              // rank (its run starts at the key; only sent to self)
+static constexpr uint8_t MW_NONE = 0xFF;      // destination: walker finished this round
 
 __device__ __forceinline__ uint64_t rec_tag(uint32_t origin, bool fin, uint64_t word_no, uint32_t idx) {
     return ((uint64_t)origin << 56) | ((uint64_t)fin << 55) | (word_no << 31) | idx;
 }
 
-// One lane per input message (static stride, no work-queue atomics), one table probe per loop
-// iteration, like k_walk. A lane's run ends when the walker finishes, migrates, or has flushed
+// One lane per input message (static stride, no work-queue atomics), one load per lane per loop
+// iteration, like k_walk_q. A lane's run ends when the walker finishes, migrates, or has flushed
 // MW_RUN_WORDS words this round (it then re-sends itself, bounding the per-input text region).
 // Chains (kh_build.hip): a probed k-mer whose slot names a head record is crossed in one step —
 // the record's tail key carries the run's bases. A chain shares one minimizer, hence one owner,
-// so it never crosses ranks.
+// so it never crosses ranks. As on one GPU (k_walk_q), a walker starts from its own record when
+// k_mw_init found one, and after a run follows the record's successor (k_rec_succ) without probing
+// the next run's head k-mer: one dependent request per run.
 template <int W, int KT>
 __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
                                                   MWalkRound mw, unsigned long long* stats) {
@@ -56,7 +60,19 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
     Key k{0, 0};
     uint64_t s = 0, buf = 0;
     uint32_t steps = 0, idx = 0, origin = 0, st = 0, nrec = 0, nwords = 0;
+    uint32_t nsucc = 0;  // the last record's successor run (head-record index + 1 in its region)
     uint64_t* rec = nullptr;
+    auto finish = [&](uint64_t jj) {
+        if (steps & 31) {
+            rec[2 * nrec] = rec_tag(origin, false, steps >> 5, idx);
+            rec[2 * nrec + 1] = buf;
+            ++nrec;
+        }
+        rec[2 * nrec] = rec_tag(origin, true, 0, idx);
+        rec[2 * nrec + 1] = steps;
+        ++nrec;
+        mw.dst[jj] = MW_NONE;
+    };
     while (true) {
         if (!active && j < mw.n_in) {
             const uint64_t* m = mw.in + j * MSG_WORDS;
@@ -65,14 +81,18 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             buf = m[2];
             steps = (uint32_t)m[3];
             idx = (uint32_t)(m[3] >> 32);
-            origin = (uint32_t)m[4] & 0xFFu;
-            st = (uint32_t)(m[4] >> 8) & 0xFFu;
+            const uint64_t m4 = m[4];
+            origin = (uint32_t)m4 & 0xFFu;
+            st = (uint32_t)(m4 >> 8) & 0xFFu;
             rec = mw.stage + j * (MW_REC_SLOTS * 2);
             nrec = 0;
             nwords = 0;
+            nsucc = 0;
             active = true;
-            probing = st == MW_LOOKUP;
-            if (probing) {
+            probing = st == MW_LOOKUP || st == MW_READREC;
+            if (st == MW_READREC) {
+                s = WQ_REC | ((m4 >> 32) - 1);
+            } else if (probing) {
                 const Place pl = place(k, p);
                 reg = pl.r;
                 s = home_of(pl, cap, p);
@@ -88,15 +108,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                 atomicAdd(&stats[ST_CYCLE], 1ull);
                 fin = true;
             } else {
-                buf |= (uint64_t)st << (2 * (steps & 31));
-                ++steps;
-                if ((steps & 31) == 0) {
-                    rec[2 * nrec] = rec_tag(origin, false, (steps >> 5) - 1, idx);
-                    rec[2 * nrec + 1] = buf;
-                    ++nrec;
-                    ++nwords;
-                    buf = 0;
-                }
+                put(st, 1, buf, steps, nrec, nwords, rec, origin, idx);
                 k = key_next(k, st, p);
                 const uint64_t hk = key_hash32(k);
                 if (mw.split_bits && (hk & ((1ull << mw.split_bits) - 1)) == 0) {
@@ -115,35 +127,33 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                                        : (mw.P == 1 ? 0u
                                                     : (p.owner_mode == 1 ? owner_key(k, p, mw.P)
                                                                          : owner_of_mini(mv, mw.P)));
+                const Place pl = place_w(mv, k, p);
                 if (fin) {
                     // finished below (length record, no message)
                 } else if (q != mw.rank || nwords >= MW_RUN_WORDS) {
+                    // to the owner (or to itself, bounding this round's text): a successor record
+                    // is only meaningful on this rank
                     uint64_t* o = mw.tmp + j * MSG_WORDS;
                     o[0] = k.hi;
                     o[1] = k.lo;
                     o[2] = buf;
                     o[3] = ((uint64_t)idx << 32) | steps;
-                    o[4] = origin | (MW_LOOKUP << 8);
+                    o[4] = (nsucc && q == mw.rank)
+                               ? origin | ((uint64_t)MW_READREC << 8) |
+                                     (((uint64_t)pl.r * mw.hcap + nsucc) << 32)
+                               : origin | ((uint64_t)MW_LOOKUP << 8);
                     mw.dst[j] = (uint8_t)q;
                     ovf = true;
                 } else {
                     probing = true;
-                    const Place pl = place_w(mv, k, p);
                     reg = pl.r;
-                    s = home_of(pl, cap, p);
+                    // the record names the run that starts at k (k_rec_succ): read it, no probe
+                    s = (nsucc && nwords + 3 <= MW_RUN_WORDS) ? WQ_REC | ((uint64_t)reg * mw.hcap + nsucc - 1)
+                                                              : home_of(pl, cap, p);
                 }
+                nsucc = 0;
             }
-            if (fin) {
-                if (steps & 31) {
-                    rec[2 * nrec] = rec_tag(origin, false, steps >> 5, idx);
-                    rec[2 * nrec + 1] = buf;
-                    ++nrec;
-                }
-                rec[2 * nrec] = rec_tag(origin, true, 0, idx);
-                rec[2 * nrec + 1] = steps;
-                ++nrec;
-                mw.dst[j] = MW_NONE;
-            }
+            if (fin) finish(j);
             if (fin || ovf) {
                 mw.nrec[j] = (uint8_t)nrec;
                 active = false;
@@ -151,7 +161,8 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             }
         }
         // quad-transposed block probe (as k_walk_q): lane q of a quad loads slot q of each member's
-        // 64-B block (one request per block), the members learn their first hit / EMPTY by ballot
+        // 64-B block (one request per block), the members learn their first hit / EMPTY by ballot;
+        // a record read loads the same 16 B in all 4 lanes (one request)
         const uint64_t sp = (active && probing) ? s : WQ_IDLE;
         uint64_t sj[4], w0[4], w1[4];
         sj[0] = qbcast64<0>(sp);
@@ -162,8 +173,15 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
         for (int jj = 0; jj < 4; ++jj) {
             w0[jj] = EMPTY;
             w1[jj] = 0;
-            const uint64_t my = (sj[jj] & ~3ull) + q4;
-            if (sj[jj] != WQ_IDLE && my < cap) load_slot_nt<W>(slots, my, w0[jj], w1[jj]);
+            if (sj[jj] == WQ_IDLE) continue;
+            if (sj[jj] & WQ_REC) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(mw.headrec + (sj[jj] & ~WQ_REC) * 2);
+                w0[jj] = v.x;
+                w1[jj] = v.y;
+            } else {
+                const uint64_t my = (sj[jj] & ~3ull) + q4;
+                if (my < cap) load_slot_nt<W>(slots, my, w0[jj], w1[jj]);
+            }
         }
         uint64_t kh_[4], kl_[4];
         kh_[0] = qbcast64<0>(k.hi);
@@ -175,10 +193,12 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
         kl_[2] = qbcast64<2>(k.lo);
         kl_[3] = qbcast64<3>(k.lo);
         uint32_t myfh = 4, myfe = 4, myext = 0;
+        uint64_t r0 = 0, r1 = 0;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
             const uint64_t my = (sj[jj] & ~3ull) + q4;
-            const bool valid = sj[jj] != WQ_IDLE && my >= sj[jj] && my < cap;
+            const bool probe_j = sj[jj] != WQ_IDLE && !(sj[jj] & WQ_REC);
+            const bool valid = probe_j && my >= sj[jj] && my < cap;
             const bool empty = w0[jj] == EMPTY;
             const bool hit = !empty & (slot_keybits(w0[jj], p) == ((W == 1) ? kl_[jj] : kh_[jj])) &
                              ((W == 1) | (w1[jj] == kl_[jj]));
@@ -193,43 +213,40 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                 myfh = fh;
                 myfe = fe;
                 myext = ext;
+                r0 = w0[jj];
+                r1 = w1[jj];
             }
         }
         if (active && probing) {
-            if (myfh < myfe) {
-                const uint32_t hidx = myext >> 7;
-                if (hidx && nwords + 3 <= MW_RUN_WORDS) {  // the run's <= 2 words fit this round
-                    const ulonglong2 rv =
-                        *reinterpret_cast<const ulonglong2*>(mw.headrec + ((uint64_t)reg * mw.hcap + hidx - 1) * 2);
-                    k = slot_key(rv.x, rv.y, p);
-                    st = ext_fwd(slot_ext(rv.x));
-                    uint32_t n = rec_links(rv.x, p);  // links: the last n bases of the tail key
-                    while (n) {
-                        const uint32_t room = 32u - (steps & 31u), m = n < room ? n : room;
-                        const int sh = 2 * (int)(n - m);  // bits [sh, sh + 2m) of V, oldest base first
-                        const uint64_t x = sh < 62 ? (k.lo >> sh) | (k.hi << (62 - sh)) : k.hi >> (sh - 62);
-                        const uint64_t v = m >= 32 ? x : x & ((1ull << (2 * m)) - 1);
-                        const uint64_t r = ((uint64_t)__builtin_bitreverse32((uint32_t)v) << 32) |
-                                           __builtin_bitreverse32((uint32_t)(v >> 32));
-                        const uint64_t rev = ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1);
-                        put(rev >> (64 - 2 * m), m, buf, steps, nrec, nwords, rec, origin, idx);
-                        n -= m;
-                    }
-                } else {
-                    st = ext_fwd(myext & 63u);
+            if (s & WQ_REC) {
+                // head record: jump to the run's tail, appending the bases of its links
+                k = slot_key(r0, r1, p);
+                st = ext_fwd(slot_ext(r0));
+                nsucc = rec_succ(r0, p);
+                uint32_t n = rec_links(r0, p);  // links: the last n bases of the tail key
+                while (n) {
+                    const uint32_t room = 32u - (steps & 31u), m = n < room ? n : room;
+                    const int sh = 2 * (int)(n - m);  // bits [sh, sh + 2m) of V, oldest base first
+                    const uint64_t x = sh < 62 ? (k.lo >> sh) | (k.hi << (62 - sh)) : k.hi >> (sh - 62);
+                    const uint64_t v = m >= 32 ? x : x & ((1ull << (2 * m)) - 1);
+                    const uint64_t r = ((uint64_t)__builtin_bitreverse32((uint32_t)v) << 32) |
+                                       __builtin_bitreverse32((uint32_t)(v >> 32));
+                    const uint64_t rev = ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1);
+                    put(rev >> (64 - 2 * m), m, buf, steps, nrec, nwords, rec, origin, idx);
+                    n -= m;
                 }
                 probing = false;
+            } else if (myfh < myfe) {
+                const uint32_t hidx = myext >> 7;
+                if (hidx && nwords + 3 <= MW_RUN_WORDS) {  // the run's <= 2 words fit this round
+                    s = WQ_REC | ((uint64_t)reg * mw.hcap + hidx - 1);
+                } else {
+                    st = ext_fwd(myext & 63u);
+                    probing = false;
+                }
             } else if (myfe < 4u) {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
                 atomicAdd(&stats[ST_MISSING], 1ull);
-                if (steps & 31) {
-                    rec[2 * nrec] = rec_tag(origin, false, steps >> 5, idx);
-                    rec[2 * nrec + 1] = buf;
-                    ++nrec;
-                }
-                rec[2 * nrec] = rec_tag(origin, true, 0, idx);
-                rec[2 * nrec + 1] = steps;
-                ++nrec;
-                mw.dst[j] = MW_NONE;
+                finish(j);
                 mw.nrec[j] = (uint8_t)nrec;
                 active = false;
                 j += stride;
@@ -241,20 +258,44 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
     }
 }
 
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p, const uint64_t* starts, uint64_t n, uint32_t rank,
+// Initial messages: one per start (or splitter) k-mer, state = its forward extension; with chains,
+// a walker whose k-mer's slot carries a head record whose run begins with the walker's own
+// extension (the walker's rule for a start, kmer_hash.cpp:42-44; as k_start_rec) starts by reading
+// that record instead (state MW_READREC).
+template <int W, int KT>
+__global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
+                                                   uint32_t hcap, const uint64_t* starts, uint64_t n, uint32_t rank,
                                                    uint64_t* msgs, uint64_t idx0) {
+    const KParams p = specialize<KT>(p_in);
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t w0 = starts[i * W];
-        const uint64_t w1 = (W == 2) ? starts[i * W + 1] : 0;
-        const Key k = slot_key(w0, w1, p);
-        const uint32_t f = ext_fwd(slot_ext(w0));
+        const uint64_t x0 = starts[i * W];
+        const uint64_t x1 = (W == 2) ? starts[i * W + 1] : 0;
+        const Key k = slot_key(x0, x1, p);
+        const uint32_t f = ext_fwd(slot_ext(x0));
+        uint64_t rix = 0;
+        if (hcap && f <= 3u) {
+            const Place pl = place(k, p);
+            uint64_t sl = home_of(pl, cap, p);
+            const uint64_t want0 = (W == 1) ? k.lo : k.hi;
+            for (uint64_t probes = 0; probes < cap; ++probes) {
+                uint64_t w0, w1;
+                load_slot<W>(slots, sl, w0, w1);
+                if (w0 == EMPTY) break;
+                if (slot_keybits(w0, p) == want0 && (W == 1 || w1 == k.lo)) {
+                    const uint32_t hidx = slot_hidx(w0, p);
+                    if (hidx && ext_fwd(slot_ext(w0)) == f) rix = (uint64_t)pl.r * hcap + hidx;
+                    break;
+                }
+                sl = (sl + 1 == cap) ? 0 : sl + 1;
+            }
+        }
         uint64_t* m = msgs + i * MSG_WORDS;
         m[0] = k.hi;
         m[1] = k.lo;
         m[2] = 0;
         m[3] = (idx0 + i) << 32;
-        m[4] = rank | ((uint64_t)(f > 4 ? EXT_BAD : f) << 8);
+        m[4] = rix ? rank | ((uint64_t)MW_READREC << 8) | (rix << 32)
+                   : rank | ((uint64_t)(f > 4 ? EXT_BAD : f) << 8);
     }
 }
 
@@ -340,13 +381,19 @@ static unsigned grid_for(uint64_t n, uint64_t cap_blocks) {
     return (unsigned)(g == 0 ? 1 : (g < cap_blocks ? g : cap_blocks));
 }
 
-hipError_t launch_mw_init(const KParams& p, const uint64_t* starts, uint64_t n, uint32_t rank, uint64_t* msgs,
-                          hipStream_t s, uint64_t idx0) {
+hipError_t launch_mw_init(const KParams& p, TableView t, uint32_t hcap, const uint64_t* starts, uint64_t n,
+                          uint32_t rank, uint64_t* msgs, hipStream_t s, uint64_t idx0) {
     if (n == 0) return hipSuccess;
+    if (!p.chain) hcap = 0;
+    const unsigned g = grid_for(n, 8192);
     if (p.W == 1)
-        k_mw_init<1><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs, idx0);
+        with_kt<1>(p.K, [&](auto kt) {
+            k_mw_init<1, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, hcap, starts, n, rank, msgs, idx0);
+        });
     else
-        k_mw_init<2><<<grid_for(n, 8192), BLOCK, 0, s>>>(p, starts, n, rank, msgs, idx0);
+        with_kt<2>(p.K, [&](auto kt) {
+            k_mw_init<2, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, hcap, starts, n, rank, msgs, idx0);
+        });
     return hipGetLastError();
 }
 

@@ -244,6 +244,13 @@ class GpuShard:
         already have the room (kh_reserve fails otherwise: the caller's ranks agree on it)."""
         check(self.L.kh_reserve(self.h, int(self.inserted + m)))
 
+    def insert_records(self, recs):
+        """One rank: the route is the identity, so the block's records go straight through the
+        single-GPU records pass (kh_insert_dev: start k-mers and splitters in the same pass)."""
+        n = recs.shape[0]
+        check(self.L.kh_insert_dev(self.h, self._p(recs), n))
+        self.inserted += n
+
     def insert_words(self, words, m):
         check(self.L.kh_insert_words_dev(self.h, self._p(words), m))
         self.inserted += m
@@ -360,8 +367,10 @@ class DistributedKmerHashMap:
     # peer (tools/dbg_a2a.py: half the elements wrong at 2.0 and 3.2 GiB, exact at 1 GiB), so no
     # single call moves more than A2A_CHUNK_BYTES per peer.
     A2A_CHUNK_BYTES = int(os.environ.get("KH_A2A_CHUNK_MB", "512")) << 20
-    # one rank: exchanges are skipped (KH_DIST_SELF_EXCHANGE=1 runs them anyway, for tests)
+    # one rank: exchanges are skipped (KH_DIST_SELF_EXCHANGE=1 runs them anyway, for tests), and the
+    # records go straight into the records pass (KH_DIST_ROUTE_ONE_RANK=1 routes them anyway)
     SELF_EXCHANGE = os.environ.get("KH_DIST_SELF_EXCHANGE") == "1"
+    ROUTE_ONE_RANK = os.environ.get("KH_DIST_ROUTE_ONE_RANK") == "1"
 
     def _exchange_counts(self, counts, elems_per_item=1):
         """counts: [P+1] int64 (per-destination, total) -> (send_splits, recv_splits, totals,
@@ -470,6 +479,12 @@ class DistributedKmerHashMap:
         sh, P, W = self.shard, self.P, self.shard.W
         n = recs.shape[0]
         exchange = P > 1 or self.SELF_EXCHANGE
+        if not exchange and not self.ROUTE_ONE_RANK and hasattr(sh, "insert_records"):
+            # one rank: every key is this shard's and nothing moves (as the count exchanges are
+            # skipped): the records pass partitions them itself, no owner route + word re-partition
+            sh.reserve(n)
+            sh.insert_records(recs)
+            return n
         nch = 1
         if exchange and self.INSERT_CHUNKS > 1 and n >= self.PIPELINE_MIN:
             # per-peer bytes of a chunk <= chunk records * W * 8: keep every transfer under the

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -59,6 +60,7 @@ public:
     }
     int64_t* words(size_t n) { return static_cast<int64_t*>(ensure(n * 8)); }
     void* get() const { return p_; }
+    size_t capacity() const { return cap_; }
     void release() {
         if (p_) (void)hipFree(p_);
         p_ = nullptr;
@@ -181,6 +183,15 @@ public:
     uint64_t insert_all_dev(const void* dev_recs, uint64_t n) {
         hip_check(hipSetDevice(device_), "hipSetDevice");
         const uint64_t P = (uint64_t)P_;
+        if (P == 1 && !route_one_rank()) {
+            // one rank: every key is this shard's and nothing moves, so the records go straight
+            // into the single-GPU records pass (start k-mers and splitters in the same pass)
+            const int rc = kh_reserve(t_, inserted_ + n);
+            if (rc != KH_OK) abi_check(rc);
+            abi_check(kh_insert_dev(t_, dev_recs, n));
+            inserted_ += n;
+            return done_insert(n);
+        }
         uint64_t nch = 1;
         if (P > 1 && n >= kPipelineMin) {
             // per-peer bytes of a chunk <= chunk records * W * 8: every message stays under the
@@ -192,12 +203,26 @@ public:
         // chunk starts at multiples of 16 records: every chunk's records stay 16-B aligned
         for (uint64_t c = 0; c < nch; ++c) bounds[c] = std::min<uint64_t>(n, (n * c / nch) & ~15ull);
         bounds[nch] = n;
-        int64_t* words = words_.words(std::max<uint64_t>(n, 1) * W_);
+        // one-pass route (kh_route_starts_win_dev): chunk c's records sorted into P owner windows of
+        // (c1 - c0) words each at P * c0 words, while the P windows of the block fit a third of the
+        // free device memory; else the two-pass route packs each chunk back to back
+        size_t free_b = 0, total_b = 0;
+        hip_check(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+        const uint64_t win_bytes = P * std::max<uint64_t>(n, 1) * W_ * 8;
+        const bool windows = R_ <= 15 && win_bytes <= words_.capacity() + free_b / (3 * ranks_per_device());
+        int64_t* words = windows ? words_.words(P * std::max<uint64_t>(n, 1) * W_)
+                                 : words_.words(std::max<uint64_t>(n, 1) * W_);
         int64_t* cnt = counts_.words(nch * (P + 1));
         const uint8_t* recs = static_cast<const uint8_t*>(dev_recs);
-        for (uint64_t c = 0; c < nch; ++c)
-            abi_check(kh_route_starts_dev(t_, recs + bounds[c] * R_, bounds[c + 1] - bounds[c], P_,
-                                          words + bounds[c] * W_, cnt + c * (P + 1)));
+        auto win_of = [&](uint64_t c) { return std::max<uint64_t>(bounds[c + 1] - bounds[c], 1); };
+        for (uint64_t c = 0; c < nch; ++c) {
+            if (windows)
+                abi_check(kh_route_starts_win_dev(t_, recs + bounds[c] * R_, bounds[c + 1] - bounds[c], P_,
+                                                  words + P * bounds[c] * W_, win_of(c), cnt + c * (P + 1)));
+            else
+                abi_check(kh_route_starts_dev(t_, recs + bounds[c] * R_, bounds[c + 1] - bounds[c], P_,
+                                              words + bounds[c] * W_, cnt + c * (P + 1)));
+        }
         // every rank learns the whole [src][chunk][dst] count matrix in one all-gather
         std::vector<uint64_t> mine(nch * (P + 1)), all(P * nch * (P + 1));
         hip_check(hipMemcpyAsync(mine.data(), cnt, mine.size() * 8, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync");
@@ -217,7 +242,7 @@ public:
         const std::string err = rc == KH_OK ? "" : kh_last_error();
         agree(rc != KH_OK, err);
         inserted_ += m;
-        if (P == 1) {  // one rank: the routed words are this shard's
+        if (P == 1) {  // one rank routed anyway (KH_DIST_ROUTE_ONE_RANK=1; one chunk): the words are this shard's
             abi_check(kh_insert_words_dev(t_, words, m));
             return done_insert(m);
         }
@@ -227,7 +252,7 @@ public:
             uint64_t so = bounds[c] * W_, ro = pos * W_;
             for (uint64_t q = 0; q < P; ++q) {
                 sc[q] = M(rank_, c, q) * W_;
-                sd[q] = so;
+                sd[q] = windows ? (P * bounds[c] + q * win_of(c)) * W_ : so;  // owner window / packed
                 so += sc[q];
                 rcn[q] = M(q, c, rank_) * W_;
                 rd[q] = ro;
@@ -363,10 +388,19 @@ public:
         comm_.barrier();
     }
 
+    // processes sharing one device (KH_DIST_DEVICE rehearsals) split its free memory
+    void set_ranks_per_device(int n) { ranks_per_device_ = n > 0 ? n : 1; }
+    uint64_t ranks_per_device() const { return (uint64_t)ranks_per_device_; }
+
     static constexpr uint64_t kInsertChunks = 4;
     static constexpr uint64_t kPipelineMin = 1ull << 22;  // records per rank below: one transfer
 
 private:
+    static bool route_one_rank() {
+        const char* e = getenv("KH_DIST_ROUTE_ONE_RANK");
+        return e && !strcmp(e, "1");
+    }
+
     // hash_map.hpp:79: insert_all ends in a barrier, so a find() right after it sees every
     // rank's keys (the shard's build has finished before any rank leaves)
     uint64_t done_insert(uint64_t m) {
@@ -550,6 +584,7 @@ private:
     uint64_t W_ = 2, R_ = 15;
     int rounds_ = 0, jump_rounds_ = 0;
     uint64_t inserted_ = 0;  // k-mers this shard holds since the last clear
+    int ranks_per_device_ = 1;
     std::mutex m_;
     std::vector<hipEvent_t> events_;
     DevBuf words_, recv_, counts_, a_, b_, tout_, trecv_, lout_, lin_, qout_, qin_, rep_, rin_, sout_, sin_, recs_;

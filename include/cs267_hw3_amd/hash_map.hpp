@@ -149,6 +149,16 @@ private:
         // expected share of the k-mers (size_ / 2 in all); the shard grows to what it receives
         const uint64_t hint = size_ / 2 / (uint64_t)world_ + 1024;
         shard_.reset(new kh::ShardedTable(KMER_LEN, hint, comm, device, peer_group));
+        // ranks driven by this process on the same device share its free memory
+        int same = 1;
+        const auto& ctx = kh::rank_contexts();
+        if ((int)ctx.size() == world_) {
+            same = 0;
+            for (const auto& c : ctx) same += c.device == device;
+        } else if (peer_group) {
+            same = world_;
+        }
+        shard_->set_ranks_per_device(same);
     }
     size_t size_;
     int rank_, world_;

@@ -173,7 +173,7 @@ def test_generated_vs_oracle(k, n, lmin, lmax, single, seed):
 
 
 @pytest.mark.parametrize("succ", ["side", "inline", "off"])
-@pytest.mark.parametrize("k", [19, 51])
+@pytest.mark.parametrize("k", [19, 31, 40, 51])
 def test_record_successors(monkeypatch, k, succ):
     """Head records name the record of the run after their tail (k_rec_succ): resolved beside the
     walk (records read before their successor is resolved still say 0), before it, or not at all;
