@@ -227,19 +227,57 @@ __device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, in
 }
 
 // ---- build ------------------------------------------------------------------------------------
+// The region slice in LDS. W=2 slots are stored as two arrays (word 0 of slot i at w[i], word 1
+// at w[sm + i], sm = the block's slice capacity) rather than 16-B pairs: the random 8-B CAS, probe
+// reads and atomicOr of the build touch one word of a slot, and with 16-B interleaving those
+// words sit only in every other bank pair (a 32-lane group of ds_read_b64 spread over 16 bank pairs
+// instead of 32). KH_LDS_SPLIT=0 compiles the interleaved layout (A/B).
+#ifndef KH_LDS_SPLIT
+#define KH_LDS_SPLIT 1
+#endif
+template <int W>
+struct Slice {
+    unsigned long long* w;
+    uint32_t sm;
+    static constexpr bool SPLIT = W == 2 && KH_LDS_SPLIT;
+    __device__ __forceinline__ unsigned long long* p0(uint32_t i) const { return w + (SPLIT ? i : W * i); }
+    __device__ __forceinline__ unsigned long long* p1(uint32_t i) const { return w + (SPLIT ? sm + i : W * i + 1); }
+    __device__ __forceinline__ uint64_t w0(uint32_t i) const { return *p0(i); }
+    __device__ __forceinline__ uint64_t w1(uint32_t i) const { return W == 2 ? *p1(i) : 0ull; }
+    // both words (one 16-B LDS read when interleaved)
+    __device__ __forceinline__ void get(uint32_t i, uint64_t& a, uint64_t& b) const {
+        if (W == 2 && !SPLIT) {
+            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(w)[i];
+            a = v.x;
+            b = v.y;
+        } else {
+            a = *p0(i);
+            b = W == 2 ? *p1(i) : 0ull;
+        }
+    }
+    __device__ __forceinline__ void put(uint32_t i, uint64_t a, uint64_t b) const {
+        if (W == 2 && !SPLIT) {
+            reinterpret_cast<ulonglong2*>(w)[i] = make_ulonglong2(a, b);
+        } else {
+            *p0(i) = a;
+            if (W == 2) *p1(i) = b;
+        }
+    }
+};
+
 // LDS insert with linear probing inside the slice: the slot (>= 0), LDS_DUP (key present) or
 // LDS_OUT (the run left the slice).
 static constexpr int LDS_DUP = -1, LDS_OUT = -2;
 template <int W>
-__device__ __forceinline__ int lds_insert(const KParams& p, unsigned long long* lt, uint32_t S, uint64_t loc,
+__device__ __forceinline__ int lds_insert(const KParams& p, const Slice<W>& lt, uint32_t S, uint64_t loc,
                                           uint64_t w0, uint64_t w1, unsigned long long* stats) {
     const uint64_t want0 = slot_keybits(w0, p);
     uint32_t spins = 0;
     while (loc < S) {
-        const unsigned long long old = atomicCAS(&lt[W * loc], (unsigned long long)EMPTY, w0);
+        const unsigned long long old = atomicCAS(lt.p0((uint32_t)loc), (unsigned long long)EMPTY, w0);
         if (old == EMPTY) {
             if (W == 2)
-                __hip_atomic_store(&lt[2 * loc + 1], (unsigned long long)w1, __ATOMIC_RELAXED,
+                __hip_atomic_store(lt.p1((uint32_t)loc), (unsigned long long)w1, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             return (int)loc;
         }
@@ -249,7 +287,7 @@ __device__ __forceinline__ int lds_insert(const KParams& p, unsigned long long* 
                 return LDS_DUP;
             }
             const unsigned long long o1 =
-                __hip_atomic_load(&lt[2 * loc + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_load(lt.p1((uint32_t)loc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (o1 == EMPTY) {  // the claiming lane has not stored word1 yet: retry this slot
                 if (++spins > (1u << 24)) {
                     atomicAdd(&stats[ST_SPIN], 1ull);
@@ -276,7 +314,7 @@ __device__ __forceinline__ int lds_insert(const KParams& p, unsigned long long* 
 #define KH_LDS_BLOCK 1
 #endif
 template <int W>
-__device__ __forceinline__ int lds_insert_blk(const KParams& p, unsigned long long* lt, uint32_t S, uint32_t loc,
+__device__ __forceinline__ int lds_insert_blk(const KParams& p, const Slice<W>& lt, uint32_t S, uint32_t loc,
                                               uint64_t w0, uint64_t w1, unsigned long long* stats) {
     const uint64_t want0 = slot_keybits(w0, p);
     uint32_t spins = 0;
@@ -284,7 +322,7 @@ __device__ __forceinline__ int lds_insert_blk(const KParams& p, unsigned long lo
         const uint32_t base = loc & ~3u;
         uint64_t v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = lt[W * (base + q)];  // past S: inside the LDS allocation, masked
+        for (int q = 0; q < 4; ++q) v[q] = lt.w0(base + q);  // past S: inside the LDS allocation, masked
         int hit = -1;
         bool key = false;
 #pragma unroll
@@ -302,10 +340,10 @@ __device__ __forceinline__ int lds_insert_blk(const KParams& p, unsigned long lo
         }
         const uint32_t i = base + (uint32_t)hit;
         if (!key) {
-            const unsigned long long old = atomicCAS(&lt[W * i], (unsigned long long)EMPTY, w0);
+            const unsigned long long old = atomicCAS(lt.p0(i), (unsigned long long)EMPTY, w0);
             if (old == EMPTY) {
                 if (W == 2)
-                    __hip_atomic_store(&lt[2 * i + 1], (unsigned long long)w1, __ATOMIC_RELAXED,
+                    __hip_atomic_store(lt.p1(i), (unsigned long long)w1, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 return (int)i;
             }
@@ -316,7 +354,7 @@ __device__ __forceinline__ int lds_insert_blk(const KParams& p, unsigned long lo
             atomicAdd(&stats[ST_DUP], 1ull);
             return LDS_DUP;
         }
-        const unsigned long long o1 = __hip_atomic_load(&lt[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned long long o1 = __hip_atomic_load(lt.p1(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (o1 == EMPTY) {  // claimed, word1 not stored yet: look again
             if (++spins > (1u << 24)) {
                 atomicAdd(&stats[ST_SPIN], 1ull);
@@ -366,8 +404,8 @@ __device__ __forceinline__ uint32_t succ_of(uint64_t w0, const KParams& p) {
     return (uint32_t)((w0 >> p.idx_lo) & ((1ull << (58 - p.idx_lo)) - 1)) - 1u;  // NO_SUCC when 0
 }
 template <int W>
-__device__ __forceinline__ unsigned long long* pred_word(unsigned long long* lt, uint32_t t) {
-    return &lt[W * t + (W - 1)];
+__device__ __forceinline__ unsigned long long* pred_word(const Slice<W>& lt, uint32_t t) {
+    return W == 2 ? lt.p1(t) : lt.p0(t);
 }
 static constexpr unsigned long long PRED = 1ull << 63;
 // slot as written to the table: successor field and predecessor bit cleaned unless it is a head
@@ -384,7 +422,7 @@ __device__ __forceinline__ void clean_out(uint64_t& w0, uint64_t& w1, const KPar
 // window carrying the top bits of its minimizer order) the test needs no window extraction and
 // y's home is this region's; a tie in the top bits counts as "no link" (never a wrong link).
 template <int W, bool MTOP>
-__device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned long long* lt, uint32_t S,
+__device__ __forceinline__ uint32_t chain_link(const KParams& p, const Slice<W>& lt, uint32_t S,
                                                uint64_t lo, uint64_t cap, uint64_t w0, uint64_t w1, bool dense = false) {
     const uint32_t f = ext_fwd(slot_ext(w0));
     const uint32_t j = slot_jstar(w0) & (W == 1 ? 31u : 63u);
@@ -413,7 +451,7 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned 
             const uint32_t base = t & ~3u;
             uint64_t v[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = lt[W * (base + q)];
+            for (int q = 0; q < 4; ++q) v[q] = lt.w0(base + q);
             int hit = -1;
             bool key = false;
 #pragma unroll
@@ -431,20 +469,14 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned 
             }
             const uint32_t i = base + (uint32_t)hit;
             if (!key) return NO_SUCC;  // EMPTY: y is not in this slice
-            if (W == 1 || (lt[W * i + 1] & LO_MASK) == y.lo) return i;
+            if (W == 1 || (lt.w1(i) & LO_MASK) == y.lo) return i;
             t = i + 1;
         }
         return NO_SUCC;
     }
     for (uint32_t t = (uint32_t)(home - lo); t < S; ++t) {
-        uint64_t v0, v1 = 0;
-        if (W == 2) {  // both words in one LDS read: a match needs no second round trip
-            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(lt)[t];
-            v0 = v.x;
-            v1 = v.y;
-        } else {
-            v0 = lt[t];
-        }
+        uint64_t v0, v1;
+        lt.get(t, v0, v1);  // interleaved: both words in one LDS read (a match needs no second trip)
         if (v0 == EMPTY) break;
         if (slot_keybits(v0, p) == want0 && (W == 1 || (v1 & LO_MASK) == y.lo)) return t;
     }
@@ -453,27 +485,25 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const unsigned 
 
 // record x's link (own slot i: successor field; the successor's predecessor bit)
 template <int W>
-__device__ __forceinline__ void put_link(unsigned long long* lt, uint32_t i, uint32_t nx, const KParams& p) {
+__device__ __forceinline__ void put_link(const Slice<W>& lt, uint32_t i, uint32_t nx, const KParams& p) {
     if (nx == NO_SUCC) return;
-    atomicOr(&lt[W * i], (unsigned long long)(nx + 1) << p.idx_lo);
+    atomicOr(lt.p0(i), (unsigned long long)(nx + 1) << p.idx_lo);
     atomicOr(pred_word<W>(lt, nx), PRED);
 }
 template <int W>
-__device__ __forceinline__ bool is_head(const unsigned long long* lt, uint32_t i, const KParams& p) {
-    uint64_t w0, wp;  // wp: the word holding the predecessor bit (one 16-B LDS read at W=2)
+__device__ __forceinline__ bool is_head(const Slice<W>& lt, uint32_t i, const KParams& p) {
+    uint64_t w0, wp;  // wp: the word holding the predecessor bit
     if (W == 2) {
-        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(lt)[i];
-        w0 = v.x;
-        wp = v.y;
+        lt.get(i, w0, wp);
     } else {
-        w0 = wp = lt[i];
+        w0 = wp = lt.w0(i);
     }
     return w0 != EMPTY && succ_of<W>(w0, p) != NO_SUCC && !(wp & PRED);
 }
 
 // Head records of the listed heads (hlist[0, min(*hcnt, hcap))): walk each chain to its tail.
 template <int W, int TB>
-__device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long* lt, const uint16_t* hlist,
+__device__ __forceinline__ void chain_heads(const KParams& p, const Slice<W>& lt, const uint16_t* hlist,
                                             uint32_t r, bool fresh, uint64_t* headrec, uint32_t hcap,
                                             const uint32_t* hcnt) {
     const uint32_t nh = min(*hcnt, hcap);
@@ -481,49 +511,48 @@ __device__ __forceinline__ void chain_heads(const KParams& p, unsigned long long
     if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(headrec + (uint64_t)nreg(p) * hcap * 2)[r] = nh;
     for (uint32_t id = threadIdx.x; id < nh; id += TB) {
         const uint32_t i = hlist[id];
-        const uint64_t w0 = lt[W * i];
+        const uint64_t w0 = lt.w0(i);
         bool own = true;
         if (!fresh) {
             // the walker reads a record at the region of the key it looked up: in a slice reloaded
             // from the table only keys of this region may own one (others may have spilled in)
-            const Key hk = slot_key(w0, W == 2 ? lt[W * i + 1] & LO_MASK : 0ull, p);
+            const Key hk = slot_key(w0, W == 2 ? lt.w1(i) & LO_MASK : 0ull, p);
             own = place_w(mini_window(hk, mini_scan(hk, p), p), hk, p).r == r;
         }
         if (!own) {
-            lt[W * i] = slot_clean(w0, p);  // no record: the walker steps this k-mer itself
+            *lt.p0(i) = slot_clean(w0, p);  // no record: the walker steps this k-mer itself
             continue;
         }
         uint32_t t = succ_of<W>(w0, p), links = 1;
-        uint64_t tw0 = lt[W * t];
+        uint64_t tw0 = lt.w0(t);
         while (succ_of<W>(tw0, p) != NO_SUCC && links < 63u) {
             t = succ_of<W>(tw0, p);
-            tw0 = lt[W * t];
+            tw0 = lt.w0(t);
             ++links;
         }
-        const uint64_t tw1 = W == 2 ? lt[W * t + 1] & LO_MASK : 0ull;
+        const uint64_t tw1 = W == 2 ? lt.w1(t) & LO_MASK : 0ull;
         *reinterpret_cast<ulonglong2*>(headrec + ((uint64_t)r * hcap + id) * 2) =
             make_ulonglong2(with_hidx(tw0 & ((1ull << p.idx_lo) - 1), links, p), tw1);  // succ 0
-        lt[W * i] = with_hidx(slot_clean(w0, p), id + 1, p);
+        *lt.p0(i) = with_hidx(slot_clean(w0, p), id + 1, p);
     }
 }
 
 // Chains over every slot of the slice (a slice reloaded from the table, or the large-window
 // build): links, then heads into the dense list, then the records.
 template <int W, int TB>
-__device__ __forceinline__ void region_chains(const KParams& p, unsigned long long* lt, uint16_t* hlist, uint32_t S,
+__device__ __forceinline__ void region_chains(const KParams& p, const Slice<W>& lt, uint16_t* hlist, uint32_t S,
                                               uint64_t lo, uint64_t cap, uint32_t r, bool fresh, uint64_t* headrec,
                                               uint32_t hcap, uint32_t* hcnt) {
     for (uint32_t i = threadIdx.x; i < S; i += TB) {
-        const uint64_t w0 = lt[W * i];
-        if (w0 != EMPTY)
-            put_link<W>(lt, i, chain_link<W, false>(p, lt, S, lo, cap, w0, W == 2 ? lt[W * i + 1] : 0ull), p);
+        const uint64_t w0 = lt.w0(i);
+        if (w0 != EMPTY) put_link<W>(lt, i, chain_link<W, false>(p, lt, S, lo, cap, w0, lt.w1(i)), p);
     }
     lds_barrier();
     for (uint32_t i = threadIdx.x; i < S; i += TB) {
         if (is_head<W>(lt, i, p)) {
             const uint32_t id = atomicAdd(hcnt, 1u);
             if (id < hcap) hlist[id] = (uint16_t)i;
-            else lt[W * i] = slot_clean(lt[W * i], p);  // no record room: no index
+            else *lt.p0(i) = slot_clean(lt.w0(i), p);  // no record room: no index
         }
     }
     lds_barrier();
@@ -542,8 +571,9 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
                                                               uint32_t RC, const uint32_t* rcnt,
                                                               uint64_t* headrec, uint32_t hcap, uint32_t smax,
                                                               const uint64_t* __restrict__ rbt) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
-    uint16_t* hlist = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lt_[];
+    uint16_t* hlist = reinterpret_cast<uint16_t*>(lt_ + (uint64_t)smax * W);
+    const Slice<W> lt{lt_, smax};
     __shared__ uint32_t hcnt;
     const uint32_t NR = nreg(p);
     for (uint32_t r = blockIdx.x; r < NR; r += gridDim.x) {
@@ -551,17 +581,16 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
         const uint64_t lo = rbt[r], hi = rbt[r + 1];
         const uint32_t S = (uint32_t)(hi - lo);
         if (W == 2) {
-            ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
             const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
                 ulonglong2 v = table_empty ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
                 if (v.x != EMPTY) v.x = slot_clean(v.x, p);  // earlier chain bits are rebuilt
-                l2[i] = v;
+                lt.put(i, v.x, v.y);
             }
         } else {
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
                 const unsigned long long v = table_empty ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
-                lt[i] = v == EMPTY ? v : slot_clean(v, p);
+                *lt.p0(i) = v == EMPTY ? v : slot_clean(v, p);
             }
         }
         __syncthreads();
@@ -592,16 +621,15 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
         if (hcap) region_chains<W, BUILD_THREADS>(p, lt, hlist, S, lo, cap, r, table_empty != 0, headrec, hcap, &hcnt);
         if (W == 2) {
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
-            const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                const ulonglong2 v = l2[i];
-                uint64_t x = v.x, y = v.y;
+                uint64_t x, y;
+                lt.get(i, x, y);
                 if (hcap && x != EMPTY) clean_out<W>(x, y, p);
                 dst[i] = make_ulonglong2(x, y);
             }
         } else {
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                uint64_t v = lt[i], u = 0;
+                uint64_t v = lt.w0(i), u = 0;
                 if (hcap && v != EMPTY) clean_out<W>(v, u, p);
                 slots[lo + i] = v;
             }
@@ -631,8 +659,9 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                                                                  uint64_t* headrec, uint32_t hcap, uint32_t smax,
                                                                  int prof, const uint64_t* __restrict__ rbt) {
     const KParams p = specialize<KT>(p_in);
-    extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
-    uint16_t* hlist = reinterpret_cast<uint16_t*>(lt + (uint64_t)smax * W);
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lt_[];
+    uint16_t* hlist = reinterpret_cast<uint16_t*>(lt_ + (uint64_t)smax * W);
+    const Slice<W> lt{lt_, smax};
     __shared__ uint32_t hcnt;
     unsigned long long pt_ = prof ? __builtin_amdgcn_s_memtime() : 0ull;
     uint64_t a[IPT], b[IPT];
@@ -672,17 +701,16 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         const bool dense = KH_LDS_BLOCK && 3u * m_cur > 2u * S;
         if (threadIdx.x == 0) hcnt = 0;
         if (W == 2) {
-            ulonglong2* l2 = reinterpret_cast<ulonglong2*>(lt);
             const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
                 ulonglong2 v = FRESH ? make_ulonglong2(EMPTY, EMPTY) : g2[i];
                 if (v.x != EMPTY) v.x = slot_clean(v.x, p);  // earlier chain bits are rebuilt
-                l2[i] = v;
+                lt.put(i, v.x, v.y);
             }
         } else {
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
                 const unsigned long long v = FRESH ? (unsigned long long)EMPTY : (unsigned long long)slots[lo + i];
-                lt[i] = v == EMPTY ? v : slot_clean(v, p);
+                *lt.p0(i) = v == EMPTY ? v : slot_clean(v, p);
             }
         }
         if (FRESH)
@@ -735,7 +763,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 if (id < hcap)
                     hlist[id] = (uint16_t)pos[j];
                 else
-                    lt[W * pos[j]] = slot_clean(lt[W * pos[j]], p);  // no record room: no index
+                    *lt.p0((uint32_t)pos[j]) = slot_clean(lt.w0((uint32_t)pos[j]), p);  // no record room: no index
             }
             lds_barrier();
             BPROF(3);
@@ -748,12 +776,12 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         if (W == 2) {
             // two slots per step: both LDS reads are in flight before either store
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
-            const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(lt);
             for (uint32_t i = threadIdx.x; i < S; i += 2 * BUILD_THREADS) {
                 const uint32_t i2 = i + BUILD_THREADS;
                 const bool two = i2 < S;
-                const ulonglong2 v = l2[i], u = l2[two ? i2 : i];
-                uint64_t x = v.x, y = v.y, x2 = u.x, y2 = u.y;
+                uint64_t x, y, x2, y2;
+                lt.get(i, x, y);
+                lt.get(two ? i2 : i, x2, y2);
                 if (hcap && x != EMPTY) clean_out<W>(x, y, p);
                 if (hcap && x2 != EMPTY) clean_out<W>(x2, y2, p);
                 dst[i] = make_ulonglong2(x, y);
@@ -761,7 +789,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             }
         } else {
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                uint64_t v = lt[i], u = 0;
+                uint64_t v = lt.w0(i), u = 0;
                 if (hcap && v != EMPTY) clean_out<W>(v, u, p);
                 slots[lo + i] = v;
             }

@@ -37,6 +37,14 @@ int fail(int code, const char* fmt, ...) {
                         __FILE__, __LINE__);                                                  \
     } while (0)
 
+// A blocking host wait on the table's stream (a device -> host round trip); counted per table so
+// that hosts can report the syncs of a sharded step (kh_host_syncs).
+#define KH_SYNC(t)                                          \
+    do {                                                    \
+        ++(t)->host_syncs;                                  \
+        KH_HIP(hipStreamSynchronize((t)->stream));          \
+    } while (0)
+
 // Grow-only device buffer.
 struct DevBuf {
     void* p = nullptr;
@@ -129,6 +137,7 @@ struct kh_table {
     uint64_t chunk_cap = 0;
 
     uint64_t n_inserted = 0;                 // host-side count (what was submitted)
+    uint64_t host_syncs = 0;                 // blocking stream waits of this table (KH_SYNC)
     uint64_t last_contigs = 0;               // n_starts seen by the last assemble
     bool assembled = false;
 
@@ -161,7 +170,7 @@ int ensure_list(kh_table* t, DevBuf& buf, uint64_t& cap, uint64_t need) {
     if (rc) return rc;
     if (buf.p && cap)
         KH_HIP(hipMemcpyAsync(nb.p, buf.p, cap * W * 8, hipMemcpyDeviceToDevice, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     buf.release();
     buf = nb;
     nb.p = nullptr;
@@ -175,7 +184,7 @@ int read_ctr(kh_table* t, int idx, uint64_t* v) {
     unsigned long long x = 0;
     KH_HIP(hipMemcpyAsync(&x, t->ctr.as<unsigned long long>() + idx, sizeof x,
                           hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     *v = x;
     return KH_OK;
 }
@@ -184,7 +193,7 @@ int read_ctr(kh_table* t, int idx, uint64_t* v) {
 int check_stats(kh_table* t) {
     unsigned long long st[kh::ST_NUM];
     KH_HIP(hipMemcpyAsync(st, t->stats.p, sizeof st, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     if (st[kh::ST_FULL]) return fail(KH_ERR_FULL, "table full: %llu probes wrapped", st[kh::ST_FULL]);
     if (st[kh::ST_DUP]) return fail(KH_ERR_DUPLICATE, "%llu duplicate k-mers inserted", st[kh::ST_DUP]);
     if (st[kh::ST_BAD_EXT])
@@ -406,7 +415,7 @@ int kh_reserve(kh_table* t, uint64_t n_kmers) {
         return fail(KH_ERR_STATE, "kh_reserve on a table holding %llu k-mers (clear it first)",
                     (unsigned long long)t->n_inserted);
     if (int rc = set_device(t)) return rc;
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     const uint64_t old_n = t->n_kmers;
     const int old_bits = t->kp.split_bits;
     size_table(t, n_kmers);
@@ -453,11 +462,17 @@ int kh_set_stream(kh_table* t, void* s) {
 int kh_sync(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (int rc = set_device(t)) return rc;
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     return check_stats(t);
 }
 
 uint64_t kh_capacity(const kh_table* t) { return t ? t->cap : 0; }
+
+int kh_host_syncs(const kh_table* t, uint64_t* n) {
+    if (!t || !n) return fail(KH_ERR_ARG, "null argument");
+    *n = t->host_syncs;
+    return KH_OK;
+}
 
 int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     if (!t) return fail(KH_ERR_ARG, "null table");
@@ -599,7 +614,7 @@ static int insert_chunked_upload(kh_table* t, const uint8_t* host_recs, uint64_t
     t->last_insert_part = true;
     t->n_inserted += n;
     t->assembled = false;
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     return check_stats(t);
 }
 
@@ -617,7 +632,7 @@ int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n) {
     if (int rc = t->stage.ensure(bytes)) return rc;
     KH_HIP(hipMemcpyAsync(t->stage.p, host_recs, bytes, hipMemcpyHostToDevice, t->stream));
     if (int rc = kh_insert_dev(t, t->stage.p, n)) return rc;
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     return check_stats(t);
 }
 
@@ -646,7 +661,7 @@ int kh_find(kh_table* t, const uint8_t* keys, uint64_t n, uint8_t* out, uint8_t*
     if ((rc = kh_find_dev(t, t->stage.p, n, t->stage2.p, t->stage3.p))) return rc;
     KH_HIP(hipMemcpyAsync(out, t->stage2.p, rb, hipMemcpyDeviceToHost, t->stream));
     KH_HIP(hipMemcpyAsync(found, t->stage3.p, n, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     return KH_OK;
 }
 
@@ -661,7 +676,7 @@ int kh_set_starts(kh_table* t, const uint8_t* recs, uint64_t n) {
     if (n) KH_HIP(hipMemcpyAsync(t->stage.p, recs, bytes, hipMemcpyHostToDevice, t->stream));
     KH_HIP(kh::launch_load_starts(t->kp, t->stage.as<uint8_t>(), n, t->starts.as<uint64_t>(),
                                   t->ctr.as<unsigned long long>(), t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     t->assembled = false;
     t->split_ok = false;  // caller's starts may share segments (e.g. two starts on one contig)
     return KH_OK;
@@ -677,7 +692,7 @@ int kh_assemble_dev(kh_table* t) {
     // start_nodes.size() on the host before walking, kmer_hash.cpp:41).
     unsigned long long cv[kh::CT_NUM];
     KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     const uint64_t ns = cv[kh::CT_N_STARTS];
     uint64_t nsp = 0;
     const unsigned long long* nsp_dev = nullptr;
@@ -816,7 +831,7 @@ int kh_assemble_dev(kh_table* t) {
         unsigned long long hv[2], ovf = 0;
         KH_HIP(hipMemcpyAsync(hv, ctr + kh::CT_CHUNK_NEXT, sizeof hv, hipMemcpyDeviceToHost, t->stream));
         KH_HIP(hipMemcpyAsync(&ovf, stats + kh::ST_CHUNK_OVF, 8, hipMemcpyDeviceToHost, t->stream));
-        KH_HIP(hipStreamSynchronize(t->stream));
+        KH_SYNC(t);
         if (ns == 0) hv[1] = 0;
         if (ovf && attempt == 0) {
             const uint64_t need = nseg + hv[0] + 64;
@@ -849,7 +864,7 @@ int kh_assemble_dev(kh_table* t) {
 
 int kh_assemble(kh_table* t, uint64_t* n_contigs, uint64_t* out_bytes) {
     if (int rc = kh_assemble_dev(t)) return rc;
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     if (int rc = check_stats(t)) return rc;
     uint64_t ob = 0;
     if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
@@ -884,7 +899,7 @@ int kh_contigs_offsets(kh_table* t, uint64_t* out, uint64_t n) {
     if (n > t->last_contigs) return fail(KH_ERR_ARG, "asked for %llu offsets of %llu contigs",
                                          (unsigned long long)n, (unsigned long long)t->last_contigs);
     if (n) {
-        KH_HIP(hipStreamSynchronize(t->stream));
+        KH_SYNC(t);
         KH_HIP(hipMemcpy(out, t->contig_off.p, n * 8, hipMemcpyDeviceToHost));
     }
     return KH_OK;
@@ -893,7 +908,7 @@ int kh_contigs_offsets(kh_table* t, uint64_t* out, uint64_t n) {
 int kh_get_stats(kh_table* t, kh_stats* s) {
     if (!t || !s) return fail(KH_ERR_ARG, "null argument");
     if (int rc = set_device(t)) return rc;
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     unsigned long long st[kh::ST_NUM], ct[kh::CT_NUM];
     KH_HIP(hipMemcpy(st, t->stats.p, sizeof st, hipMemcpyDeviceToHost));
     KH_HIP(hipMemcpy(ct, t->ctr.p, sizeof ct, hipMemcpyDeviceToHost));
@@ -1243,14 +1258,14 @@ int kh_insert_words_finish(kh_table* t) {
 // ---- migrating-walker rounds --------------------------------------------------------------------
 namespace {
 // Grow b to >= want bytes keeping its first `used` bytes.
-int grow_keep(DevBuf& b, uint64_t want, uint64_t used, hipStream_t s) {
+int grow_keep(kh_table* t, DevBuf& b, uint64_t want, uint64_t used) {
     if (want <= b.bytes && b.p) return KH_OK;
     uint64_t nb = b.bytes + b.bytes / 2;
     if (nb < want) nb = want;
     DevBuf n;
     if (int rc = n.ensure(nb)) return rc;
-    if (used) KH_HIP(hipMemcpyAsync(n.p, b.p, used, hipMemcpyDeviceToDevice, s));
-    KH_HIP(hipStreamSynchronize(s));
+    if (used) KH_HIP(hipMemcpyAsync(n.p, b.p, used, hipMemcpyDeviceToDevice, t->stream));
+    KH_SYNC(t);
     b.release();
     b.p = n.p;
     b.bytes = n.bytes;
@@ -1276,7 +1291,7 @@ static int mw_store_count(kh_table* t) {
     if (t->mw_store_known) return KH_OK;
     unsigned long long v = 0;
     KH_HIP(hipMemcpyAsync(&v, t->mw_misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     t->mw_store_n = v;
     t->mw_store_known = true;
     return KH_OK;
@@ -1292,7 +1307,7 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     int rc;
     unsigned long long cv[kh::CT_NUM];  // one read of the counters (starts, hot regions, splitters)
     KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     const uint64_t ns = cv[kh::CT_N_STARTS];
     t->mw_hot = cv[kh::CT_HOT] != 0;
     if (ns >= (1ull << 31)) return fail(KH_ERR_ARG, "%llu start k-mers on one rank (max 2^31)", (unsigned long long)ns);
@@ -1393,7 +1408,7 @@ int kh_mwalk_link_dev(kh_table* t, const void* recs, uint64_t n, void* out, void
     KH_HIP(kh::launch_mseg_scan((const uint64_t*)recs, n, nseg, st, fin, t->stream));
     uint64_t f = 0;
     KH_HIP(hipMemcpyAsync(&f, fin, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     if (f != nseg)
         return fail(KH_ERR_NOT_FOUND, "%llu of %llu walk segments did not finish (records lost in transit?)",
                     (unsigned long long)(nseg - f), (unsigned long long)nseg);
@@ -1441,7 +1456,7 @@ int kh_mwalk_jump_apply_dev(kh_table* t, const void* replies, uint64_t m, uint64
     if (pending) {  // optional: the next emit's counts already say whether any rank is pending
         uint64_t l = 0;
         KH_HIP(hipMemcpyAsync(&l, left, 8, hipMemcpyDeviceToHost, t->stream));
-        KH_HIP(hipStreamSynchronize(t->stream));
+        KH_SYNC(t);
         *pending = l;
     }
     return KH_OK;
@@ -1478,7 +1493,7 @@ int kh_mwalk_end_seg_dev(kh_table* t, const void* recs, uint64_t n, const void* 
     if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
     uint64_t bytes = 0;
     KH_HIP(hipMemcpyAsync(&bytes, ctr + kh::CT_OUT_BYTES, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     if ((rc = t->text.ensure(bytes + 64))) return rc;
     KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
                                   t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
@@ -1536,7 +1551,7 @@ int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, vo
         if ((rc = mw_store_count(t))) return rc;
         t->mw_store_bound = t->mw_store_n;
     }
-    if ((rc = grow_keep(t->mw_store, (t->mw_store_bound + add) * 16 + 16, t->mw_store_bound * 16, t->stream)))
+    if ((rc = grow_keep(t, t->mw_store, (t->mw_store_bound + add) * 16 + 16, t->mw_store_bound * 16)))
         return rc;
     KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), store_n, t->stream));
     KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>(), t->stream));
@@ -1592,7 +1607,7 @@ int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
     uint64_t hv[3] = {0, 0, 0};
     static_assert(kh::CT_MW_FIN == kh::CT_OUT_BYTES + 2, "counter layout");
     KH_HIP(hipMemcpyAsync(hv, ctr + kh::CT_OUT_BYTES, 24, hipMemcpyDeviceToHost, t->stream));
-    KH_HIP(hipStreamSynchronize(t->stream));
+    KH_SYNC(t);
     const uint64_t bytes = hv[0], fin = hv[2];
     if (fin != nc)
         return fail(KH_ERR_NOT_FOUND, "%llu of %llu walkers did not finish (records lost in transit?)",

@@ -91,6 +91,9 @@ int kh_reserve(kh_table* t, uint64_t n_kmers);
 int kh_set_stream(kh_table* t, void* hip_stream); /* NULL = back to the table's own stream */
 int kh_sync(kh_table* t);                        /* wait for the stream; report device errors */
 uint64_t kh_capacity(const kh_table* t);
+/* blocking host waits on the table's stream so far (device -> host reads of counts, syncs):
+ * hosts count the round trips of a sharded step with it (tests/test_gpu_dist.py) */
+int kh_host_syncs(const kh_table* t, uint64_t* n);
 int kh_get_stats(kh_table* t, kh_stats* out);    /* syncs */
 
 /* ---- insert: records in kmer_pair layout. Start k-mers (bwd == 'F') of every batch are appended
