@@ -44,7 +44,13 @@ class KhStats(ctypes.Structure):
 MSG_WORDS = 5  # KH_MSG_WORDS: migrating-walker message
 TEXT_REC_WORDS = 2  # KH_TEXT_REC_WORDS
 LINK_WORDS = 4  # KH_LINK_WORDS
-JUMP_REPLY_WORDS = 3  # KH_JUMP_REPLY_WORDS
+PRED_WORDS = 2  # KH_PRED_WORDS
+
+
+def slot_words(cap):
+    """KH_SLOT_WORDS: int64 words of one exchange slot of `cap` messages."""
+    return 2 + cap * MSG_WORDS
+
 SEG_REC_WORDS = 3  # KH_SEG_REC_WORDS
 
 _SIGS = {
@@ -82,17 +88,19 @@ _SIGS = {
     "kh_insert_words_stage_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_u64]),
     "kh_insert_words_finish": (ctypes.c_int, [c_vp]),
     "kh_pack_text_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, ctypes.POINTER(c_u64)]),
-    "kh_mwalk_begin": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u64, ctypes.POINTER(c_u64)]),
-    "kh_mwalk_round_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
-    "kh_mwalk_text_count": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
+    "kh_host_syncs": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
+    "kh_route_splitters_dev": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int]),
+    "kh_counters_dev": (ctypes.c_int, [c_vp, c_vp]),
+    "kh_mwalk_begin": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u64, c_u64, c_u64, c_u64,
+                                      ctypes.POINTER(c_u64)]),
+    "kh_mwalk_round_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_u64, c_vp]),
+    "kh_mwalk_text_bound": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "kh_mwalk_text_dev": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "kh_mwalk_end_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_mwalk_segments": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "kh_mwalk_link_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
-    "kh_mwalk_pred_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
-    "kh_mwalk_jump_emit_dev": (ctypes.c_int, [c_vp, c_vp, c_vp]),
-    "kh_mwalk_jump_answer_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp]),
-    "kh_mwalk_jump_apply_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, ctypes.POINTER(c_u64)]),
+    "kh_mwalk_pred_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_u64]),
+    "kh_mwalk_resolve_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),
     "kh_mwalk_retag_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
     "kh_mwalk_end_seg_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_u64]),
     "kh_dev_malloc": (ctypes.c_int, [ctypes.POINTER(c_vp), c_u64, ctypes.c_int]),

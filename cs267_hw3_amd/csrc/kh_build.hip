@@ -953,6 +953,9 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
     }
 }
 
+#ifndef KH_SORT_SPLIT
+#define KH_SORT_SPLIT 1
+#endif
 // Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
 // with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
 // out[window(bin) + reserved + rank] (positions past cap -> overflow list).
@@ -992,8 +995,9 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
     for (int j = 0; j < IPT; ++j) {
         if (a[j] != EMPTY) {
             const uint32_t pos = start[bin[j]] + rank[j];
-            items[pos * W] = a[j];
-            if (W == 2) items[pos * W + 1] = b[j];
+            // words 0 and 1 in two arrays (KH_SORT_SPLIT): random 8-B stores over every bank pair
+            items[KH_SORT_SPLIT ? pos : W * pos] = a[j];
+            if (W == 2) items[KH_SORT_SPLIT ? TILE + pos : 2 * pos + 1] = b[j];
             sbin[pos] = (uint16_t)bin[j];
         }
     }
@@ -1005,7 +1009,8 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
         const uint32_t q = sbin[x];
         const uint32_t w = gpos[q] + (x - start[q]);
         if (w < cap) {
-            const uint64_t v0 = items[W * x], v1 = (W == 2) ? items[W * x + 1] : 0;
+            const uint64_t v0 = items[KH_SORT_SPLIT ? x : W * x],
+                           v1 = (W == 2) ? items[KH_SORT_SPLIT ? TILE + x : 2 * x + 1] : 0;
             const uint64_t g = window(q) + w;
             if (W == 2) {
                 *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(v0, v1);
@@ -1038,8 +1043,8 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
             if (rr >= keepv[q]) {
                 const uint64_t d = sbase + hist[q] + (rr - keepv[q]);
                 if (d < ovf_cap) {
-                    ovf[d * W] = items[W * x];
-                    if (W == 2) ovf[d * W + 1] = items[W * x + 1];
+                    ovf[d * W] = items[KH_SORT_SPLIT ? x : W * x];
+                    if (W == 2) ovf[d * W + 1] = items[KH_SORT_SPLIT ? TILE + x : 2 * x + 1];
                 } else {
                     atomicAdd(&stats[ST_FULL], 1ull);
                 }
@@ -1154,9 +1159,17 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
                                                  uint32_t CAP1, uint32_t* wcnt, uint64_t* buf1,
                                                  uint64_t* start_mask, uint64_t* split_mask, uint64_t* ovf,
                                                  uint64_t ovf_cap, unsigned long long* ctr,
-                                                 unsigned long long* stats, uint32_t P = 1) {
+                                                 unsigned long long* stats, uint32_t P = 1,
+                                                 unsigned long long* spl = nullptr) {
     const KParams p = specialize<KT>(p_in);
     constexpr int NB = ROUTE ? MAX_RANKS : NB1;
+    // ROUTE: splitter k-mers routed to each owner (its migrating walk seeds a walker at each; the
+    // owner's host learns their number with the route counts instead of reading its list)
+    __shared__ uint32_t rspl[ROUTE ? MAX_RANKS : 1];
+    if (ROUTE && spl) {
+        if (threadIdx.x < MAX_RANKS) rspl[threadIdx.x] = 0;
+        __syncthreads();
+    }
     constexpr int IPT = TILE / TB;
     const bool hot_on = !ROUTE && p.hot && ctr[CT_HOT];
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -1234,10 +1247,12 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
             }
             a[j] = valid ? part_word0(slot_w0(k, ext, p), mn, p) : EMPTY;
             b[j] = (valid && W == 2) ? k.lo : 0;
-            if (ROUTE)
+            if (ROUTE) {
                 bin[j] = P == 1 ? 0u
                                 : (p.owner_mode == 1 ? owner_key(k, p, P) : owner_of_mini(mini_window(k, mn, p), P));
-            else
+                if (spl && valid && ext_bwd(ext) != EXT_F && is_splitter(key_hash32(k), p))
+                    atomicAdd(&rspl[bin[j]], 1u);
+            } else
                 bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on) >> (p.rbits - B1);
         }
         const uint64_t nt = t + gridDim.x, nbase = nt * TILE;
@@ -1274,6 +1289,10 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
                 [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
                 [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
         }
+    }
+    if (ROUTE && spl) {
+        __syncthreads();
+        if (threadIdx.x < P && rspl[threadIdx.x]) atomicAdd(&spl[threadIdx.x], (unsigned long long)rspl[threadIdx.x]);
     }
 }
 
@@ -1401,7 +1420,8 @@ __global__ void k_route_win_counts(const uint32_t* cnt, uint32_t P, uint64_t n, 
 template <int W, int PK>
 static hipError_t route_win_launch(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
                                    uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
-                                   unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+                                   unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
+                                   unsigned long long* spl) {
     constexpr size_t lds = 0;  // the route stages nothing in LDS (k_win1_rec ROUTE)
     hipError_t e;
     if ((e = hipMemsetAsync(cnt, 0, (size_t)MAX_RANKS * 4, s)) != hipSuccess) return e;
@@ -1414,7 +1434,8 @@ static hipError_t route_win_launch(const KParams& p, const uint8_t* recs, uint64
             hipError_t x;
             if ((x = allow_lds(k_win1_rec<W, 512, REC_TILE, PK, KT, true>, lds)) != hipSuccess) return x;
             k_win1_rec<W, 512, REC_TILE, PK, KT, true><<<(unsigned)grid, 512, lds, s>>>(
-                p, recs, n, (uint32_t)win, cnt, words, start_mask, nullptr, nullptr, 0, ctr, stats, P);
+                p, recs, n, (uint32_t)win, cnt, words, start_mask, nullptr, nullptr, 0, ctr, stats, P,
+                p.split_bits ? spl : nullptr);
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
@@ -1425,13 +1446,14 @@ static hipError_t route_win_launch(const KParams& p, const uint8_t* recs, uint64
 
 hipError_t launch_route_win(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
                             uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
-                            unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+                            unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
+                            unsigned long long* spl) {
     if (win < n || win >= (1ull << 32) || p.R > 15) return hipErrorInvalidValue;  // 64 records in 62 blocks
     if (p.W == 1)
-        return p.P == 5 ? route_win_launch<1, 5>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s)
-                        : route_win_launch<1, 0>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s);
-    return p.P == 13 ? route_win_launch<2, 13>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s)
-                     : route_win_launch<2, 0>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s);
+        return p.P == 5 ? route_win_launch<1, 5>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s, spl)
+                        : route_win_launch<1, 0>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s, spl);
+    return p.P == 13 ? route_win_launch<2, 13>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s, spl)
+                     : route_win_launch<2, 0>(p, recs, n, P, words, win, cnt, counts, start_mask, ctr, stats, s, spl);
 }
 
 // pass 2: bucket -> region windows (RC words each)

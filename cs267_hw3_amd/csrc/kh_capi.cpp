@@ -120,9 +120,14 @@ struct kh_table {
     DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
     // splitter segments of the migrating walk (kh_mseg.hip)
     DevBuf ms_len, ms_hi, ms_lo, ms_has, ms_done, ms_jump, ms_acc, ms_stab, ms_stab_id, ms_qsrc, ms_misc;
+    DevBuf mw_pack, mw_cnt, mw_list, mw_carry[2], mw_carry_dst[2];  // fixed-slot rounds
+    DevBuf ms_res[6], ms_pend;               // pointer jumping over the gathered predecessor tables
+    DevBuf route_spl;                        // splitter k-mers routed to each owner (MAX_RANKS words)
+    int mw_cur = 0;                          // carry buffer written by the last round
     bool words_split = true;   // every routed word since the last clear went through splitter collection
     bool ms_on = false;        // the current migrating walk uses splitter segments
     uint64_t ms_ns = 0, ms_nsp = 0, ms_cap2 = 0, ms_nq = 0;
+    uint64_t mw_wg = 0;        // walkers of every rank (bound of a round's input / held-back messages)
     uint64_t mw_store_n = 0;   // text records in mw_store (valid when mw_store_known)
     uint64_t mw_store_bound = 0;  // upper bound of the store's records (its device count: mw_misc[2])
     bool mw_store_known = true;
@@ -371,6 +376,7 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     if (balanced_bounds(t)) t->kp.rb = t->rbounds.as<uint64_t>();
     kh::launch_bounds(t->kp, t->cap, nullptr, 0, t->rbounds.as<uint64_t>(), t->stream);
     if ((rc = t->ctr.ensure(kh::CT_NUM * 8))) return bail(rc);
+    if ((rc = t->route_spl.ensure(kh::MAX_RANKS * 8))) return bail(rc);
     if ((rc = t->stats.ensure(kh::ST_NUM * 8))) return bail(rc);
     if ((rc = kh_clear(t))) return bail(rc);
     if (hipStreamSynchronize(t->stream) != hipSuccess) return bail(fail(KH_ERR_HIP, "sync failed"));
@@ -391,6 +397,9 @@ int kh_destroy(kh_table* t) {
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
+                      &t->mw_pack, &t->mw_cnt, &t->mw_list, &t->mw_carry[0], &t->mw_carry[1], &t->mw_carry_dst[0],
+                      &t->mw_carry_dst[1], &t->ms_res[0], &t->ms_res[1], &t->ms_res[2], &t->ms_res[3], &t->ms_res[4],
+                      &t->ms_res[5], &t->ms_pend, &t->route_spl,
                       &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot, &t->rbounds, &t->start_rec};
     if (t->side) (void)hipStreamSynchronize(t->side);  // k_rec_succ may still read the table
     for (auto* b : bufs) b->release();
@@ -419,6 +428,9 @@ int kh_reserve(kh_table* t, uint64_t n_kmers) {
     const uint64_t old_n = t->n_kmers;
     const int old_bits = t->kp.split_bits;
     size_table(t, n_kmers);
+    // the splitter density stays the one the table was created with: every shard of a sharded
+    // table must use the same (a walker stops before splitters that their owner seeds walkers at)
+    t->kp.split_bits = old_bits;
     // the new slot array first: when it cannot be had, the table keeps its old one and old size
     DevBuf ns;
     if (int rc = ns.ensure(t->cap * (uint64_t)t->kp.W * 8)) {
@@ -443,6 +455,7 @@ int kh_clear(kh_table* t) {
     KH_HIP(hipMemsetAsync(t->ctr.p, 0, kh::CT_NUM * 8, t->stream));
     KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
     KH_HIP(hipMemsetAsync(t->hot.p, 0, kh::HOT_WORDS * 4, t->stream));  // placement by minimizer again
+    KH_HIP(hipMemsetAsync(t->route_spl.p, 0, kh::MAX_RANKS * 8, t->stream));
     t->n_inserted = 0;
     t->assembled = false;
     t->split_ok = true;
@@ -1091,7 +1104,8 @@ int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nrank
     KH_HIP(kh::launch_route(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks,
                             t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
                             t->route_scratch.as<uint64_t>(), t->route_own.as<uint32_t>(), (uint64_t*)words_out,
-                            (uint64_t*)counts_out, t->stream, n ? t->mask.as<uint64_t>() : nullptr));
+                            (uint64_t*)counts_out, t->stream, n ? t->mask.as<uint64_t>() : nullptr,
+                            mseg_enabled(t) ? t->route_spl.as<unsigned long long>() : nullptr));
     if (n)
         KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
                                          t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
@@ -1123,13 +1137,32 @@ int kh_route_starts_win_dev(kh_table* t, const void* dev_recs, uint64_t n, int n
     if ((rc = ensure_starts(t, t->collected_n + n))) return rc;
     KH_HIP(kh::launch_route_win(t->kp, (const uint8_t*)dev_recs, n, (uint32_t)nranks, (uint64_t*)words_out, win,
                                 t->route_own.as<uint32_t>(), (uint64_t*)counts_out, n ? t->mask.as<uint64_t>() : nullptr,
-                                t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(), t->stream));
+                                t->ctr.as<unsigned long long>(), t->stats.as<unsigned long long>(), t->stream,
+                                mseg_enabled(t) ? t->route_spl.as<unsigned long long>() : nullptr));
     if (n)
         KH_HIP(kh::launch_collect_starts(t->kp, (const uint8_t*)dev_recs, n, t->mask.as<uint64_t>(),
                                          t->mask_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
                                          t->starts.as<uint64_t>(), t->ctr.as<unsigned long long>(), t->stream));
     t->collected_n += n;
     t->assembled = false;
+    return KH_OK;
+}
+
+int kh_route_splitters_dev(kh_table* t, void* dev_out, int nranks) {
+    if (!t || !dev_out) return fail(KH_ERR_ARG, "null argument");
+    if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(hipMemcpyAsync(dev_out, t->route_spl.p, (size_t)nranks * 8, hipMemcpyDeviceToDevice, t->stream));
+    return KH_OK;
+}
+
+int kh_counters_dev(kh_table* t, void* dev_out) {
+    if (!t || !dev_out) return fail(KH_ERR_ARG, "null argument");
+    if (int rc = set_device(t)) return rc;
+    uint64_t* o = (uint64_t*)dev_out;
+    const unsigned long long* c = t->ctr.as<unsigned long long>();
+    KH_HIP(hipMemcpyAsync(o, c + kh::CT_N_STARTS, 8, hipMemcpyDeviceToDevice, t->stream));
+    KH_HIP(hipMemcpyAsync(o + 1, c + kh::CT_N_SPLIT, 8, hipMemcpyDeviceToDevice, t->stream));
     return KH_OK;
 }
 
@@ -1286,18 +1319,12 @@ static kh::MSegState mseg_state(kh_table* t) {
     return st;
 }
 
-// The text store's record count (one host read after the rounds, not one per round).
-static int mw_store_count(kh_table* t) {
-    if (t->mw_store_known) return KH_OK;
-    unsigned long long v = 0;
-    KH_HIP(hipMemcpyAsync(&v, t->mw_misc.as<unsigned long long>() + 2, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_SYNC(t);
-    t->mw_store_n = v;
-    t->mw_store_known = true;
-    return KH_OK;
-}
+// device words of mw_misc: [0] link-scan finish count, [2] text-store count, [3] first round's
+// walkers, [4] carry count of buffer 0, [5] of buffer 1
+static unsigned long long* mw_word(kh_table* t, int i) { return t->mw_misc.as<unsigned long long>() + i; }
 
-int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t* n_walkers) {
+int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t n_starts, uint64_t n_splitters,
+                   uint64_t total_walkers, uint64_t* n_walkers) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (nranks < 1 || nranks > kh::MAX_RANKS || rank < 0 || rank >= nranks)
         return fail(KH_ERR_ARG, "bad rank %d of %d", rank, nranks);
@@ -1305,25 +1332,23 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     if (int rc = join_succ(t)) return rc;
     if (int rc = clean_slots(t)) return rc;
     int rc;
-    unsigned long long cv[kh::CT_NUM];  // one read of the counters (starts, hot regions, splitters)
-    KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
-    KH_SYNC(t);
-    const uint64_t ns = cv[kh::CT_N_STARTS];
-    t->mw_hot = cv[kh::CT_HOT] != 0;
+    // the counts come from the caller (kh_counters_dev / kh_route_splitters_dev, read together
+    // with its own exchange): no device read here
+    const uint64_t ns = n_starts;
     if (ns >= (1ull << 31)) return fail(KH_ERR_ARG, "%llu start k-mers on one rank (max 2^31)", (unsigned long long)ns);
-    // splitter segments: every splitter this shard owns seeds a walker too (kh_mseg.hip)
-    // on or off the same way on every rank (walkers stop before splitters owned anywhere)
     uint64_t nsp = 0;
+    // splitter segments: every splitter this shard owns seeds a walker too (kh_mseg.hip), on or
+    // off the same way on every rank (walkers stop before splitters owned anywhere)
     t->ms_on = mseg_enabled(t) && t->words_split;
-    if (t->ms_on && t->splits.p) {
-        nsp = cv[kh::CT_N_SPLIT];
-        if (nsp > t->splits_cap)
-            return fail(KH_ERR_FULL, "%llu splitter k-mers exceed the list (%llu)", (unsigned long long)nsp,
-                        (unsigned long long)t->splits_cap);
+    if (t->ms_on) {
+        nsp = n_splitters;
+        if ((rc = ensure_list(t, t->splits, t->splits_cap, nsp))) return rc;
         if (ns + nsp >= (1ull << 31))
             return fail(KH_ERR_ARG, "%llu walk segments on one rank (max 2^31)", (unsigned long long)(ns + nsp));
     }
     const uint64_t nseg = ns + nsp;
+    // walkers of every rank: a rank may host (and hold back) at most all of them in a round
+    t->mw_wg = total_walkers > nseg ? total_walkers : nseg;
     if ((rc = t->mw_init.ensure((nseg + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_misc.ensure(64)) ||
         (rc = t->mw_store.ensure((nseg + 1024) * 16)))
         return rc;
@@ -1337,24 +1362,28 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
             (rc = t->ms_lo.ensure((nseg + 1) * 8)) || (rc = t->ms_has.ensure(nseg + 1)) ||
             (rc = t->ms_done.ensure(nseg + 1)) || (rc = t->ms_jump.ensure((nseg + 1) * 8)) ||
             (rc = t->ms_acc.ensure((nseg + 1) * 8)) || (rc = t->ms_stab.ensure(cap2 * 16)) ||
-            (rc = t->ms_stab_id.ensure(cap2 * 4)) || (rc = t->ms_qsrc.ensure((nsp + 1) * 4)) ||
-            (rc = t->ms_misc.ensure(64)))
+            (rc = t->ms_stab_id.ensure(cap2 * 4)) || (rc = t->ms_misc.ensure(64)))
             return rc;
     }
+    unsigned long long* ctr = t->ctr.as<unsigned long long>();
+    unsigned long long* stats = t->stats.as<unsigned long long>();
+    // the caller's counts must be the device's (a mismatch fails the walk at the next sync)
+    KH_HIP(kh::launch_fin_check(ctr + kh::CT_N_STARTS, ns, nullptr, 0, stats, t->stream));
+    if (t->ms_on) KH_HIP(kh::launch_fin_check(ctr + kh::CT_N_SPLIT, nsp, nullptr, 0, stats, t->stream));
     t->mw_P = (uint32_t)nranks;
     t->mw_rank = (uint32_t)rank;
-    t->rw_n = ns;
+    t->rw_n = nseg;
     t->rw_total = total_kmers > ns ? total_kmers : ns;
     t->mw_store_n = 0;
     t->mw_store_bound = 0;
-    t->mw_store_known = true;
-    KH_HIP(hipMemsetAsync(t->mw_misc.as<unsigned long long>() + 2, 0, 8, t->stream));
+    t->mw_store_known = false;
+    t->mw_cur = 0;
+    KH_HIP(hipMemsetAsync(mw_word(t, 2), 0, 8 * 4, t->stream));  // store count, walkers, carries
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
     t->wk_timed = false;
     // chain records: every walker whose k-mer heads a record starts from it (k_mw_init), and the
     // records' successor runs are resolved beside the first round (k_rec_succ, as on one GPU)
     kh::KParams ikp = t->kp;
-    if (!t->mw_hot) ikp.hot = nullptr;
     const uint32_t hcap = (t->headrec.p && t->kp.chain && !kh::debug_flag("no_start_rec") &&
                            (uint64_t)t->hcap * (1ull << t->kp.rbits) < 0xFFFFFFFFull)
                               ? t->hcap
@@ -1380,11 +1409,152 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
         KH_HIP(kh::launch_mseg_stab(t->kp, t->splits.as<uint64_t>(), nsp, t->ms_stab.as<uint64_t>(),
                                     t->ms_stab_id.as<uint32_t>(), t->ms_cap2, t->stream));
     }
-    t->rw_n = nseg;
     t->mw_live = true;
     t->mw_stepped = false;
     t->assembled = false;
     if (n_walkers) *n_walkers = nseg;
+    return KH_OK;
+}
+
+int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void* out_slots, uint64_t out_cap,
+                       void* dev_live) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (!out_slots || !dev_live || out_cap == 0) return fail(KH_ERR_ARG, "null output slots / live word");
+    if (t->mw_stepped && !in_slots) return fail(KH_ERR_ARG, "null input slots");
+    if (int rc = set_device(t)) return rc;
+    const uint32_t P = t->mw_P;
+    int rc;
+    // this round's walkers: the begin's (first round), or the P slots received
+    const uint64_t* src = t->mw_init.as<uint64_t>();
+    uint64_t nb = t->rw_n;  // bound (every walker is live in the first round)
+    unsigned long long* n_dev = mw_word(t, 3);
+    if (t->mw_stepped) {
+        nb = (uint64_t)P * in_cap;
+        if (nb > t->mw_wg) nb = t->mw_wg;  // walkers never multiply
+        if ((rc = t->mw_list.ensure((nb + 1) * kh::MSG_WORDS * 8))) return rc;
+        KH_HIP(kh::launch_slot_gather((const uint64_t*)in_slots, P, in_cap, t->mw_list.as<uint64_t>(), n_dev,
+                                      t->stream));
+        src = t->mw_list.as<uint64_t>();
+    } else {
+        KH_HIP(kh::launch_add_count(n_dev, t->rw_n, nullptr, 0, t->stream));
+    }
+    const uint64_t cb = t->mw_wg;  // held-back messages: at most every walker
+    if ((rc = t->mw_tmp.ensure((nb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_dst.ensure(nb + 1)) ||
+        (rc = t->mw_stage.ensure((nb + 1) * kh::MW_REC_SLOTS * 16)) || (rc = t->mw_nrec.ensure(nb + 1)) ||
+        (rc = t->mw_off.ensure((nb + 1) * 8)) || (rc = t->scratch.ensure(kh::scan_scratch_words(nb) * 8 + 64)) ||
+        (rc = t->mw_pack.ensure((nb + cb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_cnt.ensure((P + 1) * 8)) ||
+        (rc = t->mw_carry[0].ensure((cb + 1) * kh::MSG_WORDS * 8)) ||
+        (rc = t->mw_carry[1].ensure((cb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_carry_dst[0].ensure(cb + 1)) ||
+        (rc = t->mw_carry_dst[1].ensure(cb + 1)) || (rc = ensure_route(t, nb + cb, (int)P)))
+        return rc;
+    kh::MWalkRound mw;
+    mw.P = P;
+    mw.rank = t->mw_rank;
+    mw.split_bits = t->ms_on ? (uint32_t)mseg_params(t).split_bits : 0u;
+    mw.headrec = t->headrec.as<uint64_t>();
+    mw.hcap = t->headrec.p ? t->hcap : 0u;
+    mw.max_steps = t->rw_total;
+    mw.in = src;
+    mw.n_in = nb;
+    mw.n_dev = n_dev;
+    mw.hot_on = t->ctr.as<unsigned long long>() + kh::CT_HOT;  // the kernel skips the bitmap when 0
+    mw.tmp = t->mw_tmp.as<uint64_t>();
+    mw.dst = t->mw_dst.as<uint8_t>();
+    mw.stage = t->mw_stage.as<uint64_t>();
+    mw.nrec = t->mw_nrec.as<uint8_t>();
+    KH_HIP(kh::launch_mw_run(t->kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
+    // text records of this round -> the rank-local store at offsets continuing its device-side
+    // count (the store is sized from an upper bound: MW_REC_SLOTS per walker and round)
+    unsigned long long* store_n = mw_word(t, 2);
+    const uint64_t add = nb * (uint64_t)kh::MW_REC_SLOTS;
+    if ((rc = grow_keep(t, t->mw_store, (t->mw_store_bound + add) * 16 + 16, t->mw_store_bound * 16))) return rc;
+    KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), store_n, t->stream));
+    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>(), t->stream));
+    t->mw_store_bound += add;
+    // outgoing walkers (+ the ones held back last round) -> P slots of out_cap; overflow held back
+    const int cur = t->mw_cur, nxt = 1 - cur;
+    kh::SlotRound r;
+    r.P = P;
+    r.nb = nb;
+    r.n_dev = n_dev;
+    r.dst = mw.dst;
+    r.tmp = mw.tmp;
+    r.cb = t->mw_stepped ? cb : 0;
+    r.carry_n = mw_word(t, 4 + cur);
+    r.carry_dst = t->mw_carry_dst[cur].as<uint8_t>();
+    r.carry = t->mw_carry[cur].as<uint64_t>();
+    r.cap = out_cap;
+    r.out = (uint64_t*)out_slots;
+    r.carry_out = t->mw_carry[nxt].as<uint64_t>();
+    r.carry_dst_out = t->mw_carry_dst[nxt].as<uint8_t>();
+    r.carry_n_out = mw_word(t, 4 + nxt);
+    r.live = (unsigned long long*)dev_live;
+    r.pack = t->mw_pack.as<uint64_t>();
+    r.cnt = t->mw_cnt.as<uint64_t>();
+    KH_HIP(kh::launch_slot_round(r, t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
+                                 t->route_scratch.as<uint64_t>(), t->stream));
+    t->mw_cur = nxt;
+    t->mw_stepped = true;
+    return KH_OK;
+}
+
+int kh_mwalk_text_bound(kh_table* t, uint64_t* n_records) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (!n_records) return fail(KH_ERR_ARG, "null output");
+    *n_records = t->mw_store_bound;
+    return KH_OK;
+}
+
+int kh_mwalk_text_dev(kh_table* t, void* out, void* counts) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (int rc = join_succ(t)) return rc;
+    if (!counts || (t->mw_store_bound && !out)) return fail(KH_ERR_ARG, "null buffer");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = ensure_route(t, t->mw_store_bound, (int)t->mw_P)) return rc;
+    // the store's records (device count) grouped by origin; out holds kh_mwalk_text_bound records
+    KH_HIP(kh::launch_mw_group_text(t->mw_store.as<uint64_t>(), t->mw_store_bound, t->mw_P,
+                                    t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
+                                    t->route_scratch.as<uint64_t>(), (uint64_t*)out, (uint64_t*)counts, t->stream,
+                                    mw_word(t, 2)));
+    return KH_OK;
+}
+
+// the contig text bytes: at most K + 1 per contig + 32 per word record (no device read)
+static int text_for(kh_table* t, uint64_t nc, uint64_t word_recs) {
+    return t->text.ensure(nc * (uint64_t)(t->kp.K + 1) + 32 * word_recs + 64);
+}
+
+int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (t->ms_on && t->ms_nsp)
+        return fail(KH_ERR_STATE, "segmented walk: use kh_mwalk_link_dev .. kh_mwalk_end_seg_dev");
+    if (n && !recs) return fail(KH_ERR_ARG, "null records");
+    if (int rc = set_device(t)) return rc;
+    const uint64_t nc = t->ms_ns;
+    int rc;
+    if ((rc = t->contig_len.ensure((nc + 1) * 4)) || (rc = t->contig_off.ensure((nc + 1) * 8)) ||
+        (rc = t->scratch.ensure(kh::scan_scratch_words(nc) * 8 + 64)) || (rc = text_for(t, nc, n)))
+        return rc;
+    unsigned long long* ctr = t->ctr.as<unsigned long long>();
+    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
+    KH_HIP(hipMemsetD32Async((hipDeviceptr_t)t->contig_len.p, 1, nc + 1, t->stream));
+    KH_HIP(hipMemsetAsync(ctr + kh::CT_MW_FIN, 0, 8, t->stream));
+    KH_HIP(kh::launch_mw_lens((const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(), ctr + kh::CT_MW_FIN,
+                              t->stream));
+    // every walker came home (else kh_sync reports KH_ERR_NOT_FOUND)
+    KH_HIP(kh::launch_fin_check(ctr + kh::CT_MW_FIN, nc, nullptr, 0, t->stats.as<unsigned long long>(), t->stream));
+    KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
+                                     t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
+    if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
+    KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
+                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+    KH_HIP(kh::launch_mw_words(t->kp.K, (const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(),
+                               t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+    KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
+    t->walk_timed = true;
+    t->last_contigs = nc;
+    t->assembled = true;
+    t->mw_live = false;
     return KH_OK;
 }
 
@@ -1406,59 +1576,49 @@ int kh_mwalk_link_dev(kh_table* t, const void* recs, uint64_t n, void* out, void
     KH_HIP(hipMemsetAsync(fin, 0, 8, t->stream));
     const kh::MSegState st = mseg_state(t);
     KH_HIP(kh::launch_mseg_scan((const uint64_t*)recs, n, nseg, st, fin, t->stream));
-    uint64_t f = 0;
-    KH_HIP(hipMemcpyAsync(&f, fin, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_SYNC(t);
-    if (f != nseg)
-        return fail(KH_ERR_NOT_FOUND, "%llu of %llu walk segments did not finish (records lost in transit?)",
-                    (unsigned long long)(nseg - f), (unsigned long long)nseg);
-    KH_HIP(kh::launch_mseg_link(t->kp, st, nseg, t->mw_P, t->mw_rank, t->route_hist.as<uint64_t>(),
+    // every segment's walker came home (else kh_sync reports KH_ERR_NOT_FOUND)
+    KH_HIP(kh::launch_fin_check(fin, nseg, nullptr, 0, t->stats.as<unsigned long long>(), t->stream));
+    KH_HIP(kh::launch_mseg_link(t->kp, st, t->ms_ns, nseg, t->mw_P, t->mw_rank, t->route_hist.as<uint64_t>(),
                                 t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(), (uint64_t*)out,
                                 (uint64_t*)counts, t->stream));
     return KH_OK;
 }
 
-int kh_mwalk_pred_dev(kh_table* t, const void* links, uint64_t m) {
+int kh_mwalk_pred_dev(kh_table* t, const void* links, uint64_t m, void* preds_out, uint64_t stride) {
     if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
-    if (m && !links) return fail(KH_ERR_ARG, "null links");
+    if ((m && !links) || (stride && !preds_out)) return fail(KH_ERR_ARG, "null buffer");
+    if (stride < t->ms_nsp)
+        return fail(KH_ERR_ARG, "stride %llu below this rank's %llu splitter segments", (unsigned long long)stride,
+                    (unsigned long long)t->ms_nsp);
     if (int rc = set_device(t)) return rc;
+    const kh::MSegState st = mseg_state(t);
     KH_HIP(kh::launch_mseg_pred((const uint64_t*)links, m, t->ms_stab.as<uint64_t>(), t->ms_stab_id.as<uint32_t>(),
-                                t->ms_cap2, t->ms_ns, mseg_state(t), t->stats.as<unsigned long long>(), t->stream));
+                                t->ms_cap2, t->ms_ns, st, t->stats.as<unsigned long long>(), t->stream));
+    // nsp on the device: this rank's exact count (the host's, checked at begin)
+    unsigned long long* nsp = t->ms_misc.as<unsigned long long>() + 1;
+    KH_HIP(kh::launch_add_count(nsp, t->ms_nsp, nullptr, 0, t->stream));
+    KH_HIP(kh::launch_mseg_preds_out(st, t->ms_ns, nsp, t->ms_nsp, stride, (uint64_t*)preds_out, t->stream));
     return KH_OK;
 }
 
-int kh_mwalk_jump_emit_dev(kh_table* t, void* out, void* counts) {
+int kh_mwalk_resolve_dev(kh_table* t, const void* all_preds, uint64_t stride) {
     if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
-    if (!counts || (t->ms_nsp && !out)) return fail(KH_ERR_ARG, "null buffer");
+    const uint64_t N = (uint64_t)t->mw_P * stride;
+    if (N && !all_preds) return fail(KH_ERR_ARG, "null predecessor tables");
     if (int rc = set_device(t)) return rc;
-    if (int rc = ensure_route(t, t->ms_nsp, (int)t->mw_P)) return rc;
-    KH_HIP(kh::launch_mseg_jump_emit(mseg_state(t), t->ms_ns, t->ms_nsp, t->mw_P, t->route_hist.as<uint64_t>(),
-                                     t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(), (uint64_t*)out,
-                                     t->ms_qsrc.as<uint32_t>(), (uint64_t*)counts, t->stream));
-    return KH_OK;
-}
-
-int kh_mwalk_jump_answer_dev(kh_table* t, const void* queries, uint64_t m, void* replies) {
-    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
-    if (m && (!queries || !replies)) return fail(KH_ERR_ARG, "null buffer");
-    if (int rc = set_device(t)) return rc;
-    KH_HIP(kh::launch_mseg_jump_answer((const uint64_t*)queries, m, mseg_state(t), (uint64_t*)replies, t->stream));
-    return KH_OK;
-}
-
-int kh_mwalk_jump_apply_dev(kh_table* t, const void* replies, uint64_t m, uint64_t* pending) {
-    if (!t || !t->mw_live || !t->ms_on) return fail(KH_ERR_STATE, "no segmented migrating walk");
-    if (m && !replies) return fail(KH_ERR_ARG, "null buffer");
-    if (int rc = set_device(t)) return rc;
-    unsigned long long* left = t->ms_misc.as<unsigned long long>() + 1;
-    KH_HIP(kh::launch_mseg_jump_apply((const uint64_t*)replies, m, t->ms_qsrc.as<uint32_t>(), t->ms_ns,
-                                      mseg_state(t), left, t->stream));
-    if (pending) {  // optional: the next emit's counts already say whether any rank is pending
-        uint64_t l = 0;
-        KH_HIP(hipMemcpyAsync(&l, left, 8, hipMemcpyDeviceToHost, t->stream));
-        KH_SYNC(t);
-        *pending = l;
-    }
+    int rc;
+    const uint32_t np = kh::mseg_resolve_passes(N);
+    if ((rc = t->ms_res[0].ensure((N + 1) * 8)) || (rc = t->ms_res[1].ensure((N + 1) * 8)) ||
+        (rc = t->ms_res[2].ensure(N + 1)) || (rc = t->ms_res[3].ensure((N + 1) * 8)) ||
+        (rc = t->ms_res[4].ensure((N + 1) * 8)) || (rc = t->ms_res[5].ensure(N + 1)) ||
+        (rc = t->ms_pend.ensure((uint64_t)np * 8 + 8)))
+        return rc;
+    unsigned long long* nsp = t->ms_misc.as<unsigned long long>() + 1;
+    KH_HIP(kh::launch_mseg_resolve((const uint64_t*)all_preds, N, stride, t->mw_rank, t->ms_ns, nsp, t->ms_nsp,
+                                   mseg_state(t), t->ms_res[0].as<uint64_t>(), t->ms_res[1].as<uint64_t>(),
+                                   t->ms_res[2].as<uint8_t>(), t->ms_res[3].as<uint64_t>(),
+                                   t->ms_res[4].as<uint64_t>(), t->ms_res[5].as<uint8_t>(),
+                                   t->ms_pend.as<unsigned long long>(), t->stream));
     return KH_OK;
 }
 
@@ -1468,7 +1628,8 @@ int kh_mwalk_retag_dev(kh_table* t, const void* recs, uint64_t n, void* out, voi
     if (int rc = set_device(t)) return rc;
     if (int rc = ensure_route(t, n + t->ms_nsp, (int)t->mw_P)) return rc;
     const kh::MSegState st = mseg_state(t);
-    KH_HIP(kh::launch_mseg_check(t->ms_ns, t->ms_ns + t->ms_nsp, st, t->stats.as<unsigned long long>(), t->stream));
+    KH_HIP(kh::launch_mseg_check(t->ms_ns, t->ms_ns + t->ms_nsp, st, nullptr, t->stats.as<unsigned long long>(),
+                                 t->stream));
     KH_HIP(kh::launch_mseg_retag((const uint64_t*)recs, n, t->ms_ns, t->ms_nsp, st, t->mw_P,
                                  t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
                                  t->route_scratch.as<uint64_t>(), (uint64_t*)out, (uint64_t*)counts, t->stream));
@@ -1482,7 +1643,7 @@ int kh_mwalk_end_seg_dev(kh_table* t, const void* recs, uint64_t n, const void* 
     const uint64_t nc = t->ms_ns;
     int rc;
     if ((rc = t->contig_len.ensure((nc + 1) * 4)) || (rc = t->contig_off.ensure((nc + 1) * 8)) ||
-        (rc = t->scratch.ensure(kh::scan_scratch_words(nc) * 8 + 64)))
+        (rc = t->scratch.ensure(kh::scan_scratch_words(nc) * 8 + 64)) || (rc = text_for(t, nc, n + m)))
         return rc;
     unsigned long long* ctr = t->ctr.as<unsigned long long>();
     const kh::MSegState st = mseg_state(t);
@@ -1491,132 +1652,10 @@ int kh_mwalk_end_seg_dev(kh_table* t, const void* recs, uint64_t n, const void* 
     KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
                                      t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
     if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
-    uint64_t bytes = 0;
-    KH_HIP(hipMemcpyAsync(&bytes, ctr + kh::CT_OUT_BYTES, 8, hipMemcpyDeviceToHost, t->stream));
-    KH_SYNC(t);
-    if ((rc = t->text.ensure(bytes + 64))) return rc;
     KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
                                   t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
     KH_HIP(kh::launch_mseg_words(t->kp.K, (const uint64_t*)recs, n, (const uint64_t*)seg_recs, m, nc, st,
                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
-    KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
-    t->walk_timed = true;
-    t->last_contigs = nc;
-    t->assembled = true;
-    t->mw_live = false;
-    return KH_OK;
-}
-
-int kh_mwalk_round_dev(kh_table* t, const void* in, uint64_t n_in, void* out, void* counts) {
-    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
-    if (!counts) return fail(KH_ERR_ARG, "null counts");
-    const uint64_t* src = (const uint64_t*)in;
-    uint64_t n = n_in;
-    if (!t->mw_stepped) {
-        src = t->mw_init.as<uint64_t>();
-        n = t->rw_n;
-    } else if (n && !in) {
-        return fail(KH_ERR_ARG, "null input messages");
-    }
-    if (n && !out) return fail(KH_ERR_ARG, "null output messages");
-    if (int rc = set_device(t)) return rc;
-    int rc;
-    if ((rc = t->mw_tmp.ensure((n + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_dst.ensure(n + 1)) ||
-        (rc = t->mw_stage.ensure((n + 1) * kh::MW_REC_SLOTS * 16)) || (rc = t->mw_nrec.ensure(n + 1)) ||
-        (rc = t->mw_off.ensure((n + 1) * 8)) || (rc = t->scratch.ensure(kh::scan_scratch_words(n) * 8 + 64)) ||
-        (rc = ensure_route(t, n, (int)t->mw_P)))
-        return rc;
-    kh::MWalkRound mw;
-    mw.P = t->mw_P;
-    mw.rank = t->mw_rank;
-    mw.split_bits = t->ms_on ? (uint32_t)mseg_params(t).split_bits : 0u;
-    mw.headrec = t->headrec.as<uint64_t>();
-    mw.hcap = t->headrec.p ? t->hcap : 0u;
-    mw.max_steps = t->rw_total;
-    mw.in = src;
-    mw.n_in = n;
-    mw.tmp = t->mw_tmp.as<uint64_t>();
-    mw.dst = t->mw_dst.as<uint8_t>();
-    mw.stage = t->mw_stage.as<uint64_t>();
-    mw.nrec = t->mw_nrec.as<uint8_t>();
-    kh::KParams kp = t->kp;
-    if (!t->mw_hot) kp.hot = nullptr;
-    KH_HIP(kh::launch_mw_run(kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
-    // text records of this round -> the rank-local store at offsets continuing its device-side
-    // count: the store is sized from an upper bound (MW_REC_SLOTS per walker and round), so no
-    // host round trip per round; past a few GB of bound the actual count is read once
-    unsigned long long* store_n = t->mw_misc.as<unsigned long long>() + 2;
-    const uint64_t add = n * (uint64_t)kh::MW_REC_SLOTS;
-    if (t->mw_store_bound + add > (1ull << 28) && !t->mw_store_known) {
-        if ((rc = mw_store_count(t))) return rc;
-        t->mw_store_bound = t->mw_store_n;
-    }
-    if ((rc = grow_keep(t, t->mw_store, (t->mw_store_bound + add) * 16 + 16, t->mw_store_bound * 16)))
-        return rc;
-    KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), store_n, t->stream));
-    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>(), t->stream));
-    t->mw_store_bound += add;
-    t->mw_store_known = false;
-    KH_HIP(kh::launch_mw_group(mw, t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
-                               t->route_scratch.as<uint64_t>(), (uint64_t*)out, (uint64_t*)counts, t->stream));
-    t->mw_stepped = true;
-    return KH_OK;
-}
-
-int kh_mwalk_text_count(kh_table* t, uint64_t* n_records) {
-    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
-    if (!n_records) return fail(KH_ERR_ARG, "null output");
-    if (int rc = mw_store_count(t)) return rc;
-    *n_records = t->mw_store_n;
-    return KH_OK;
-}
-
-int kh_mwalk_text_dev(kh_table* t, void* out, void* counts) {
-    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
-    if (int rc = join_succ(t)) return rc;
-    if (int rc = mw_store_count(t)) return rc;
-    if (!counts || (t->mw_store_n && !out)) return fail(KH_ERR_ARG, "null buffer");
-    if (int rc = set_device(t)) return rc;
-    if (int rc = ensure_route(t, t->mw_store_n, (int)t->mw_P)) return rc;
-    KH_HIP(kh::launch_mw_group_text(t->mw_store.as<uint64_t>(), t->mw_store_n, t->mw_P, t->route_hist.as<uint64_t>(),
-                                    t->route_off.as<uint64_t>(), t->route_scratch.as<uint64_t>(), (uint64_t*)out,
-                                    (uint64_t*)counts, t->stream));
-    return KH_OK;
-}
-
-int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
-    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
-    if (t->ms_on && t->ms_nsp)
-        return fail(KH_ERR_STATE, "segmented walk: use kh_mwalk_link_dev .. kh_mwalk_end_seg_dev");
-    if (n && !recs) return fail(KH_ERR_ARG, "null records");
-    if (int rc = set_device(t)) return rc;
-    const uint64_t nc = t->rw_n;
-    int rc;
-    if ((rc = t->contig_len.ensure((nc + 1) * 4)) || (rc = t->contig_off.ensure((nc + 1) * 8)) ||
-        (rc = t->scratch.ensure(kh::scan_scratch_words(nc) * 8 + 64)))
-        return rc;
-    unsigned long long* ctr = t->ctr.as<unsigned long long>();
-    KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
-    KH_HIP(hipMemsetD32Async((hipDeviceptr_t)t->contig_len.p, 1, nc + 1, t->stream));
-    KH_HIP(hipMemsetAsync(ctr + kh::CT_MW_FIN, 0, 8, t->stream));
-    KH_HIP(kh::launch_mw_lens((const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(), ctr + kh::CT_MW_FIN,
-                              t->stream));
-    KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
-                                     t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
-    if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
-    uint64_t hv[3] = {0, 0, 0};
-    static_assert(kh::CT_MW_FIN == kh::CT_OUT_BYTES + 2, "counter layout");
-    KH_HIP(hipMemcpyAsync(hv, ctr + kh::CT_OUT_BYTES, 24, hipMemcpyDeviceToHost, t->stream));
-    KH_SYNC(t);
-    const uint64_t bytes = hv[0], fin = hv[2];
-    if (fin != nc)
-        return fail(KH_ERR_NOT_FOUND, "%llu of %llu walkers did not finish (records lost in transit?)",
-                    (unsigned long long)(nc - fin), (unsigned long long)nc);
-    if ((rc = t->text.ensure(bytes + 64))) return rc;
-    KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
-                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
-    KH_HIP(kh::launch_mw_words(t->kp.K, (const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(),
-                               t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = nc;

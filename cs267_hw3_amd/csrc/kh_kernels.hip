@@ -1145,11 +1145,11 @@ __device__ __forceinline__ uint32_t owner_mn(Key k, uint32_t mn, const KParams& 
 template <int KT>
 __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p_in, const uint8_t* __restrict__ recs, uint64_t n,
                                                      uint32_t P, uint32_t* own, uint64_t* hist,
-                                                     uint64_t* start_mask) {
+                                                     uint64_t* start_mask, unsigned long long* spl) {
     const KParams p = specialize<KT>(p_in);
-    __shared__ uint32_t h[MAX_RANKS];
+    __shared__ uint32_t h[MAX_RANKS], hs[MAX_RANKS];  // records / splitter k-mers per owner
     __shared__ __attribute__((aligned(16))) uint8_t st[BLOCK * 17 + 16];
-    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = 0;
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) h[q] = hs[q] = 0;
     __syncthreads();  // counters zeroed before any wave counts (records of <= 16 B take no barrier below)
     const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
     for (uint32_t j = 0; j < ROUTE_TILE / BLOCK; ++j) {
@@ -1162,7 +1162,9 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p_in, const uint8_t
         if (threadIdx.x < cnt) {
             const uint32_t mn = mini_scan(k, p);
             own[sub + threadIdx.x] = mn;
-            atomicAdd(&h[owner_mn(k, mn, p, P)], 1u);
+            const uint32_t q = owner_mn(k, mn, p, P);
+            atomicAdd(&h[q], 1u);
+            if (spl && ext_bwd(ext) != EXT_F && is_splitter(key_hash32(k), p)) atomicAdd(&hs[q], 1u);
         }
         if (start_mask) {  // kmer_hash.cpp:27-31 start bits, same pass (ROUTE_TILE is 64-aligned)
             const uint64_t bal = __ballot(threadIdx.x < cnt && ext_bwd(ext) == EXT_F);
@@ -1171,7 +1173,10 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p_in, const uint8_t
         }
     }
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) hist[(uint64_t)blockIdx.x * P + q] = h[q];
+    for (uint32_t q = threadIdx.x; q < P; q += BLOCK) {
+        hist[(uint64_t)blockIdx.x * P + q] = h[q];
+        if (spl && hs[q]) atomicAdd(&spl[q], (unsigned long long)hs[q]);
+    }
 }
 
 template <int W, int KT>
@@ -1206,14 +1211,15 @@ __global__ __launch_bounds__(BLOCK) void k_route_scatter(KParams p_in, const uin
 
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
                         uint64_t* hist, uint64_t* off, uint64_t* scratch, uint32_t* own, uint64_t* out_words,
-                        uint64_t* counts, hipStream_t s, uint64_t* start_mask) {
+                        uint64_t* counts, hipStream_t s, uint64_t* start_mask, unsigned long long* spl) {
+    if (!p.split_bits) spl = nullptr;
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
     const uint64_t nb = route_blocks(n);
     if (nb == 0) return hipMemsetAsync(counts, 0, (nranks + 1) * 8, s);
     if (p.W == 1)
-        with_kt<1>(p.K, [&](auto kt) { k_route_own<decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask); });
+        with_kt<1>(p.K, [&](auto kt) { k_route_own<decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask, spl); });
     else
-        with_kt<2>(p.K, [&](auto kt) { k_route_own<decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask); });
+        with_kt<2>(p.K, [&](auto kt) { k_route_own<decltype(kt)::value><<<(unsigned)nb, BLOCK, 0, s>>>(p, recs, n, nranks, own, hist, start_mask, spl); });
     hipError_t e = scan_exclusive(HistF{hist, nb, nranks}, nb * nranks, off, scratch + 1,
                                   (unsigned long long*)nullptr, total, s);
     if (e != hipSuccess) return e;

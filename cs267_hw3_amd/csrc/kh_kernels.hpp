@@ -152,7 +152,9 @@ struct MWalkRound {
     uint32_t split_bits = 0;  // > 0: walkers stop before splitter k-mers (kh_mseg.hip)
     uint64_t max_steps;
     const uint64_t* in;   // n_in messages
-    uint64_t n_in;
+    uint64_t n_in;        // bound (grids, buffers)
+    const unsigned long long* n_dev = nullptr;  // live inputs on the device (null: n_in)
+    const unsigned long long* hot_on = nullptr;  // ctr[CT_HOT]: remapped regions exist (null: use p.hot)
     uint64_t* tmp;        // n_in * MSG_WORDS: outgoing message of input j
     uint8_t* dst;         // n_in: its destination rank (0xFF = finished)
     uint64_t* stage;      // n_in * MW_REC_SLOTS * 2: text records of input j
@@ -181,19 +183,24 @@ hipError_t launch_mseg_stab(const KParams& p, const uint64_t* splits, uint64_t n
 hipError_t launch_mseg_init(uint64_t ns, uint64_t nseg, uint32_t rank, const MSegState& st, hipStream_t s);
 hipError_t launch_mseg_scan(const uint64_t* recs, uint64_t n, uint64_t nseg, const MSegState& st,
                             unsigned long long* fin, hipStream_t s);
-hipError_t launch_mseg_link(const KParams& p, const MSegState& st, uint64_t nseg, uint32_t P, uint32_t rank,
+hipError_t launch_mseg_link(const KParams& p, const MSegState& st, uint64_t ns, uint64_t nseg, uint32_t P, uint32_t rank,
                             uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out, uint64_t* counts,
                             hipStream_t s);
 hipError_t launch_mseg_pred(const uint64_t* msgs, uint64_t m, const uint64_t* stab, const uint32_t* id, uint64_t cap2,
                             uint64_t ns, const MSegState& st, unsigned long long* stats, hipStream_t s);
-hipError_t launch_mseg_jump_emit(const MSegState& st, uint64_t ns, uint64_t nsp, uint32_t P, uint64_t* hist,
-                                 uint64_t* off, uint64_t* scratch, uint64_t* out, uint32_t* qsrc, uint64_t* counts,
-                                 hipStream_t s);
-hipError_t launch_mseg_jump_answer(const uint64_t* q, uint64_t m, const MSegState& st, uint64_t* rep, hipStream_t s);
-hipError_t launch_mseg_jump_apply(const uint64_t* rep, uint64_t m, const uint32_t* qsrc, uint64_t ns,
-                                  const MSegState& st, unsigned long long* left, hipStream_t s);
-hipError_t launch_mseg_check(uint64_t ns, uint64_t nseg, const MSegState& st, unsigned long long* stats,
-                             hipStream_t s);
+// this rank's splitter segments' {predecessor id, predecessor length} (stride entries, the tail
+// past *nsp = none), for the all-gather of every rank's table
+hipError_t launch_mseg_preds_out(const MSegState& st, uint64_t ns, const unsigned long long* nsp, uint64_t nsp_max,
+                                 uint64_t stride, uint64_t* out, hipStream_t s);
+uint32_t mseg_resolve_passes(uint64_t N);
+// pointer jumping over the gathered tables (N = P * stride entries, buffers of N each, pend:
+// mseg_resolve_passes(N) words) -> head and offset of this rank's splitter segments
+hipError_t launch_mseg_resolve(const uint64_t* all, uint64_t N, uint64_t stride, uint32_t rank, uint64_t ns,
+                               const unsigned long long* nsp, uint64_t nsp_max, const MSegState& st, uint64_t* J0,
+                               uint64_t* A0, uint8_t* D0, uint64_t* J1, uint64_t* A1, uint8_t* D1,
+                               unsigned long long* pend, hipStream_t s);
+hipError_t launch_mseg_check(uint64_t ns, uint64_t nseg, const MSegState& st, const unsigned long long* nsp,
+                             unsigned long long* stats, hipStream_t s);
 hipError_t launch_mseg_retag(const uint64_t* recs, uint64_t n, uint64_t ns, uint64_t nsp, const MSegState& st,
                              uint32_t P, uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out,
                              uint64_t* counts, hipStream_t s);
@@ -203,6 +210,39 @@ hipError_t launch_mseg_words(int K, const uint64_t* recs, uint64_t n, const uint
                              const MSegState& st, const uint64_t* off, char* out, hipStream_t s);
 hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
                          hipStream_t s);
+// ---- fixed-size exchange slots (no host read per round) ----------------------------------------
+// A round's exchange buffer is P slots of slot_words(cap) words: [count, 0, cap messages].
+__host__ __device__ inline uint64_t slot_words(uint64_t cap) { return 2 + cap * MSG_WORDS; }
+// messages of P slots -> list (contiguous), *n = their number
+hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
+                              unsigned long long* n, hipStream_t s);
+// this round's outgoing messages (walk outputs j < *n_dev with a destination, then the messages
+// held back last round) -> P slots of cap (overflow held back in carry_out / carry_dst_out,
+// *carry_n_out); live = [messages in flight, largest per-destination count]. pack / cnt: scratch
+// of (nb + cb) messages / P + 1 words.
+struct SlotRound {
+    uint32_t P;
+    uint64_t nb;                     // walk outputs (bound)
+    const unsigned long long* n_dev; // walk outputs live
+    const uint8_t* dst;              // their destination (MW_NONE: finished)
+    const uint64_t* tmp;             // their messages
+    uint64_t cb;                     // held-back messages (bound)
+    const unsigned long long* carry_n;
+    const uint8_t* carry_dst;
+    const uint64_t* carry;
+    uint64_t cap;
+    uint64_t* out;                   // P slots
+    uint64_t* carry_out;
+    uint8_t* carry_dst_out;
+    unsigned long long* carry_n_out;
+    unsigned long long* live;        // 2 words
+    uint64_t* pack;                  // (nb + cb) * MSG_WORDS
+    uint64_t* cnt;                   // P + 1
+};
+hipError_t launch_slot_round(const SlotRound& r, uint64_t* hist, uint64_t* off, uint64_t* scratch, hipStream_t s);
+// *out = a + min(*b, bmax) (the first round's live walkers: starts + collected splitters)
+hipError_t launch_add_count(unsigned long long* out, uint64_t a, const unsigned long long* b, uint64_t bmax,
+                            hipStream_t s);
 // text records of this round: absolute store offsets continuing *store_n (device counter, updated)
 hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
                                   unsigned long long* store_n, hipStream_t s);
@@ -210,7 +250,11 @@ hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t
 hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, uint64_t* scratch,
                            uint64_t* out, uint64_t* counts, hipStream_t s);
 hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
-                                uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s);
+                                uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s,
+                                const unsigned long long* n_dev = nullptr);
+// *fin != want (+ *want_dev) -> stats[ST_MISSING] (walkers that never came home)
+hipError_t launch_fin_check(const unsigned long long* fin, uint64_t want, const unsigned long long* want_dev,
+                            uint64_t want_max, unsigned long long* stats, hipStream_t s);
 hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,
                           unsigned long long* fin, hipStream_t s);
 hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
@@ -249,7 +293,8 @@ hipError_t launch_start_mask(const KParams& p, const uint8_t* recs, uint64_t n, 
 // hist/off: route_blocks(n) * nranks words each; counts: nranks + 1 words (last = n).
 hipError_t launch_route(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t nranks,
                         uint64_t* hist, uint64_t* off, uint64_t* scratch, uint32_t* own, uint64_t* out_words,
-                        uint64_t* counts, hipStream_t s, uint64_t* start_mask = nullptr);
+                        uint64_t* counts, hipStream_t s, uint64_t* start_mask = nullptr,
+                        unsigned long long* spl = nullptr);
 
 // Insert routed internal words.
 hipError_t launch_insert_words(const KParams& p, const uint64_t* words, uint64_t m, TableView t,
@@ -333,9 +378,11 @@ hipError_t launch_part_stage_recs(const KParams& p, const uint8_t* recs, uint64_
                                   hipStream_t s, bool sample, uint64_t cap);
 // One-pass route of the sharded insert: owner q's words at words + q * win * W (win >= n, < 2^32),
 // counts[q] = their number, counts[P] = n; start bits into start_mask (kh_build.hip).
+// spl: splitter k-mers routed to each owner are added to spl[owner] (null: not counted)
 hipError_t launch_route_win(const KParams& p, const uint8_t* recs, uint64_t n, uint32_t P, uint64_t* words,
                             uint64_t win, uint32_t* cnt, uint64_t* counts, uint64_t* start_mask,
-                            unsigned long long* ctr, unsigned long long* stats, hipStream_t s);
+                            unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
+                            unsigned long long* spl = nullptr);
 hipError_t launch_part_finish(const KParams& p, uint64_t total, TableView t, bool table_empty,
                               const PartBuffers& b, unsigned long long* ctr, unsigned long long* stats,
                               hipStream_t s);

@@ -21,10 +21,18 @@
 namespace kh {
 
 static constexpr uint64_t GID_NONE = ~0ull;
+// segment ids: rank << 40 | index; a splitter segment's index is its splitter number with
+// GID_SPLIT set (start segments: the start's index), so every rank can place any rank's splitter
+// segment in the all-gathered predecessor table without knowing that rank's start count
+static constexpr uint64_t GID_SPLIT = 1ull << 39;
 
 __device__ __forceinline__ uint64_t gid_make(uint32_t rank, uint64_t idx) { return ((uint64_t)rank << 40) | idx; }
 __device__ __forceinline__ uint32_t gid_rank(uint64_t g) { return (uint32_t)(g >> 40); }
 __device__ __forceinline__ uint64_t gid_idx(uint64_t g) { return g & ((1ull << 40) - 1); }
+// local segment c (starts [0, ns), splitter segments ns + j) -> its id
+__device__ __forceinline__ uint64_t gid_seg(uint32_t rank, uint64_t c, uint64_t ns) {
+    return c < ns ? gid_make(rank, c) : gid_make(rank, GID_SPLIT | (c - ns));
+}
 
 // ---- splitter collection on the owner (routed words) ------------------------------------------
 // One chunk of SPLIT_CHUNK words per block; splitters are gathered in LDS and reserved in the
@@ -151,6 +159,7 @@ struct LinkOp {
     KParams p;
     MSegState st;
     uint32_t P, rank;
+    uint64_t ns;
     uint64_t* out;
     __device__ int owner(uint64_t i) const {
         if (!st.has_link[i]) return -1;
@@ -161,16 +170,16 @@ struct LinkOp {
         uint64_t* o = out + d * 4;
         o[0] = st.link_hi[i];
         o[1] = st.link_lo[i];
-        o[2] = gid_make(rank, i);
+        o[2] = gid_seg(rank, i, ns);
         o[3] = st.len[i];
     }
 };
 
-hipError_t launch_mseg_link(const KParams& p, const MSegState& st, uint64_t nseg, uint32_t P, uint32_t rank,
+hipError_t launch_mseg_link(const KParams& p, const MSegState& st, uint64_t ns, uint64_t nseg, uint32_t P, uint32_t rank,
                             uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out, uint64_t* counts,
                             hipStream_t s) {
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    return group_by_owner(LinkOp{p, st, P, rank, out}, nseg, P, hist, off, scratch + 1, counts, total, s);
+    return group_by_owner(LinkOp{p, st, P, rank, ns, out}, nseg, P, hist, off, scratch + 1, counts, total, s);
 }
 
 // Owner of each linked splitter: its segment's predecessor; then the jump state of every segment.
@@ -211,68 +220,90 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_init(uint64_t ns, uint64_t nseg,
     }
 }
 
-// ---- pointer jumping -------------------------------------------------------------------------------
-// query: 1 word = target's local index; the requester of send position d is qsrc[d]
-struct JumpOp {
-    MSegState st;
-    uint64_t ns;
-    uint64_t* out;
-    uint32_t* qsrc;
-    __device__ int owner(uint64_t i) const {
-        const uint64_t g = ns + i;
-        if (st.done[g] || st.jump[g] == GID_NONE) return -1;
-        return (int)gid_rank(st.jump[g]);
+// ---- pointer jumping (Wyllie list ranking) over every rank's splitter segments --------------------
+// After the links, each rank knows the predecessor {id, length} of its own splitter segments. Those
+// tables are all-gathered (rank q's at q * stride, stride = the largest per-rank count), and every
+// rank ranks the whole set on its device: log2(segments per chain) passes over the gathered table
+// with no exchange per pass (the exchanged query/reply rounds of the earlier protocol needed a
+// host round trip each). A pass whose predecessor found nothing pending returns at once, so the
+// host launches enough passes for any chain without reading when they are done.
+__global__ __launch_bounds__(BLOCK) void k_mseg_preds_out(MSegState st, uint64_t ns, const unsigned long long* nsp,
+                                                          uint64_t nsp_max, uint64_t stride, uint64_t* out) {
+    const uint64_t n = min((uint64_t)*nsp, nsp_max);
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < stride; j += (uint64_t)gridDim.x * BLOCK) {
+        const bool live = j < n;
+        out[2 * j] = live ? st.jump[ns + j] : GID_NONE;
+        out[2 * j + 1] = live ? st.acc[ns + j] : 0;
     }
-    __device__ void emit(uint64_t i, int q, uint64_t d) const {
-        if (q < 0) return;
-        out[d] = gid_idx(st.jump[ns + i]);
-        qsrc[d] = (uint32_t)i;
-    }
+}
+
+struct ResBuf {
+    uint64_t* J;   // pointer: predecessor id, then the id it jumped to; when done: the head (a start)
+    uint64_t* A;   // bases from the start of J's segment to this segment's start
+    uint8_t* D;    // J is the contig's start segment
 };
 
-hipError_t launch_mseg_jump_emit(const MSegState& st, uint64_t ns, uint64_t nsp, uint32_t P, uint64_t* hist,
-                                 uint64_t* off, uint64_t* scratch, uint64_t* out, uint32_t* qsrc, uint64_t* counts,
-                                 hipStream_t s) {
-    unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    return group_by_owner(JumpOp{st, ns, out, qsrc}, nsp, P, hist, off, scratch + 1, counts, total, s);
-}
-
-// reply: [done, done ? head gid : next jump, done ? offset : accumulated bases]
-__global__ __launch_bounds__(BLOCK) void k_mseg_jump_answer(const uint64_t* q, uint64_t m, MSegState st, uint64_t* rep) {
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t j = q[i];
-        rep[3 * i] = st.done[j];
-        rep[3 * i + 1] = st.jump[j];
-        rep[3 * i + 2] = st.acc[j];
+__global__ __launch_bounds__(BLOCK) void k_res_init(const uint64_t* all, uint64_t N, ResBuf b) {
+    for (uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; g < N; g += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t j = all[2 * g];
+        b.J[g] = j;
+        b.A[g] = all[2 * g + 1];
+        b.D[g] = (j != GID_NONE && !(gid_idx(j) & GID_SPLIT)) ? 1 : 0;
     }
 }
 
-// apply the replies (synchronous Wyllie step: answers were computed from the pre-round state)
-__global__ __launch_bounds__(BLOCK) void k_mseg_jump_apply(const uint64_t* rep, uint64_t m, const uint32_t* qsrc,
-                                                           uint64_t ns, MSegState st, unsigned long long* left) {
-    uint64_t l = 0;
-    for (uint64_t d = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; d < m; d += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t g = ns + qsrc[d];
-        const uint64_t done = rep[3 * d], nx = rep[3 * d + 1], a = rep[3 * d + 2];
-        if (done) {  // target knows its head: offset of g = bases before the target + target's offset
-            st.jump[g] = nx;
-            st.acc[g] += a;
-            st.done[g] = 1;
-        } else {
-            st.jump[g] = nx;
-            st.acc[g] += a;
-            l += nx != GID_NONE ? 1 : 0;
+// pass k: in -> out; pend[k] = entries still pending after it (pass k returns at once when pass
+// k - 1 left none: the last written buffer is final)
+__global__ __launch_bounds__(BLOCK) void k_res_pass(uint32_t k, ResBuf in, ResBuf out, uint64_t N, uint64_t stride,
+                                                    unsigned long long* pend) {
+    if (k > 0 && pend[k - 1] == 0) return;
+    uint64_t left = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; g < N; g += (uint64_t)gridDim.x * BLOCK) {
+        uint64_t j = in.J[g], a = in.A[g];
+        uint8_t d = in.D[g];
+        if (!d && j != GID_NONE) {
+            const uint64_t t = (uint64_t)gid_rank(j) * stride + (gid_idx(j) & ~GID_SPLIT);
+            if (t < N) {
+                const uint64_t jt = in.J[t];
+                a += in.A[t];
+                d = in.D[t];
+                j = jt;  // a broken predecessor (GID_NONE, not done) breaks this chain too
+            } else {
+                j = GID_NONE;
+            }
+            left += (!d && j != GID_NONE) ? 1 : 0;
         }
+        out.J[g] = j;
+        out.A[g] = a;
+        out.D[g] = d;
     }
     uint64_t tot;
-    block_excl_scan(l, tot);
-    if (threadIdx.x == 0 && tot) atomicAdd(left, (unsigned long long)tot);
+    block_excl_scan(left, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(&pend[k], (unsigned long long)tot);
+}
+
+// this rank's splitter segments <- the final buffer (the output of the first pass that left
+// nothing pending)
+__global__ __launch_bounds__(BLOCK) void k_res_apply(ResBuf b0, ResBuf b1, const unsigned long long* pend, uint32_t npass,
+                                                     uint32_t rank, uint64_t stride, uint64_t ns,
+                                                     const unsigned long long* nsp, uint64_t nsp_max, MSegState st) {
+    uint32_t k = 0;
+    while (k + 1 < npass && pend[k] != 0) ++k;
+    const ResBuf& f = (k & 1) ? b0 : b1;  // pass k writes buffer (k + 1) % 2
+    const uint64_t n = min((uint64_t)*nsp, nsp_max);
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t g = (uint64_t)rank * stride + j;
+        st.done[ns + j] = f.D[g];
+        st.jump[ns + j] = f.J[g];
+        st.acc[ns + j] = f.A[g];
+    }
 }
 
 // splitter segments whose head was never found (a broken chain: a missing k-mer upstream)
-__global__ __launch_bounds__(BLOCK) void k_mseg_check(uint64_t ns, uint64_t nseg, MSegState st,
-                                                      unsigned long long* stats) {
+__global__ __launch_bounds__(BLOCK) void k_mseg_check(uint64_t ns, uint64_t nseg_max, MSegState st,
+                                                      const unsigned long long* nsp, unsigned long long* stats) {
     uint64_t bad = 0;
+    const uint64_t nseg = nsp ? min(ns + (uint64_t)*nsp, nseg_max) : nseg_max;
     for (uint64_t i = ns + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg; i += (uint64_t)gridDim.x * BLOCK)
         bad += st.done[i] ? 0 : 1;
     uint64_t tot;
@@ -280,10 +311,10 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_check(uint64_t ns, uint64_t nseg
     if (threadIdx.x == 0 && tot) atomicAdd(&stats[ST_MISSING], (unsigned long long)tot);
 }
 
-hipError_t launch_mseg_check(uint64_t ns, uint64_t nseg, const MSegState& st, unsigned long long* stats,
-                             hipStream_t s) {
+hipError_t launch_mseg_check(uint64_t ns, uint64_t nseg, const MSegState& st, const unsigned long long* nsp,
+                             unsigned long long* stats, hipStream_t s) {
     if (nseg <= ns) return hipSuccess;
-    k_mseg_check<<<(unsigned)hmin((nseg - ns + BLOCK - 1) / BLOCK, 1024), BLOCK, 0, s>>>(ns, nseg, st, stats);
+    k_mseg_check<<<(unsigned)hmin((nseg - ns + BLOCK - 1) / BLOCK, 1024), BLOCK, 0, s>>>(ns, nseg, st, nsp, stats);
     return hipGetLastError();
 }
 
@@ -417,17 +448,34 @@ hipError_t launch_mseg_init(uint64_t ns, uint64_t nseg, uint32_t rank, const MSe
     return hipGetLastError();
 }
 
-hipError_t launch_mseg_jump_answer(const uint64_t* q, uint64_t m, const MSegState& st, uint64_t* rep, hipStream_t s) {
-    if (m == 0) return hipSuccess;
-    k_mseg_jump_answer<<<grid_n(m, 4096), BLOCK, 0, s>>>(q, m, st, rep);
+hipError_t launch_mseg_preds_out(const MSegState& st, uint64_t ns, const unsigned long long* nsp, uint64_t nsp_max,
+                                 uint64_t stride, uint64_t* out, hipStream_t s) {
+    if (stride == 0) return hipSuccess;
+    k_mseg_preds_out<<<grid_n(stride, 4096), BLOCK, 0, s>>>(st, ns, nsp, nsp_max, stride, out);
     return hipGetLastError();
 }
 
-hipError_t launch_mseg_jump_apply(const uint64_t* rep, uint64_t m, const uint32_t* qsrc, uint64_t ns,
-                                  const MSegState& st, unsigned long long* left, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(left, 0, 8, s);
-    if (e != hipSuccess || m == 0) return e;
-    k_mseg_jump_apply<<<grid_n(m, 4096), BLOCK, 0, s>>>(rep, m, qsrc, ns, st, left);
+// passes for any chain of <= N segments: pointer jumping halves the distance to the head each pass
+uint32_t mseg_resolve_passes(uint64_t N) {
+    uint32_t k = 1;
+    while (k < 62 && (1ull << (k - 1)) < N + 1) ++k;
+    return k + 1;
+}
+
+hipError_t launch_mseg_resolve(const uint64_t* all, uint64_t N, uint64_t stride, uint32_t rank, uint64_t ns,
+                               const unsigned long long* nsp, uint64_t nsp_max, const MSegState& st, uint64_t* J0,
+                               uint64_t* A0, uint8_t* D0, uint64_t* J1, uint64_t* A1, uint8_t* D1,
+                               unsigned long long* pend, hipStream_t s) {
+    const uint32_t np = mseg_resolve_passes(N);
+    hipError_t e = hipMemsetAsync(pend, 0, np * 8, s);
+    if (e != hipSuccess) return e;
+    const ResBuf b0{J0, A0, D0}, b1{J1, A1, D1};
+    if (N) {
+        k_res_init<<<grid_n(N, 4096), BLOCK, 0, s>>>(all, N, b0);
+        for (uint32_t k = 0; k < np; ++k)
+            k_res_pass<<<grid_n(N, 4096), BLOCK, 0, s>>>(k, (k & 1) ? b1 : b0, (k & 1) ? b0 : b1, N, stride, pend);
+        k_res_apply<<<grid_n(nsp_max, 4096), BLOCK, 0, s>>>(b0, b1, pend, np, rank, stride, ns, nsp, nsp_max, st);
+    }
     return hipGetLastError();
 }
 

@@ -36,8 +36,10 @@ __device__ __forceinline__ uint64_t rec_tag(uint32_t origin, bool fin, uint64_t 
 template <int W, int KT>
 __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
                                                   MWalkRound mw, unsigned long long* stats) {
-    const KParams p = specialize<KT>(p_in);
+    KParams p = specialize<KT>(p_in);
+    if (mw.hot_on && *mw.hot_on == 0) p.hot = nullptr;  // no remapped region: skip the bitmap loads
     const bool chains = p.chain && mw.hcap != 0;
+    const uint64_t n_live = mw.n_dev ? (uint64_t)*mw.n_dev : mw.n_in;
     const uint32_t q4 = lane_id() & 3u, ql4 = lane_id() & ~3u;  // quad member, quad's first lane
     uint32_t reg = 0;  // region of the k-mer being probed (its head records live there)
     // append n bases (base i at bits 2i of piece, n <= room in the current word) to the walker's
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
         mw.dst[jj] = MW_NONE;
     };
     while (true) {
-        if (!active && j < mw.n_in) {
+        if (!active && j < n_live) {
             const uint64_t* m = mw.in + j * MSG_WORDS;
             k.hi = m[0];
             k.lo = m[1];
@@ -301,11 +303,14 @@ __global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p_in, const uint64_t*
 
 struct NrecF {
     const uint8_t* n;
-    __device__ uint64_t operator()(uint64_t i) const { return n[i]; }
+    const unsigned long long* n_dev;  // inputs past the live count wrote nothing
+    __device__ uint64_t operator()(uint64_t i) const { return (!n_dev || i < *n_dev) ? n[i] : 0u; }
 };
 
 __global__ __launch_bounds__(BLOCK) void k_mw_compact(const uint64_t* stage, const uint8_t* nrec,
-                                                      const uint64_t* off, uint64_t n, uint64_t* store) {
+                                                      const uint64_t* off, uint64_t nb, uint64_t* store,
+                                                      const unsigned long long* n_dev) {
+    const uint64_t n = n_dev ? min((uint64_t)*n_dev, nb) : nb;
     for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
         const uint32_t c = nrec[j];
         const ulonglong2* src = reinterpret_cast<const ulonglong2*>(stage + j * (MW_REC_SLOTS * 2));
@@ -331,9 +336,10 @@ struct MsgOp {
 struct RecOp {
     const uint64_t* recs;
     uint64_t* out;
-    __device__ int owner(uint64_t i) const { return (int)(recs[2 * i] >> 56); }
+    const unsigned long long* n_dev;  // records past the live count do not exist (null: all)
+    __device__ int owner(uint64_t i) const { return (n_dev && i >= *n_dev) ? -1 : (int)(recs[2 * i] >> 56); }
     __device__ void emit(uint64_t i, int q, uint64_t d) const {
-        (void)q;
+        if (q < 0) return;  // past the live count
         reinterpret_cast<ulonglong2*>(out)[d] = reinterpret_cast<const ulonglong2*>(recs)[i];
     }
 };
@@ -413,12 +419,12 @@ hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t*
                                   unsigned long long* store_n, hipStream_t s) {
     if (mw.n_in == 0) return hipSuccess;
     // offsets continue the store's running count (store_n, on the device: no host round trip)
-    return scan_exclusive(NrecF{mw.nrec}, mw.n_in, off, scratch, store_n, (unsigned long long*)nullptr, s);
+    return scan_exclusive(NrecF{mw.nrec, mw.n_dev}, mw.n_in, off, scratch, store_n, (unsigned long long*)nullptr, s);
 }
 
 hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, hipStream_t s) {
     if (mw.n_in == 0) return hipSuccess;
-    k_mw_compact<<<grid_for(mw.n_in, 8192), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store);
+    k_mw_compact<<<grid_for(mw.n_in, 8192), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store, mw.n_dev);
     return hipGetLastError();
 }
 
@@ -429,9 +435,145 @@ hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, 
 }
 
 hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
-                                uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s) {
+                                uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s,
+                                const unsigned long long* n_dev) {
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    return group_by_owner(RecOp{recs, out}, n, P, hist, off, scratch + 1, counts, total, s);
+    return group_by_owner(RecOp{recs, out, n_dev}, n, P, hist, off, scratch + 1, counts, total, s);
+}
+
+// ---- fixed-size exchange slots ---------------------------------------------------------------------
+// prefix of the P slot counts (clamped to cap) in LDS; returns the total
+__device__ __forceinline__ uint64_t slot_prefix(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* pre) {
+    __shared__ uint64_t tot;
+    if (threadIdx.x == 0) {
+        uint64_t a = 0;
+        for (uint32_t q = 0; q < P; ++q) {
+            pre[q] = a;
+            const uint64_t c = slots[q * slot_words(cap)];
+            a += c < cap ? c : cap;
+        }
+        pre[P] = a;
+        tot = a;
+    }
+    __syncthreads();
+    return tot;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
+                                                       unsigned long long* n) {
+    __shared__ uint64_t pre[MAX_RANKS + 1];
+    const uint64_t tot = slot_prefix(slots, P, cap, pre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n = tot;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * BLOCK) {
+        uint32_t q = 0;
+        while (q + 1 < P && pre[q + 1] <= i) ++q;
+        const uint64_t* src = slots + q * slot_words(cap) + 2 + (i - pre[q]) * MSG_WORDS;
+        uint64_t* d = list + i * MSG_WORDS;
+#pragma unroll
+        for (int w = 0; w < MSG_WORDS; ++w) d[w] = src[w];
+    }
+}
+
+hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
+                              unsigned long long* n, hipStream_t s) {
+    k_slot_gather<<<grid_for((uint64_t)P * cap, 4096), BLOCK, 0, s>>>(slots, P, cap, list, n);
+    return hipGetLastError();
+}
+
+// outgoing messages of a round: last round's held-back ones first (they go out before newer
+// ones to the same destination), then the walk outputs with a destination
+struct SlotMsgOp {
+    SlotRound r;
+    __device__ int owner(uint64_t i) const {
+        if (i < r.cb) return i < *r.carry_n ? (int)r.carry_dst[i] : -1;
+        const uint64_t j = i - r.cb;
+        return (j < *r.n_dev && r.dst[j] != MW_NONE) ? (int)r.dst[j] : -1;
+    }
+    __device__ void emit(uint64_t i, int q, uint64_t d) const {
+        if (q < 0) return;
+        const uint64_t* a = i < r.cb ? r.carry + i * MSG_WORDS : r.tmp + (i - r.cb) * MSG_WORDS;
+        uint64_t* b = r.pack + d * MSG_WORDS;
+#pragma unroll
+        for (int w = 0; w < MSG_WORDS; ++w) b[w] = a[w];
+    }
+};
+
+// packed (grouped by destination, cnt[P+1]) -> slots of cap; the rest is held back for the next round
+__global__ __launch_bounds__(BLOCK) void k_slot_pack(SlotRound r) {
+    __shared__ uint64_t pre[MAX_RANKS + 1];
+    if (threadIdx.x == 0) {
+        uint64_t a = 0;
+        for (uint32_t q = 0; q < r.P; ++q) {
+            pre[q] = a;
+            a += r.cnt[q];
+        }
+        pre[r.P] = a;
+    }
+    __syncthreads();
+    const uint64_t tot = pre[r.P];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < r.P) {
+            const uint64_t c = r.cnt[threadIdx.x];
+            r.out[threadIdx.x * slot_words(r.cap)] = c < r.cap ? c : r.cap;
+            r.out[threadIdx.x * slot_words(r.cap) + 1] = 0;
+        }
+        if (threadIdx.x == 0) {
+            uint64_t mx = 0;
+            for (uint32_t q = 0; q < r.P; ++q) mx = r.cnt[q] > mx ? r.cnt[q] : mx;
+            r.live[0] = tot;
+            r.live[1] = mx;
+        }
+    }
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * BLOCK) {
+        uint32_t q = 0;
+        while (q + 1 < r.P && pre[q + 1] <= i) ++q;
+        const uint64_t k = i - pre[q];
+        const uint64_t* a = r.pack + i * MSG_WORDS;
+        uint64_t* b;
+        if (k < r.cap) {
+            b = r.out + q * slot_words(r.cap) + 2 + k * MSG_WORDS;
+        } else {  // slot full: held back (rare; carry capacity = every message of the round)
+            const unsigned long long c = atomicAdd(r.carry_n_out, 1ull);
+            b = r.carry_out + c * MSG_WORDS;
+            r.carry_dst_out[c] = (uint8_t)q;
+        }
+#pragma unroll
+        for (int w = 0; w < MSG_WORDS; ++w) b[w] = a[w];
+    }
+}
+
+hipError_t launch_slot_round(const SlotRound& r, uint64_t* hist, uint64_t* off, uint64_t* scratch, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(r.carry_n_out, 0, 8, s);
+    if (e != hipSuccess) return e;
+    unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
+    if ((e = group_by_owner(SlotMsgOp{r}, r.nb + r.cb, r.P, hist, off, scratch + 1, r.cnt, total, s)) != hipSuccess)
+        return e;
+    k_slot_pack<<<grid_for(r.nb + r.cb, 4096), BLOCK, 0, s>>>(r);
+    return hipGetLastError();
+}
+
+__global__ void k_add_count(unsigned long long* out, uint64_t a, const unsigned long long* b, uint64_t bmax) {
+    const uint64_t v = b ? (uint64_t)*b : 0;
+    *out = a + (v < bmax ? v : bmax);
+}
+
+hipError_t launch_add_count(unsigned long long* out, uint64_t a, const unsigned long long* b, uint64_t bmax,
+                            hipStream_t s) {
+    k_add_count<<<1, 1, 0, s>>>(out, a, b, bmax);
+    return hipGetLastError();
+}
+
+__global__ void k_fin_check(const unsigned long long* fin, uint64_t want, const unsigned long long* want_dev,
+                            uint64_t want_max, unsigned long long* stats) {
+    uint64_t w = want;
+    if (want_dev) w += (uint64_t)*want_dev < want_max ? (uint64_t)*want_dev : want_max;
+    if ((uint64_t)*fin != w) atomicAdd(&stats[ST_MISSING], 1ull);
+}
+
+hipError_t launch_fin_check(const unsigned long long* fin, uint64_t want, const unsigned long long* want_dev,
+                            uint64_t want_max, unsigned long long* stats, hipStream_t s) {
+    k_fin_check<<<1, 1, 0, s>>>(fin, want, want_dev, want_max, stats);
+    return hipGetLastError();
 }
 
 hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len, unsigned long long* fin,

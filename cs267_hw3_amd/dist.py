@@ -90,6 +90,18 @@ class TorchComm:
     def barrier(self):
         self.dist.barrier(group=self.group)
 
+    def all_gather(self, out, inp):
+        """Equal-size blocks: rank q's inp lands at out[q * inp.numel() ...]."""
+        if self.backend == "nccl":
+            self.dist.all_gather_into_tensor(out, inp, group=self.group)
+        else:
+            self.dist.all_gather(list(out.view(self.world, -1).unbind(0)), inp, group=self.group)
+
+    def max_to_host(self, t):
+        """Element-wise max over ranks of a small int64 tensor, read on the host (ONE device read)."""
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return t.cpu()
+
     def all_reduce_max(self, x):
         t = torch.tensor([float(x)], dtype=torch.float64)
         if self.dist.get_backend(self.group) == "nccl":
@@ -174,6 +186,24 @@ class ThreadComm:
 
     def barrier(self):
         self.sh.barrier.wait()
+
+    def all_gather(self, out, inp):
+        self._sync(inp)
+        self.sh.slots[self.rank] = inp
+        self.sh.barrier.wait()
+        n = inp.numel()
+        for q in range(self.world):
+            out[q * n:(q + 1) * n].copy_(self.sh.slots[q])
+        self._sync(out)
+        self.sh.barrier.wait()
+
+    def max_to_host(self, t):
+        h = t.cpu()
+        self.sh.slots[self.rank] = h
+        self.sh.barrier.wait()
+        m = torch.stack(list(self.sh.slots)).max(0).values
+        self.sh.barrier.wait()
+        return m
 
     def all_reduce_max(self, x):
         self.sh.slots[self.rank] = x
@@ -263,25 +293,42 @@ class GpuShard:
     def finish_words(self):
         check(self.L.kh_insert_words_finish(self.h))
 
-    # migrating-walker rounds
+    def counters(self):
+        """[start k-mers, splitter k-mers] collected so far (device int64[2], async)."""
+        out = self.zeros(2, torch.int64)
+        check(self.L.kh_counters_dev(self.h, self._p(out)))
+        return out
+
+    def route_splitters(self, nranks):
+        """Splitter k-mers this rank's routes sent to each owner (device int64[P], async)."""
+        out = self.zeros(nranks, torch.int64)
+        check(self.L.kh_route_splitters_dev(self.h, self._p(out), nranks))
+        return out
+
+    def host_syncs(self):
+        v = ctypes.c_uint64(0)
+        check(self.L.kh_host_syncs(self.h, ctypes.byref(v)))
+        return v.value
+
+    # migrating-walker rounds (fixed-size exchange slots: no device read per round)
     MSG_WORDS = _lib.MSG_WORDS
     TEXT_REC_WORDS = _lib.TEXT_REC_WORDS
 
-    def mw_begin(self, nranks, rank, total_kmers):
+    def mw_begin(self, nranks, rank, total_kmers, n_starts, n_splitters, total_walkers):
         nw = ctypes.c_uint64(0)
-        check(self.L.kh_mwalk_begin(self.h, nranks, rank, total_kmers, ctypes.byref(nw)))
+        check(self.L.kh_mwalk_begin(self.h, nranks, rank, total_kmers, n_starts, n_splitters, total_walkers,
+                                    ctypes.byref(nw)))
         self.nranks = nranks
         return nw.value
 
-    def mw_round(self, inp, n_in, out):
-        counts = self.zeros(self.nranks + 1, torch.int64)
-        check(self.L.kh_mwalk_round_dev(self.h, self._p(inp) if inp is not None else None, n_in,
-                                        self._p(out), self._p(counts)))
-        return counts
+    def mw_round(self, inp, cap_in, out, cap_out, live):
+        """inp: the received slots (None: the first round); out: P slots of cap_out; live: int64[2]."""
+        check(self.L.kh_mwalk_round_dev(self.h, self._p(inp) if inp is not None else None, cap_in, self._p(out),
+                                        cap_out, self._p(live)))
 
-    def mw_text_count(self):
+    def mw_text_bound(self):
         v = ctypes.c_uint64(0)
-        check(self.L.kh_mwalk_text_count(self.h, ctypes.byref(v)))
+        check(self.L.kh_mwalk_text_bound(self.h, ctypes.byref(v)))
         return v.value
 
     def mw_text(self, out):
@@ -294,7 +341,7 @@ class GpuShard:
 
     # splitter segments of the migrating walk (kh_mseg.hip)
     LINK_WORDS = _lib.LINK_WORDS
-    JUMP_REPLY_WORDS = _lib.JUMP_REPLY_WORDS
+    PRED_WORDS = _lib.PRED_WORDS
     SEG_REC_WORDS = _lib.SEG_REC_WORDS
 
     def mw_segments(self):
@@ -307,20 +354,11 @@ class GpuShard:
         check(self.L.kh_mwalk_link_dev(self.h, self._p(recs), n, self._p(out), self._p(counts)))
         return counts
 
-    def mw_pred(self, links, m):
-        check(self.L.kh_mwalk_pred_dev(self.h, self._p(links), m))
+    def mw_pred(self, links, m, preds, stride):
+        check(self.L.kh_mwalk_pred_dev(self.h, self._p(links), m, self._p(preds), stride))
 
-    def mw_jump_emit(self, out):
-        counts = self.zeros(self.nranks + 1, torch.int64)
-        check(self.L.kh_mwalk_jump_emit_dev(self.h, self._p(out), self._p(counts)))
-        return counts
-
-    def mw_jump_answer(self, queries, m, out):
-        check(self.L.kh_mwalk_jump_answer_dev(self.h, self._p(queries), m, self._p(out)))
-
-    def mw_jump_apply(self, replies, m):
-        # no pending count: the next emit's exchanged counts end the loop (no host sync here)
-        check(self.L.kh_mwalk_jump_apply_dev(self.h, self._p(replies), m, None))
+    def mw_resolve(self, all_preds, stride):
+        check(self.L.kh_mwalk_resolve_dev(self.h, self._p(all_preds), stride))
 
     def mw_retag(self, recs, n, out):
         counts = self.zeros(self.nranks + 1, torch.int64)
@@ -355,42 +393,59 @@ class DistributedKmerHashMap:
         self.shard = shard
         self.P = comm.world
         self.rounds = 0
-        self.jump_rounds = 0
+        self.checks = 0
+        self.syncs = 0          # host reads of device data by this host since the last reset
+        self._caps = []         # per-round slot capacities learnt from the last assemble
+        self._rounds_hint = 0   # its round count (the next assemble checks for the end there first)
 
     def close(self):
         pass
 
+    def host_syncs(self):
+        """Blocking device reads so far: this host's plus the shard library's own (kh_host_syncs)."""
+        lib = self.shard.host_syncs() if hasattr(self.shard, "host_syncs") else 0
+        return self.syncs + lib
+
+    def _host(self, t):
+        """A device tensor read on the host: one blocking round trip (counted)."""
+        self.syncs += 1
+        return t.cpu()
+
     def _int64(self, like, n):
         return torch.empty(max(int(n), 1), dtype=torch.int64, device=like.device)
 
-    # RCCL as shipped with this torch build corrupts all_to_all_single messages of >= 2 GiB per
-    # peer (tools/dbg_a2a.py: half the elements wrong at 2.0 and 3.2 GiB, exact at 1 GiB), so no
-    # single call moves more than A2A_CHUNK_BYTES per peer.
+    # One-rank self send/recv through RCCL loses everything past the first half of a message of
+    # >= 2 GiB - 8 B (tools/rccl_big_msg.cpp and .py; profiles/r04/rccl_big_msg: RCCL 2.27.7 and
+    # torch's 2.26.6, equal and split all_to_all and grouped send/recv alike; exact at 1 GiB), so
+    # no single call moves more than A2A_CHUNK_BYTES per peer.
     A2A_CHUNK_BYTES = int(os.environ.get("KH_A2A_CHUNK_MB", "512")) << 20
     # one rank: exchanges are skipped (KH_DIST_SELF_EXCHANGE=1 runs them anyway, for tests), and the
     # records go straight into the records pass (KH_DIST_ROUTE_ONE_RANK=1 routes them anyway)
     SELF_EXCHANGE = os.environ.get("KH_DIST_SELF_EXCHANGE") == "1"
     ROUTE_ONE_RANK = os.environ.get("KH_DIST_ROUTE_ONE_RANK") == "1"
 
-    def _exchange_counts(self, counts, elems_per_item=1):
+    def _exchange_counts(self, counts, extra=None):
         """counts: [P+1] int64 (per-destination, total) -> (send_splits, recv_splits, totals,
-        global max per-peer split). One small all-to-all; each rank also learns every rank's
-        total (global termination) and largest split (chunk count), no extra all-reduce."""
+        global max per-peer split, extras). One small all-to-all and ONE host read; each rank also
+        learns every rank's total and largest split (chunk count), and `extra` (a device int64
+        scalar of this rank, e.g. its splitter count) of every rank."""
         P = self.P
         mx = counts[:P].max().reshape(1)
-        send = torch.stack([counts[:P], counts[P:P + 1].expand(P), mx.expand(P)], 1)
+        ex = extra.reshape(1) if extra is not None else mx.new_zeros(1)
+        send = torch.stack([counts[:P], counts[P:P + 1].expand(P), mx.expand(P), ex.expand(P)], 1)
         send = send.contiguous().view(-1)
         if P == 1 and not self.SELF_EXCHANGE:
             recv = send  # one rank: the exchange is the identity (no collective launch)
         else:
             recv = torch.empty_like(send)
-            self.comm.all_to_all(recv, send, [3] * P, [3] * P)
-        host = torch.cat([send, recv]).cpu().view(2, P, 3)
+            self.comm.all_to_all(recv, send, [4] * P, [4] * P)
+        host = self._host(torch.cat([send, recv])).view(2, P, 4)
         send_splits = host[0, :, 0].tolist()
         recv_splits = host[1, :, 0].tolist()
         totals = host[1, :, 1].tolist()
         gmax = int(host[1, :, 2].max())
-        return send_splits, recv_splits, totals, gmax
+        extras = host[1, :, 3].tolist()
+        return send_splits, recv_splits, totals, gmax, extras
 
     def _all_to_all(self, out, inp, out_splits, in_splits, gmax_elems, in_off=None):
         """all_to_all_single in chunks of at most A2A_CHUNK_BYTES per peer. gmax_elems is the
@@ -443,47 +498,51 @@ class DistributedKmerHashMap:
     ROUTE_WINDOW_BYTES = int(os.environ.get("KH_ROUTE_WINDOW_GB", "64")) << 30
     PIPELINE_MIN = int(os.environ.get("KH_PIPELINE_MIN", 1 << 22))  # records per rank below which one chunk
 
-    def _exchange_count_matrix(self, counts):
-        """counts: list over chunks of [P+1] int64 device tensors (per-destination, total) ->
-        (send[c][q], recv[c][q], global max per-peer split over every chunk and rank). One small
-        all-to-all for all chunks."""
+    def _exchange_count_matrix(self, counts, spl, mine):
+        """counts: list over chunks of [P+1] int64 device tensors (per-destination, total); spl:
+        splitter k-mers routed to each owner [P]; mine: this rank's [start k-mers, splitters it
+        routed] -> (send[c][q], recv[c][q], global max per-peer split, splitters this rank owns,
+        walkers and splitters of all ranks). One small all-to-all and ONE host read for all chunks."""
         P, nch = self.P, len(counts)
         mat = torch.stack([c[:P] for c in counts])            # [nch, P]
         mx = mat.max().reshape(1)
-        send = torch.cat([mat.t(), mx.expand(P).reshape(P, 1)], 1).contiguous().view(-1)  # [P, nch+1]
+        cols = [mat.t(), mx.expand(P).reshape(P, 1), spl[:P].reshape(P, 1),
+                mine[:2].reshape(1, 2).expand(P, 2)]
+        send = torch.cat(cols, 1).contiguous().view(-1)       # [P, nch + 4]
+        w = nch + 4
         if P == 1 and not self.SELF_EXCHANGE:
             recv = send
         else:
             recv = torch.empty_like(send)
-            self.comm.all_to_all(recv, send, [nch + 1] * P, [nch + 1] * P)
-        host = torch.cat([send, recv]).cpu().view(2, P, nch + 1)
+            self.comm.all_to_all(recv, send, [w] * P, [w] * P)
+        host = self._host(torch.cat([send, recv])).view(2, P, w)
         send_c = [[int(host[0, q, c]) for q in range(P)] for c in range(nch)]
         recv_c = [[int(host[1, q, c]) for q in range(P)] for c in range(nch)]
         gmax = int(host[1, :, nch].max())
-        return send_c, recv_c, gmax
-
-    def _agree(self, err):
-        """Every rank learns whether any rank failed (one small exchange), and all of them raise
-        together, so no rank is left waiting in a collective the failed one skipped."""
-        bad = self._global_max(1 if err is not None else 0) if self.P > 1 else (1 if err else 0)
-        if bad:
-            if err is not None:
-                raise err
-            raise _lib.KmerHashError(_lib.KH_ERR_FULL, "another rank failed to size its shard")
+        nsp = int(host[1, :, nch + 1].sum())                  # splitters routed to this rank
+        walkers = int(host[1, :, nch + 2].sum() + host[1, :, nch + 3].sum())
+        splitters = int(host[1, :, nch + 3].sum())
+        return send_c, recv_c, gmax, int(host[0, 0, nch + 2]), nsp, walkers, splitters
 
     def insert_all(self, recs):
         """Route every record to its owner (+ this block's start k-mers), learn the per-chunk
         counts in one exchange, size the shard from what it receives (kh_reserve; minimizer
         ownership can be skewed on repetitive inputs), then move the words, partitioning each
-        received chunk while the next one is on the wire; one build at the end."""
+        received chunk while the next one is on the wire; one build at the end. A shard that
+        cannot be sized still takes part in every exchange; every rank raises together at the
+        walk's first check (one host read fewer than agreeing here)."""
         sh, P, W = self.shard, self.P, self.shard.W
         n = recs.shape[0]
         exchange = P > 1 or self.SELF_EXCHANGE
+        self._err = None
         if not exchange and not self.ROUTE_ONE_RANK and hasattr(sh, "insert_records"):
             # one rank: every key is this shard's and nothing moves (as the count exchanges are
             # skipped): the records pass partitions them itself, no owner route + word re-partition
             sh.reserve(n)
             sh.insert_records(recs)
+            c = self._host(sh.counters())      # the walk's start / splitter counts
+            self._ns, self._nsp = int(c[0]), int(c[1])
+            self._walkers, self._splitters = self._ns + self._nsp, self._nsp
             return n
         nch = 1
         if exchange and self.INSERT_CHUNKS > 1 and n >= self.PIPELINE_MIN:
@@ -520,22 +579,27 @@ class DistributedKmerHashMap:
             else:
                 offs = [c0 * W + sum(send[:q]) * W for q in range(P)]
             return [words[offs[q]:offs[q] + send[q] * W] for q in range(P)], offs
-        send_c, recv_c, gmax = self._exchange_count_matrix(counts)
+        spl = sh.route_splitters(P)
+        cnt = sh.counters()
+        mine = torch.stack([cnt[0], spl[:P].sum()])
+        send_c, recv_c, gmax, self._ns, self._nsp, self._walkers, self._splitters = \
+            self._exchange_count_matrix(counts, spl, mine)
         m = sum(sum(r) for r in recv_c)
-        err = None
+        ok = True
         try:
             sh.reserve(m)
         except RuntimeError as ex:  # KmerHashError (NOMEM) or a test shard's error
-            err = ex
-        self._agree(err)
+            self._err, ok = ex, False
         if not exchange:
-            sh.insert_words(words, m)      # one rank: the routed words are this shard's
+            if ok:
+                sh.insert_words(words, m)      # one rank: the routed words are this shard's
             return m
         recv = self._grow("_ins_recv", max(m, 1) * W, torch.int64, recs.device)
         if nch == 1:
             self._all_to_all(recv[:m * W], words, [x * W for x in recv_c[0]],
                              [x * W for x in send_c[0]], gmax * W, in_off=views(0, send_c[0])[1])
-            sh.insert_words(recv, m)
+            if ok:
+                sh.insert_words(recv, m)
             return m
         works, spans, pos = [], [], 0
         for c in range(nch):
@@ -550,11 +614,13 @@ class DistributedKmerHashMap:
             if c > 0:  # previous chunk received: partition it while this one is on the wire
                 works[c - 1].wait()
                 p0, pm = spans[c - 1]
-                sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
+                if ok:
+                    sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
         works[-1].wait()
         p0, pm = spans[-1]
-        sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
-        sh.finish_words()
+        if ok:
+            sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
+            sh.finish_words()
         return m
 
     def assemble(self, total_kmers):
@@ -571,72 +637,107 @@ class DistributedKmerHashMap:
             setattr(self, name, t)
         return t
 
+    def _cap(self, r):
+        """Slot capacity of round r, the same on every rank: the largest per-destination count of
+        round r in the last assemble (+ 25 %), else an even spread of every walker (first round)
+        or the last learnt one. Messages past it are held back, never lost."""
+        if r < len(self._caps):
+            c = self._caps[r]
+        elif self._caps:
+            c = self._caps[-1]
+        else:
+            P = self.P
+            c = max(1024, (self._walkers + P * P - 1) // (P * P) * 5 // 4 + 1024) if P > 1 else self._walkers + 16
+        return max(1, min(c, self.SLOT_CAP_MAX))
+
+    SLOT_CAP_MAX = int(os.environ.get("KH_MW_SLOT_CAP", str(1 << 40)))  # tests: tiny slots (messages held back)
+
     def _assemble_migrate(self, total_kmers):
         """Walkers move to the rank owning their next k-mer (minimizer sharding keeps runs of
-        consecutive k-mers on one rank): round = local walk -> one all-to-all of migrating
-        walkers; then the text records go home in one more all-to-all."""
+        consecutive k-mers on one rank). A round = local walk -> one all-to-all of fixed-size
+        slots: no host read per round; the host reads the global in-flight count only at checks
+        (first at the last assemble's round count, then every CHECK_EVERY rounds). Then the text
+        records go home in one more all-to-all."""
         sh, P = self.shard, self.P
         M, T = sh.MSG_WORDS, sh.TEXT_REC_WORDS
-        n_in = sh.mw_begin(P, self.comm.rank, total_kmers)
-        n_in_total = n_in
-        inp = None
-        self.rounds = 0
+        dev = sh.zeros(1, torch.int64).device
+        local = P == 1 and not self.SELF_EXCHANGE
+        failed = self._err is not None  # this shard could not be sized: it sends nothing until the check
+        if not failed:
+            sh.mw_begin(P, self.comm.rank, total_kmers, self._ns, self._nsp, self._walkers)
+        self.rounds = self.checks = 0
+        live = self._grow("_mw_live", 2 * 4096, torch.int64, dev, slack=1.0)
+        inp, cap_in = None, 0
+        check_at = self._rounds_hint or self.CHECK_EVERY
+        maxes = []
         while True:
-            counts = sh.mw_round(inp, n_in, self._grow("_mw_out", max(n_in, 1) * M, torch.int64,
-                                                       sh.zeros(1, torch.int64).device))
-            out = self._mw_out
-            send_splits, recv_splits, totals, gmax = self._exchange_counts(counts)
-            self.rounds += 1
-            if sum(totals) == 0:
-                break
-            m = sum(recv_splits)
-            if P == 1 and not self.SELF_EXCHANGE:
-                nxt = out      # the round kernel reads its input before the grouping rewrites it
+            cap = self._cap(self.rounds)
+            sw = _lib.slot_words(cap)
+            out = self._grow("_mw_out_%d" % (self.rounds & 1), P * sw, torch.int64, dev)
+            if failed:
+                out.view(-1)[:P * sw].view(P, sw)[:, 0] = 0
+                live[2 * self.rounds:2 * self.rounds + 2] = 0
             else:
-                nxt = self._grow("_mw_in", max(m, 1) * M, torch.int64, out.device)
-                self._all_to_all(nxt[:m * M], out[:sum(send_splits) * M], [c * M for c in recv_splits],
-                                 [c * M for c in send_splits], gmax * M)
-            # ping-pong: the next round reads _mw_in and writes _mw_out
-            inp, n_in = nxt, m
-        nrec = sh.mw_text_count()
-        tout = sh.zeros(max(nrec, 1) * T, torch.int64)
+                sh.mw_round(inp, cap_in, out, cap, live[2 * self.rounds:])
+            if local:
+                nxt = out      # one rank: slot 0 is the next round's input
+            else:
+                nxt = self._grow("_mw_in_%d" % (self.rounds & 1), P * sw, torch.int64, dev)
+                self.comm.all_to_all(nxt[:P * sw], out[:P * sw], [sw] * P, [sw] * P)
+            inp, cap_in = nxt, cap
+            self.rounds += 1
+            if self.rounds >= check_at or self.rounds * 2 + 2 > live.numel():
+                # global max of every round's [in flight, largest per-destination] so far + errors
+                err = torch.tensor([1 if self._err is not None else 0], dtype=torch.int64, device=dev)
+                h = self.comm.max_to_host(torch.cat([live[:2 * self.rounds], err]))
+                self.checks += 1
+                self.syncs += 1
+                if int(h[-1]):
+                    if self._err is not None:
+                        raise self._err
+                    raise _lib.KmerHashError(_lib.KH_ERR_FULL, "another rank failed to size its shard")
+                maxes = h[1:2 * self.rounds:2].tolist()
+                if int(h[2 * self.rounds - 2]) == 0:
+                    break
+                if self.rounds * 2 + 2 > live.numel():
+                    raise _lib.KmerHashError(_lib.KH_ERR_CYCLE, "migrating walk did not end in 4096 rounds")
+                check_at = self.rounds + self.CHECK_EVERY
+        # the next assemble: slots sized by what each round carried, and its first check here
+        self._caps = [max(256, int(x) * 5 // 4 + 256) for x in maxes]
+        self._rounds_hint = self.rounds
+        tb = sh.mw_text_bound()
+        tout = self._grow("_mw_tout", max(tb, 1) * T, torch.int64, dev)
         counts = sh.mw_text(tout)
-        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
+        send_splits, recv_splits, _, gmax, _ = self._exchange_counts(counts)
         r = sum(recv_splits)
-        if P == 1 and not self.SELF_EXCHANGE:
+        if local:
             trecv = tout
         else:
-            trecv = sh.zeros(max(r, 1) * T, torch.int64)
-            self._all_to_all(trecv[:r * T], tout[:nrec * T], [c * T for c in recv_splits],
+            trecv = self._grow("_mw_trecv", max(r, 1) * T, torch.int64, dev)
+            self._all_to_all(trecv[:r * T], tout[:sum(send_splits) * T], [c * T for c in recv_splits],
                              [c * T for c in send_splits], gmax * T)
-        nseg = sh.mw_segments() if hasattr(sh, "mw_segments") else 0
         # every rank takes the same branch (a rank without splitters still links and answers)
-        seg_any = self._global_max(nseg) if P > 1 else nseg
-        if seg_any:
-            self._segments_end(trecv, r, n_in_total)
+        if self._splitters and hasattr(sh, "mw_segments"):
+            self._segments_end(trecv, r, self._ns + self._nsp)
         else:
             sh.mw_end(trecv, r)
-        sh.sync()
+        sh.sync()  # the library counts this one (kh_sync)
         return self.rounds
 
-    def _global_max(self, x):
-        """max of a host int over ranks (one small all-to-all)."""
-        P = self.P
-        send = torch.full((P,), int(x), dtype=torch.int64, device=self.shard.zeros(1, torch.int64).device)
-        recv = torch.empty_like(send)
-        self.comm.all_to_all(recv, send, [1] * P, [1] * P)
-        return int(recv.max().item())
+    CHECK_EVERY = int(os.environ.get("KH_MW_CHECK_EVERY", "4"))
 
     def _segments_end(self, trecv, r, nseg):
-        """Splitter segments: link each segment to its successor's owner, pointer-jump to the
-        contig heads, send the segments' text to the contig origins, materialise."""
+        """Splitter segments: link each segment to its successor's owner, all-gather every rank's
+        predecessor table, rank the chains on the device (pointer jumping, no exchange per step),
+        send the segments' text to the contig origins, materialise."""
         sh, P = self.shard, self.P
         dev = trecv.device
-        L, J, S = sh.LINK_WORDS, sh.JUMP_REPLY_WORDS, sh.SEG_REC_WORDS
+        L, S, PW = sh.LINK_WORDS, sh.SEG_REC_WORDS, sh.PRED_WORDS
         local = P == 1 and not self.SELF_EXCHANGE  # one rank: every exchange is the identity
         lout = self._grow("_ms_links", max(nseg, 1) * L, torch.int64, dev)
         counts = sh.mw_link(trecv, r, lout)
-        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
+        nsp = torch.tensor([self._nsp], dtype=torch.int64, device=dev)
+        send_splits, recv_splits, _, gmax, nsps = self._exchange_counts(counts, nsp)
         m = sum(recv_splits)
         if local:
             lin = lout
@@ -644,35 +745,18 @@ class DistributedKmerHashMap:
             lin = self._grow("_ms_links_in", max(m, 1) * L, torch.int64, dev)
             self._all_to_all(lin[:m * L], lout[:sum(send_splits) * L], [c * L for c in recv_splits],
                              [c * L for c in send_splits], gmax * L)
-        sh.mw_pred(lin, m)
-        self.jump_rounds = 0
-        qout = self._grow("_ms_q", max(nseg, 1), torch.int64, dev)
-        while True:
-            counts = sh.mw_jump_emit(qout)
-            send_splits, recv_splits, totals, gmax = self._exchange_counts(counts)
-            if sum(totals) == 0:
-                break
-            self.jump_rounds += 1
-            ms, mr = sum(send_splits), sum(recv_splits)
-            if local:
-                qin = qout
-            else:
-                qin = self._grow("_ms_qin", max(mr, 1), torch.int64, dev)
-                self._all_to_all(qin[:mr], qout[:ms], recv_splits, send_splits, gmax)
-            rep = self._grow("_ms_rep", max(mr, 1) * J, torch.int64, dev)
-            sh.mw_jump_answer(qin, mr, rep)
-            if local:
-                rin = rep
-            else:
-                rin = self._grow("_ms_rin", max(ms, 1) * J, torch.int64, dev)
-                # replies go back the way the queries came (per-peer counts swapped; the global
-                # max per-peer split is the queries' one)
-                self._all_to_all(rin[:ms * J], rep[:mr * J], [c * J for c in send_splits],
-                                 [c * J for c in recv_splits], gmax * J)
-            sh.mw_jump_apply(rin, ms)
+        stride = max(int(x) for x in nsps)
+        preds = self._grow("_ms_preds", max(stride, 1) * PW, torch.int64, dev)
+        sh.mw_pred(lin, m, preds, stride)
+        if local:
+            allp = preds
+        else:
+            allp = self._grow("_ms_allp", max(P * stride, 1) * PW, torch.int64, dev)
+            self.comm.all_gather(allp[:P * stride * PW], preds[:stride * PW])
+        sh.mw_resolve(allp, stride)
         tout = self._grow("_ms_t", max(r + nseg, 1) * S, torch.int64, dev)
         counts = sh.mw_retag(trecv, r, tout)
-        send_splits, recv_splits, _, gmax = self._exchange_counts(counts)
+        send_splits, recv_splits, _, gmax, _ = self._exchange_counts(counts)
         m = sum(recv_splits)
         if local:
             tin = tout
@@ -689,12 +773,14 @@ class DistributedKmerHashMap:
 
 # --------------------------------------------------------------------------------------------
 def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard_kmers=None,
-                 check=None, load_factor=0.5):
+                 check=None, load_factor=0.5, steps=1):
     """P logical ranks on one GPU (threads): returns the per-rank contig texts. recs: a host
     record array, or a SyntheticKmers whose blocks each rank generates on the GPU (C4-size
     inputs). Shards start at shard_kmers (default n / P) and grow to what they are routed.
     check(rank, text) (optional) consumes each rank's text instead of returning it (large runs).
-    `info` (a dict) receives the round count and per-rank table stats."""
+    `info` (a dict) receives the round count, per-rank table stats and, per rank, the blocking
+    host reads of the last step (insert_all + assemble: this host's and the library's).
+    steps > 1 repeats clear + insert + assemble on the same records (buffers sized by step 1)."""
     import numpy as np
     comms = ThreadComm.group(nranks)
     gen = recs if hasattr(recs, "records_dev") else None
@@ -719,11 +805,15 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
                 if insert_chunks:
                     dm.INSERT_CHUNKS = insert_chunks
                     dm.PIPELINE_MIN = 0
-                dm.insert_all(mine)
-                shard.sync()
+                for step in range(steps):
+                    if step:
+                        shard.clear()
+                    s0 = dm.host_syncs()
+                    dm.insert_all(mine)
+                    comms[r].barrier()
+                    dm.assemble(n)
+                    syncs = dm.host_syncs() - s0
                 del mine
-                comms[r].barrier()
-                dm.assemble(n)
                 text = dm.contigs_text()
                 if check is not None:
                     check(r, text)
@@ -732,6 +822,8 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
                 if info is not None:
                     info.setdefault("rounds", dm.rounds)
                     info.setdefault("stats", {})[r] = shard.stats()
+                    info.setdefault("syncs", {})[r] = syncs
+                    info.setdefault("checks", {})[r] = dm.checks
             shard.table.close()
         except BaseException as ex:  # surface thread failures
             errs.append(ex)

@@ -45,6 +45,9 @@ public:
                            const uint64_t* rcount, const uint64_t* rdispl, uint64_t max_pair,
                            hipStream_t stream) = 0;
     virtual void barrier() = 0;
+    // Device all-gather: every rank's n words at dev_in land at dev_out + q * n (rank q's), ordered
+    // on `stream` (no host wait: the caller reads the result with its own copy).
+    virtual void allgather_dev(const int64_t* dev_in, size_t n, int64_t* dev_out, hipStream_t stream) = 0;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -145,6 +148,12 @@ public:
     }
 
     void barrier() override { g_->wait_all(); }
+
+    void allgather_dev(const int64_t* dev_in, size_t n, int64_t* dev_out, hipStream_t stream) override {
+        std::vector<uint64_t> cnt(g_->world_, n), dsp(g_->world_, 0), rd(g_->world_);
+        for (int q = 0; q < g_->world_; ++q) rd[q] = (uint64_t)q * n;
+        alltoallv(dev_in, cnt.data(), dsp.data(), dev_out, cnt.data(), rd.data(), n, stream);
+    }
 
     ~ThreadComm() override {
         if (ev_) (void)hipEventDestroy(ev_);

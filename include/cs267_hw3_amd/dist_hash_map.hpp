@@ -6,15 +6,19 @@
 // RPC per owner, hash_map.hpp:38-46,64-77; one blocking find RPC per remote walk step,
 // hash_map.hpp:94-100) becomes bulk exchanges through a kh::Comm (comm.hpp / rccl_comm.hpp):
 //
-//   insert_all  route every record to its owner on the GPU (kh_route_starts_dev; the block's start
-//               k-mers are collected in the same pass, kmer_hash.cpp:27-31) -> one count all-gather
-//               -> each shard sized from what it receives (kh_reserve) -> all-to-all of the routed
-//               words in chunks, each received chunk partitioned while the next is on the wire
-//               (kh_insert_words_stage_dev), one region build at the end (kh_insert_words_finish)
+//   insert_all  route every record to its owner on the GPU in one pass into per-owner windows
+//               (kh_route_starts_win_dev; the block's start k-mers are collected in the same pass,
+//               kmer_hash.cpp:27-31) -> one device all-gather of the counts, read once -> each shard
+//               sized from what it receives (kh_reserve) -> all-to-all of the routed words in
+//               chunks, each received chunk partitioned while the next is on the wire
+//               (kh_insert_words_stage_dev), one region build at the end (kh_insert_words_finish).
+//               One rank: the records go straight into the single-GPU records pass.
 //   assemble    migrating walkers (kh_mwalk_*): a walker walks the local shard until its next
-//               k-mer is owned elsewhere, then moves there in the round's all-to-all; the bases
-//               go home in one more all-to-all; splitter segments (long chains) are stitched by
-//               distributed pointer jumping. Each rank ends with its test_<rank>.dat bytes.
+//               k-mer is owned elsewhere, then moves there in the round's all-to-all of fixed-size
+//               slots (no host read per round; the end is checked where the last walk ended); the
+//               bases go home in one more all-to-all; splitter segments (long chains) are ranked on
+//               the device from an all-gathered predecessor table. Each rank ends with its
+//               test_<rank>.dat bytes. A step reads the device at most 8 times (host_syncs()).
 //   find        the owner's table answers (the RPC of hash_map.hpp:94-100): ranks that are threads
 //               of one process (a peer group) look the owner's table up directly; otherwise every
 //               find() is one collective round (all ranks' queries gathered, each owner answers its
@@ -146,8 +150,8 @@ public:
         if (group_) PeerRegistry::get().remove(group_, rank_);
         (void)hipSetDevice(device_);
         if (t_) kh_destroy(t_);
-        for (auto* b : {&words_, &recv_, &counts_, &a_, &b_, &tout_, &trecv_, &lout_, &lin_, &qout_, &qin_, &rep_,
-                        &rin_, &sout_, &sin_, &recs_})
+        for (auto* b : {&words_, &recv_, &counts_, &tout_, &trecv_, &lout_, &lin_, &qout_, &qin_, &sout_, &sin_,
+                        &recs_, &pack_, &gather_, &live_, &slots_[0], &slots_[1], &recv_slots_[0], &recv_slots_[1]})
             b->release();
         for (auto e : events_) (void)hipEventDestroy(e);
         if (stream_) (void)hipStreamDestroy(stream_);
@@ -161,7 +165,15 @@ public:
     int rank() const { return rank_; }
     int world() const { return P_; }
     int rounds() const { return rounds_; }
-    int jump_rounds() const { return jump_rounds_; }
+    int checks() const { return checks_; }
+    // blocking device reads so far: this host's (count exchanges, walk checks) + the library's
+    uint64_t host_syncs() const {
+        uint64_t lib = 0;
+        (void)kh_host_syncs(t_, &lib);
+        return syncs_ + lib;
+    }
+    // tests: slots of at most this many messages (the rest is held back on the sender)
+    void set_slot_cap_max(uint64_t c) { slot_cap_max_ = c ? c : 1; }
     std::mutex& mutex() { return m_; }
 
     void clear() {
@@ -190,6 +202,14 @@ public:
             if (rc != KH_OK) abi_check(rc);
             abi_check(kh_insert_dev(t_, dev_recs, n));
             inserted_ += n;
+            err_.clear();
+            int64_t* c2 = pack_.words(2);
+            abi_check(kh_counters_dev(t_, c2));
+            uint64_t hv[2];
+            read_host(hv, c2, 2);  // the walk's start / splitter counts
+            ns_ = hv[0];
+            nsp_ = splitters_ = hv[1];
+            walkers_ = ns_ + nsp_;
             return done_insert(n);
         }
         uint64_t nch = 1;
@@ -223,27 +243,43 @@ public:
                 abi_check(kh_route_starts_dev(t_, recs + bounds[c] * R_, bounds[c + 1] - bounds[c], P_,
                                               words + bounds[c] * W_, cnt + c * (P + 1)));
         }
-        // every rank learns the whole [src][chunk][dst] count matrix in one all-gather
-        std::vector<uint64_t> mine(nch * (P + 1)), all(P * nch * (P + 1));
-        hip_check(hipMemcpyAsync(mine.data(), cnt, mine.size() * 8, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync");
-        hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-        abi_check(kh_sync(t_));
-        comm_.allgather(mine.data(), mine.size(), all.data(), stream_);
-        auto M = [&](uint64_t src, uint64_t c, uint64_t dst) { return all[(src * nch + c) * (P + 1) + dst]; };
+        // every rank learns the whole [src][chunk][dst] count matrix, the splitters each rank
+        // routed to each owner and every rank's start count in one device all-gather, read once
+        const uint64_t row = nch * (P + 1) + P + 1;
+        int64_t* pk = pack_.words(row * (P + 1));
+        hip_check(hipMemcpyAsync(pk, cnt, nch * (P + 1) * 8, hipMemcpyDeviceToDevice, stream_), "hipMemcpyAsync");
+        abi_check(kh_route_splitters_dev(t_, pk + nch * (P + 1), P_));
+        int64_t* ctr2 = pk + row * P;  // scratch for {starts, splitters collected}
+        abi_check(kh_counters_dev(t_, ctr2));
+        hip_check(hipMemcpyAsync(pk + nch * (P + 1) + P, ctr2, 8, hipMemcpyDeviceToDevice, stream_), "hipMemcpyAsync");
+        int64_t* allp = gather_.words(row * P);
+        comm_.allgather_dev(pk, row, allp, stream_);
+        std::vector<uint64_t> all(row * P);
+        read_host(all.data(), allp, row * P);
+        auto M = [&](uint64_t src, uint64_t c, uint64_t dst) { return all[src * row + c * (P + 1) + dst]; };
+        auto SPL = [&](uint64_t src, uint64_t dst) { return all[src * row + nch * (P + 1) + dst]; };
         uint64_t m = 0, gmax = 0;
-        for (uint64_t q = 0; q < P; ++q)
+        ns_ = all[(uint64_t)rank_ * row + nch * (P + 1) + P];
+        nsp_ = walkers_ = splitters_ = 0;
+        for (uint64_t q = 0; q < P; ++q) {
+            nsp_ += SPL(q, rank_);
+            walkers_ += all[q * row + nch * (P + 1) + P];
+            for (uint64_t d = 0; d < P; ++d) splitters_ += SPL(q, d);
             for (uint64_t c = 0; c < nch; ++c) {
                 m += M(q, c, rank_);
                 for (uint64_t d = 0; d < P; ++d) gmax = std::max(gmax, M(q, c, d));
             }
+        }
+        walkers_ += splitters_;
         // size the shard from what it holds after this insert (a non-empty shard cannot grow:
-        // kh_reserve fails); every rank fails together if any rank cannot
+        // kh_reserve fails); a rank that cannot still takes part in every exchange, sends no
+        // walkers, and every rank raises together at the walk's first check
         const int rc = kh_reserve(t_, inserted_ + m);
-        const std::string err = rc == KH_OK ? "" : kh_last_error();
-        agree(rc != KH_OK, err);
+        err_ = rc == KH_OK ? "" : kh_last_error();
+        const bool ok = rc == KH_OK;
         inserted_ += m;
         if (P == 1) {  // one rank routed anyway (KH_DIST_ROUTE_ONE_RANK=1; one chunk): the words are this shard's
-            abi_check(kh_insert_words_dev(t_, words, m));
+            if (ok) abi_check(kh_insert_words_dev(t_, words, m));
             return done_insert(m);
         }
         int64_t* recv = recv_.words(std::max<uint64_t>(m, 1) * W_);
@@ -262,7 +298,7 @@ public:
         if (nch == 1) {
             plan(0, 0);
             comm_.alltoallv(words, sc.data(), sd.data(), recv, rcn.data(), rd.data(), gmax * W_, stream_);
-            abi_check(kh_insert_words_dev(t_, recv, m));
+            if (ok) abi_check(kh_insert_words_dev(t_, recv, m));
             return done_insert(m);
         }
         // chunk c moves on the exchange stream while chunk c-1, received, is partitioned on the
@@ -277,61 +313,97 @@ public:
             plan(c, pos);
             comm_.alltoallv(words, sc.data(), sd.data(), recv, rcn.data(), rd.data(), gmax * W_, xstream_);
             hip_check(hipEventRecord(events_[c], xstream_), "hipEventRecord");
-            if (c > 0) stage(recv, prev_pos, prev_m, m, events_[c - 1]);
+            if (c > 0 && ok) stage(recv, prev_pos, prev_m, m, events_[c - 1]);
             prev_pos = pos;
             prev_m = mc;
             pos += mc;
         }
-        stage(recv, prev_pos, prev_m, m, events_[nch - 1]);
-        abi_check(kh_insert_words_finish(t_));
+        if (ok) {
+            stage(recv, prev_pos, prev_m, m, events_[nch - 1]);
+            abi_check(kh_insert_words_finish(t_));
+        } else {
+            hip_check(hipStreamWaitEvent(stream_, events_[nch - 1], 0), "hipStreamWaitEvent");
+        }
         return done_insert(m);
     }
 
     // kmer_hash.cpp:38-55 assemble_contigs for this rank's start k-mers, every rank at once.
     // total_kmers bounds contig length (cycle detection). Collective. Returns walk rounds.
+    // Rounds exchange fixed-size slots (KH_SLOT_WORDS): no host read per round; the host reads
+    // the global in-flight count first where the last walk ended, then every kCheckEvery rounds.
     int assemble(uint64_t total_kmers) {
         hip_check(hipSetDevice(device_), "hipSetDevice");
-        constexpr uint64_t M = KH_MSG_WORDS, T = KH_TEXT_REC_WORDS;
+        constexpr uint64_t T = KH_TEXT_REC_WORDS;
+        const uint64_t P = (uint64_t)P_;
+        const bool failed = !err_.empty();  // this shard could not be sized: it sends no walkers
         uint64_t n_in = 0;
-        abi_check(kh_mwalk_begin(t_, P_, rank_, total_kmers, &n_in));
-        const uint64_t n_walkers = n_in;
+        if (!failed) abi_check(kh_mwalk_begin(t_, P_, rank_, total_kmers, ns_, nsp_, walkers_, &n_in));
+        rounds_ = checks_ = 0;
+        int64_t* live = live_.words(2 * kMaxRounds + 2);
         const int64_t* in = nullptr;
-        DevBuf* out = &a_;
-        DevBuf* nxt = &b_;
-        rounds_ = 0;
-        Exchange ex;
+        uint64_t cap_in = 0;
+        int check_at = rounds_hint_ ? rounds_hint_ : kCheckEvery;
+        std::vector<uint64_t> maxes;
         for (;;) {
-            int64_t* o = out->words(std::max<uint64_t>(n_in, 1) * M);
-            abi_check(kh_mwalk_round_dev(t_, in, n_in, o, counts_.words(P_ + 1)));
-            exchange_counts(ex);  // syncs: the round has consumed `in`
-            ++rounds_;
-            if (ex.total_all == 0) break;
-            if (P_ == 1) {
-                in = o;  // nothing to move: the next round reads this round's output
-                std::swap(out, nxt);
+            const uint64_t cap = slot_cap(rounds_), sw = KH_SLOT_WORDS(cap);
+            int64_t* out = slots_[rounds_ & 1].words(P * sw);
+            if (failed) {
+                hip_check(hipMemset2DAsync(out, sw * 8, 0, 8, P, stream_), "hipMemset2DAsync");
+                hip_check(hipMemsetAsync(live + 2 * rounds_, 0, 16, stream_), "hipMemsetAsync");
             } else {
-                int64_t* r = nxt->words(std::max<uint64_t>(ex.recv_total, 1) * M);
-                move(o, r, ex, M);
-                in = r;
+                abi_check(kh_mwalk_round_dev(t_, in, cap_in, out, cap, live + 2 * rounds_));
             }
-            n_in = ex.recv_total;
+            int64_t* nxt = out;  // one rank: slot 0 is the next round's input
+            if (P > 1) {
+                nxt = recv_slots_[rounds_ & 1].words(P * sw);
+                std::vector<uint64_t> cnt(P, sw), dsp(P);
+                for (uint64_t q = 0; q < P; ++q) dsp[q] = q * sw;
+                comm_.alltoallv(out, cnt.data(), dsp.data(), nxt, cnt.data(), dsp.data(), sw, stream_);
+            }
+            in = nxt;
+            cap_in = cap;
+            ++rounds_;
+            if (rounds_ >= check_at || rounds_ >= kMaxRounds) {
+                // every rank's [in flight, largest per-destination] of every round so far + errors
+                const uint64_t w = 2 * (uint64_t)rounds_ + 1;
+                int64_t* mine = pack_.words(w);
+                hip_check(hipMemcpyAsync(mine, live, (w - 1) * 8, hipMemcpyDeviceToDevice, stream_), "hipMemcpyAsync");
+                put_word(mine + w - 1, failed ? 1 : 0);
+                int64_t* allg = gather_.words(w * P);
+                comm_.allgather_dev(mine, w, allg, stream_);
+                std::vector<uint64_t> h(w * P);
+                read_host(h.data(), allg, w * P);
+                ++checks_;
+                std::vector<uint64_t> mx(w, 0);
+                for (uint64_t q = 0; q < P; ++q)
+                    for (uint64_t i = 0; i < w; ++i) mx[i] = std::max(mx[i], h[q * w + i]);
+                if (mx[w - 1]) throw std::runtime_error(failed ? err_ : "another rank failed to size its shard");
+                maxes.assign(rounds_, 0);
+                for (int r = 0; r < rounds_; ++r) maxes[r] = mx[2 * r + 1];
+                if (mx[2 * (uint64_t)rounds_ - 2] == 0) break;
+                if (rounds_ >= kMaxRounds) throw std::runtime_error("migrating walk did not end in kMaxRounds rounds");
+                check_at = rounds_ + kCheckEvery;
+            }
         }
-        uint64_t nrec = 0;
-        abi_check(kh_mwalk_text_count(t_, &nrec));
-        int64_t* tout = tout_.words(std::max<uint64_t>(nrec, 1) * T);
-        abi_check(kh_mwalk_text_dev(t_, tout, counts_.words(P_ + 1)));
+        // the next assemble: slots sized by what each round carried, and its first check here
+        caps_.assign(maxes.size(), 0);
+        for (size_t r = 0; r < maxes.size(); ++r) caps_[r] = std::max<uint64_t>(256, maxes[r] * 5 / 4 + 256);
+        rounds_hint_ = rounds_;
+        uint64_t tb = 0;
+        abi_check(kh_mwalk_text_bound(t_, &tb));
+        int64_t* tout = tout_.words(std::max<uint64_t>(tb, 1) * T);
+        abi_check(kh_mwalk_text_dev(t_, tout, counts_.words(P + 1)));
+        Exchange ex;
         exchange_counts(ex);
         const uint64_t r = ex.recv_total;
         int64_t* trecv = tout;
-        if (P_ > 1) {
+        if (P > 1) {
             trecv = trecv_.words(std::max<uint64_t>(r, 1) * T);
             move(tout, trecv, ex, T);
         }
-        uint64_t nseg = 0;
-        abi_check(kh_mwalk_segments(t_, &nseg));
         // every rank takes the same branch (a rank without splitters still links and answers)
-        if (global_max(nseg))
-            segments_end(trecv, r, n_walkers);
+        if (splitters_)
+            segments_end(trecv, r, ns_ + nsp_);
         else
             abi_check(kh_mwalk_end_dev(t_, trecv, r));
         abi_check(kh_sync(t_));
@@ -393,6 +465,8 @@ public:
     uint64_t ranks_per_device() const { return (uint64_t)ranks_per_device_; }
 
     static constexpr uint64_t kInsertChunks = 4;
+    static constexpr int kCheckEvery = 4;
+    static constexpr int kMaxRounds = 4096;
     static constexpr uint64_t kPipelineMin = 1ull << 22;  // records per rank below: one transfer
 
 private:
@@ -461,27 +535,53 @@ private:
     struct Exchange {
         std::vector<uint64_t> send, recv;  // per peer, in items
         uint64_t send_total = 0, recv_total = 0, total_all = 0, gmax = 0;
+        std::vector<uint64_t> extra;       // every rank's extra word
     };
 
-    // counts_ holds [P+1] device words (per destination, total) -> every rank's view
-    void exchange_counts(Exchange& ex) {
-        const uint64_t P = (uint64_t)P_;
-        std::vector<uint64_t> mine(P + 1), all(P * (P + 1));
-        hip_check(hipMemcpyAsync(mine.data(), counts_.get(), (P + 1) * 8, hipMemcpyDeviceToHost, stream_),
-                  "hipMemcpyAsync");
-        hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
-        abi_check(kh_sync(t_));
-        comm_.allgather(mine.data(), P + 1, all.data(), stream_);
-        ex.send.assign(mine.begin(), mine.begin() + P);
+    // counts_ holds [P+1] device words (per destination, total) -> every rank's view, with one
+    // extra word of this rank's (e.g. its splitter count): one device all-gather, read once
+    void exchange_counts(Exchange& ex, uint64_t extra = 0) {
+        const uint64_t P = (uint64_t)P_, w = P + 2;
+        int64_t* mine = pack_.words(w);
+        hip_check(hipMemcpyAsync(mine, counts_.get(), (P + 1) * 8, hipMemcpyDeviceToDevice, stream_), "hipMemcpyAsync");
+        put_word(mine + P + 1, extra);
+        int64_t* allg = gather_.words(w * P);
+        comm_.allgather_dev(mine, w, allg, stream_);
+        std::vector<uint64_t> all(w * P);
+        read_host(all.data(), allg, w * P);
+        ex.send.assign(P, 0);
         ex.recv.resize(P);
+        ex.extra.resize(P);
         ex.send_total = ex.recv_total = ex.total_all = ex.gmax = 0;
         for (uint64_t q = 0; q < P; ++q) {
-            ex.recv[q] = all[q * (P + 1) + rank_];
+            ex.send[q] = all[(uint64_t)rank_ * w + q];
+            ex.recv[q] = all[q * w + rank_];
+            ex.extra[q] = all[q * w + P + 1];
             ex.send_total += ex.send[q];
             ex.recv_total += ex.recv[q];
-            ex.total_all += all[q * (P + 1) + P];
-            for (uint64_t d = 0; d < P; ++d) ex.gmax = std::max(ex.gmax, all[q * (P + 1) + d]);
+            ex.total_all += all[q * w + P];
+            for (uint64_t d = 0; d < P; ++d) ex.gmax = std::max(ex.gmax, all[q * w + d]);
         }
+    }
+
+    // one blocking device -> host read (counted: host_syncs())
+    void read_host(void* dst, const void* dev, uint64_t words) {
+        hip_check(hipMemcpyAsync(dst, dev, words * 8, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync");
+        hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        ++syncs_;
+    }
+
+    uint64_t slot_cap(int r) const {
+        uint64_t c;
+        if (r < (int)caps_.size())
+            c = caps_[r];
+        else if (!caps_.empty())
+            c = caps_.back();
+        else {
+            const uint64_t P = (uint64_t)P_;
+            c = P > 1 ? std::max<uint64_t>(1024, (walkers_ + P * P - 1) / (P * P) * 5 / 4 + 1024) : walkers_ + 16;
+        }
+        return std::max<uint64_t>(1, std::min<uint64_t>(c, slot_cap_max_));
     }
 
     // items of `width` words grouped by destination (ex.send) -> received (ex.recv); reverse:
@@ -503,16 +603,11 @@ private:
         comm_.alltoallv(send, sc.data(), sd.data(), recv, rc.data(), rd.data(), ex.gmax * width, stream_);
     }
 
-    uint64_t global_max(uint64_t x) {
-        if (P_ == 1) return x;
-        std::vector<uint64_t> all(P_);
-        comm_.allgather(&x, 1, all.data(), stream_);
-        return *std::max_element(all.begin(), all.end());
-    }
-
-    void agree(bool failed, const std::string& err) {
-        if (global_max(failed ? 1 : 0) == 0) return;
-        throw std::runtime_error(failed ? err : "another rank failed to size its shard");
+    // a host value into device memory without a host-side copy (two 32-bit fills: async)
+    void put_word(int64_t* dev, uint64_t v) {
+        hip_check(hipMemsetD32Async((hipDeviceptr_t)dev, (int)(uint32_t)v, 1, stream_), "hipMemsetD32Async");
+        hip_check(hipMemsetD32Async((hipDeviceptr_t)((char*)dev + 4), (int)(uint32_t)(v >> 32), 1, stream_),
+                  "hipMemsetD32Async");
     }
 
     void stage(const int64_t* recv, uint64_t pos, uint64_t m, uint64_t total, hipEvent_t arrived) {
@@ -528,42 +623,31 @@ private:
         }
     }
 
-    // Splitter segments: link each segment to its successor's owner, pointer-jump to the contig
-    // heads, send the segments' text to the contig origins, materialise.
+    // Splitter segments: link each segment to its successor's owner, all-gather every rank's
+    // predecessor table, rank the chains on the device, send the segments' text to the contig
+    // origins, materialise.
     void segments_end(const int64_t* trecv, uint64_t r, uint64_t nseg) {
-        constexpr uint64_t L = KH_LINK_WORDS, J = KH_JUMP_REPLY_WORDS, S = KH_SEG_REC_WORDS;
+        constexpr uint64_t L = KH_LINK_WORDS, S = KH_SEG_REC_WORDS, PW = KH_PRED_WORDS;
         const bool local = P_ == 1;
         Exchange ex;
         int64_t* lout = lout_.words(std::max<uint64_t>(nseg, 1) * L);
         abi_check(kh_mwalk_link_dev(t_, trecv, r, lout, counts_.words(P_ + 1)));
-        exchange_counts(ex);
+        exchange_counts(ex, nsp_);
         int64_t* lin = lout;
         if (!local) {
             lin = lin_.words(std::max<uint64_t>(ex.recv_total, 1) * L);
             move(lout, lin, ex, L);
         }
-        abi_check(kh_mwalk_pred_dev(t_, lin, ex.recv_total));
-        jump_rounds_ = 0;
-        int64_t* qout = qout_.words(std::max<uint64_t>(nseg, 1));
-        for (;;) {
-            abi_check(kh_mwalk_jump_emit_dev(t_, qout, counts_.words(P_ + 1)));
-            exchange_counts(ex);
-            if (ex.total_all == 0) break;
-            ++jump_rounds_;
-            int64_t* qin = qout;
-            if (!local) {
-                qin = qin_.words(std::max<uint64_t>(ex.recv_total, 1));
-                move(qout, qin, ex, 1);
-            }
-            int64_t* rep = rep_.words(std::max<uint64_t>(ex.recv_total, 1) * J);
-            abi_check(kh_mwalk_jump_answer_dev(t_, qin, ex.recv_total, rep));
-            int64_t* rin = rep;
-            if (!local) {
-                rin = rin_.words(std::max<uint64_t>(ex.send_total, 1) * J);
-                move(rep, rin, ex, J, /*reverse=*/true);
-            }
-            abi_check(kh_mwalk_jump_apply_dev(t_, rin, ex.send_total, nullptr));
+        uint64_t stride = 0;
+        for (uint64_t x : ex.extra) stride = std::max(stride, x);
+        int64_t* preds = qout_.words(std::max<uint64_t>(stride, 1) * PW);
+        abi_check(kh_mwalk_pred_dev(t_, lin, ex.recv_total, preds, stride));
+        int64_t* allp = preds;
+        if (!local) {
+            allp = qin_.words(std::max<uint64_t>(stride * P_, 1) * PW);
+            comm_.allgather_dev(preds, stride * PW, allp, stream_);
         }
+        abi_check(kh_mwalk_resolve_dev(t_, allp, stride));
         int64_t* tout = sout_.words(std::max<uint64_t>(r + nseg, 1) * S);
         abi_check(kh_mwalk_retag_dev(t_, trecv, r, tout, counts_.words(P_ + 1)));
         exchange_counts(ex);
@@ -582,12 +666,18 @@ private:
     kh_table* t_ = nullptr;
     hipStream_t stream_ = nullptr, xstream_ = nullptr;
     uint64_t W_ = 2, R_ = 15;
-    int rounds_ = 0, jump_rounds_ = 0;
+    int rounds_ = 0, checks_ = 0, rounds_hint_ = 0;
     uint64_t inserted_ = 0;  // k-mers this shard holds since the last clear
     int ranks_per_device_ = 1;
+    uint64_t syncs_ = 0;     // blocking device reads by this host (host_syncs() adds the library's)
+    uint64_t ns_ = 0, nsp_ = 0, walkers_ = 0, splitters_ = 0;  // of the last insert_all
+    std::string err_;        // this shard could not be sized by the last insert_all
+    std::vector<uint64_t> caps_;  // slot capacity per round, learnt from the last assemble
+    uint64_t slot_cap_max_ = ~0ull;
     std::mutex m_;
     std::vector<hipEvent_t> events_;
-    DevBuf words_, recv_, counts_, a_, b_, tout_, trecv_, lout_, lin_, qout_, qin_, rep_, rin_, sout_, sin_, recs_;
+    DevBuf words_, recv_, counts_, tout_, trecv_, lout_, lin_, qout_, qin_, sout_, sin_, recs_, pack_, gather_, live_;
+    DevBuf slots_[2], recv_slots_[2];
 };
 
 }  // namespace kh

@@ -81,6 +81,11 @@ public:
         }
     }
 
+    void allgather_dev(const int64_t* dev_in, size_t n, int64_t* dev_out, hipStream_t stream) override {
+        hip_check(hipSetDevice(dev_), "hipSetDevice");
+        check(ncclAllGather(dev_in, dev_out, n, ncclInt64, comm_, stream), "ncclAllGather");
+    }
+
     void barrier() override {
         uint64_t x = 0;
         std::vector<uint64_t> all(world_);

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KH_ABI_VERSION 1
+#define KH_ABI_VERSION 2
 #define KH_K_MAX 60
 
 enum {
@@ -119,7 +119,7 @@ int kh_contigs_offsets(kh_table* t, uint64_t* host_offsets, uint64_t n); /* line
 
 /* ---- sharded multi-GPU path --------------------------------------------------------------------
  * One table per rank (GPU). The key space is split by an owner hash; the caller moves the buffers
- * between ranks (RCCL all-to-all over xGMI; cs267_hw3_amd/csrc/kh_dist.cpp, cs267_hw3_amd/dist.py). Replaces the per-owner batched
+ * between ranks (RCCL all-to-all over xGMI: include/cs267_hw3_amd/dist_hash_map.hpp, cs267_hw3_amd/dist.py). Replaces the per-owner batched
  * insert RPCs (hash_map.hpp:38-46,64-77) and the per-step remote find RPCs (hash_map.hpp:94-100).
  * Routed records and query keys are kh_word_count(k) 64-bit words each. counts_out receives
  * nranks + 1 uint64 on the device: per-destination counts, then their total. All async. */
@@ -157,47 +157,59 @@ int kh_insert_words_dev(kh_table* t, const void* dev_words, uint64_t m);
  * has been issued on the table's stream. */
 int kh_insert_words_stage_dev(kh_table* t, const void* dev_words, uint64_t m, uint64_t total_hint);
 int kh_insert_words_finish(kh_table* t);
-/* Migrating-walker rounds. The table is sharded by
- * a hash of each k-mer's minimizer, so consecutive k-mers of a contig mostly share an owner; a
- * walker walks the local shard until its next k-mer is owned elsewhere and is then sent there:
- *   begin -> loop { round(in, n_in -> out grouped by destination, counts[P+1])
- *                   -> exchange counts, all-to-all out -> next in }   until every rank's total is 0
- *   -> text_count / text_dev (text records grouped by origin rank) -> all-to-all
- *   -> end_dev(records received): this rank's contig text (kh_contigs_text*).
- * Messages are KH_MSG_WORDS int64 words, text records KH_TEXT_REC_WORDS. The first round reads
- * this rank's start k-mers (in may be NULL); out needs room for one message per input (the
- * first round: one per walker). Routing by minimizer must also be used for the inserts: this
- * sharding and kh_route_dev agree (both use the minimizer owner). */
+/* Splitter k-mers routed to each owner since the last clear (async copy of nranks uint64 into
+ * device memory): a shard's splitter count is the sum of its column over the senders, learnt with
+ * the route counts instead of by a device read. */
+int kh_route_splitters_dev(kh_table* t, void* dev_out, int nranks);
+/* Async copy of {start k-mers collected, splitter k-mers collected} (2 uint64) into device memory,
+ * for hosts that read them together with their own counts (one host round trip). */
+int kh_counters_dev(kh_table* t, void* dev_out);
+/* Migrating-walker rounds. The table is sharded by a hash of each k-mer's minimizer, so
+ * consecutive k-mers of a contig mostly share an owner; a walker walks the local shard until its
+ * next k-mer is owned elsewhere and is then sent there. Nothing below reads the device on the host:
+ *   begin(n_starts, n_splitters, total_walkers)
+ *   loop { round(in slots -> out slots, live) -> all-to-all of the fixed-size slot buffers }
+ *          (every few rounds the host reads the global sum of live[0]; rounds past the end find
+ *           empty slots and do nothing)
+ *   -> text_dev (text records grouped by origin rank, counts[P+1]) -> exchange -> end_dev(records)
+ * A round's exchange buffer is nranks slots of KH_SLOT_WORDS(cap) int64 words: [count, 0, up to
+ * cap messages of KH_MSG_WORDS]; slot q goes to rank q and the received buffer (slot q = what rank q
+ * sent) is the next round's input. Messages past cap are held back on the sender and go out in a
+ * later round. live: 2 uint64 on the device = [messages in flight after the round (sent + held
+ * back), largest per-destination count]. The first round takes in_slots = NULL (the walkers of
+ * begin). n_starts / n_splitters: this rank's counts (kh_counters_dev, or the column sums of
+ * kh_route_splitters_dev); total_walkers: the sum of n_starts + n_splitters over all ranks.
+ * Routing by minimizer must also be used for the inserts: this sharding and the routes agree. */
 #define KH_MSG_WORDS 5
 #define KH_TEXT_REC_WORDS 2
-int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t* n_walkers);
-int kh_mwalk_round_dev(kh_table* t, const void* dev_in, uint64_t n_in, void* dev_out,
-                       void* dev_counts_out);
-int kh_mwalk_text_count(kh_table* t, uint64_t* n_records);
+#define KH_SLOT_WORDS(cap) (2 + (cap) * KH_MSG_WORDS)
+int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t n_starts, uint64_t n_splitters,
+                   uint64_t total_walkers, uint64_t* n_walkers);
+int kh_mwalk_round_dev(kh_table* t, const void* dev_in_slots, uint64_t in_cap, void* dev_out_slots, uint64_t out_cap,
+                       void* dev_live);
+int kh_mwalk_text_bound(kh_table* t, uint64_t* n_records); /* text_dev writes at most this many */
 int kh_mwalk_text_dev(kh_table* t, void* dev_out, void* dev_counts_out);
 int kh_mwalk_end_dev(kh_table* t, const void* dev_recs, uint64_t n);
 /* Splitter segments of the migrating walk (kh_mseg.hip; on when the shard collects splitters,
  * KH_MW_SEGMENTS=0 turns them off). kh_mwalk_begin then also seeds a walker at every splitter
  * k-mer this shard owns (n_walkers includes them) and walkers stop before splitters. When
- * kh_mwalk_segments reports > 0 (on any rank: the count is per rank), after the text records have
- * come home (kh_mwalk_text_dev + exchange) the end of the walk is, instead of kh_mwalk_end_dev:
- *   kh_mwalk_link_dev(recs)  -> KH_LINK_WORDS-word links grouped by owner -> exchange -> kh_mwalk_pred_dev
- *   repeat: kh_mwalk_jump_emit_dev -> 1-word queries, exchange -> kh_mwalk_jump_answer_dev ->
- *           KH_JUMP_REPLY_WORDS-word replies, exchange back (counts reversed) ->
- *           kh_mwalk_jump_apply_dev (pending, may be NULL = segments still without a head); until no
- *           rank emits
+ * kh_mwalk_segments reports > 0 on any rank, after the text records have come home the end of the
+ * walk is, instead of kh_mwalk_end_dev:
+ *   kh_mwalk_link_dev(recs)  -> KH_LINK_WORDS-word links grouped by owner -> exchange
+ *   kh_mwalk_pred_dev(links, preds, stride) -> this rank's table of {predecessor id, length} for
+ *        its splitter segments (stride >= every rank's kh_mwalk_segments entries; the tail is "none")
+ *   all-gather of the tables (rank q's at q * stride) -> kh_mwalk_resolve_dev(all, stride): every
+ *        segment's contig and offset by pointer jumping on the device (no exchange per step)
  *   kh_mwalk_retag_dev(recs) -> KH_SEG_REC_WORDS-word records grouped by contig origin -> exchange
  *   kh_mwalk_end_seg_dev(recs, received segment records)   (this rank's test_<rank>.dat in HBM)
- * Buffers: links <= n_walkers records, queries <= segments, retag output <= n + segments. */
+ * Buffers: links <= n_walkers records, preds 2 * stride words, retag output <= n + segments. */
 #define KH_LINK_WORDS 4
-#define KH_JUMP_REPLY_WORDS 3
+#define KH_PRED_WORDS 2
 #define KH_SEG_REC_WORDS 3
 int kh_mwalk_segments(kh_table* t, uint64_t* n_splitter_segments);
 int kh_mwalk_link_dev(kh_table* t, const void* dev_recs, uint64_t n, void* dev_links_out, void* dev_counts_out);
-int kh_mwalk_pred_dev(kh_table* t, const void* dev_links, uint64_t m);
-int kh_mwalk_jump_emit_dev(kh_table* t, void* dev_queries_out, void* dev_counts_out);
-int kh_mwalk_jump_answer_dev(kh_table* t, const void* dev_queries, uint64_t m, void* dev_replies_out);
-int kh_mwalk_jump_apply_dev(kh_table* t, const void* dev_replies, uint64_t m, uint64_t* pending);
+int kh_mwalk_pred_dev(kh_table* t, const void* dev_links, uint64_t m, void* dev_preds_out, uint64_t stride);
+int kh_mwalk_resolve_dev(kh_table* t, const void* dev_all_preds, uint64_t stride);
 int kh_mwalk_retag_dev(kh_table* t, const void* dev_recs, uint64_t n, void* dev_seg_recs_out, void* dev_counts_out);
 int kh_mwalk_end_seg_dev(kh_table* t, const void* dev_recs, uint64_t n, const void* dev_seg_recs, uint64_t m);
 

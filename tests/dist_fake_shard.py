@@ -107,24 +107,41 @@ class FakeShard:
     def zeros(self, n, dtype):
         return torch.zeros(max(int(n), 1), dtype=dtype)
 
-    def mw_begin(self, nranks, rank, total_kmers):
+    def counters(self):
+        return torch.tensor([len(self.starts), 0], dtype=torch.int64)
+
+    def route_splitters(self, nranks):
+        return torch.zeros(nranks, dtype=torch.int64)   # no splitter segments in the double
+
+    def mw_begin(self, nranks, rank, total_kmers, n_starts, n_splitters, total_walkers):
+        assert n_starts == len(self.starts)
         self.nranks, self.rank = nranks, rank
         self.store = []                                    # (origin, fin, pos, idx, value)
         self.first = True
+        self.carry = []                                    # (owner, message) held back
         return len(self.starts)
 
     def _msg(self, key, fwd, steps, idx, origin):
         kw = self._enc([key]).numpy()[:2]
         return [int(kw[0]), int(kw[1]), steps, idx, origin | (fwd << 8)]
 
-    def mw_round(self, inp, n_in, out):
+    def mw_round(self, inp, cap_in, out, cap_out, live):
+        """kh_mwalk_round_dev: P slots in (None: this rank's starts), P slots of cap_out out,
+        messages past a slot's capacity held back for the next round; live = [in flight, largest
+        per-destination count]."""
+        P = self.nranks
         if self.first:
             msgs = [self._msg(s[:self.P], s[self.P + 1], 0, i, self.rank) for i, s in enumerate(self.starts)]
             self.first = False
         else:
-            a = inp[:n_in * 5].numpy().reshape(n_in, 5)
-            msgs = [list(map(int, r)) for r in a]
-        outs = []
+            a = inp.numpy()
+            sw = 2 + cap_in * 5
+            msgs = []
+            for q in range(P):
+                c = int(a[q * sw])
+                for i in range(c):
+                    msgs.append(list(map(int, a[q * sw + 2 + 5 * i:q * sw + 7 + 5 * i])))
+        outs = list(self.carry)
         for m in msgs:
             key = bytes(np.array(m[:2], np.int64).view(np.uint8)[:self.P])
             steps, idx, origin, fwd = m[2], m[3], m[4] & 0xFF, (m[4] >> 8) & 0xFF
@@ -149,22 +166,31 @@ class FakeShard:
                 if rec is None:
                     raise RuntimeError("Error: k-mer not found in Distributed HashMap.")
                 fwd = rec[self.P + 1]
-        outs.sort(key=lambda x: x[0])
         o = out.numpy()
-        for j, (_, m) in enumerate(outs):
-            o[j * 5:(j + 1) * 5] = m
-        counts = np.zeros(self.nranks + 1, np.int64)
+        sw = 2 + cap_out * 5
+        counts = [0] * P
+        self.carry = []
+        for q, m in outs:
+            if counts[q] < cap_out:
+                o[q * sw + 2 + 5 * counts[q]:q * sw + 7 + 5 * counts[q]] = m
+                counts[q] += 1
+            else:
+                self.carry.append((q, m))
+        per = [0] * P
         for q, _ in outs:
-            counts[q] += 1
-        counts[self.nranks] = len(outs)
-        return torch.from_numpy(counts)
+            per[q] += 1
+        for q in range(P):
+            o[q * sw] = counts[q]
+            o[q * sw + 1] = 0
+        live[0] = len(outs)
+        live[1] = max(per) if per else 0
+
+    def mw_text_bound(self):
+        return len(self.store)
 
     def _rec_words(self, r):
         origin, fin, pos, idx, val = r
         return [(origin << 56) | (fin << 55) | (pos << 31) | idx, val]
-
-    def mw_text_count(self):
-        return len(self.store)
 
     def mw_text(self, out):
         recs = sorted(self.store, key=lambda r: r[0])

@@ -127,3 +127,21 @@ def test_sharded_table_generated(k, n, P, lmin, lmax):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gen ok" in r.stdout
+
+
+@pytest.mark.parametrize("P", [1, 8])
+def test_cpp_host_sharded_step_syncs(P):
+    """The C++ host's sharded step (tools/kh_bench_cpp: clear + insert_all_dev + assemble) over P
+    logical ranks on one GPU, C3 shape at 500K k-mers per rank: verified against the generator's
+    truth, at most 8 blocking device reads per rank and step (count exchanges, the walk's end
+    check, the library's own; ThreadComm's transport waits are not the protocol's), one check."""
+    exe = os.path.join(ROOT, "tools", "kh_bench_cpp")
+    if not os.path.exists(exe):
+        pytest.skip("kh_bench_cpp not built")
+    r = subprocess.run([exe, "--ranks", str(P), "--comm", "thread", "--n", "500000", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["verified_vs_truth"] is True
+    assert d["host_syncs_per_step_max"] <= 8, d
+    assert d["walk_checks"] == 1, d

@@ -45,12 +45,12 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, insert_chunks=
         dm.A2A_CHUNK_BYTES = chunk_bytes   # force the chunked all-to-all path
     try:
         dm.insert_all(torch.from_numpy(recs))
+        rounds = dm.assemble(MANIFEST[name]["n"])
     except Exception as ex:                # every rank must fail together (no rank left waiting)
         with open(os.path.join(outdir, f"err_{rank}"), "w") as f:
             f.write(str(ex))
         dist.destroy_process_group()
         return
-    rounds = dm.assemble(MANIFEST[name]["n"])
     with open(os.path.join(outdir, f"test_{rank}.dat"), "wb") as f:
         f.write(dm.contigs_text())
     with open(os.path.join(outdir, f"rounds_{rank}"), "w") as f:
@@ -97,8 +97,9 @@ def test_sharded_pipelined_insert_gloo(tmp_path, name, world, chunks):
 
 
 def test_sharded_shard_full_fails_on_every_rank(tmp_path):
-    """A shard that cannot hold what it is routed (rank 0 here) makes EVERY rank raise after the
-    count exchange, instead of leaving the others blocked in the next collective."""
+    """A shard that cannot hold what it is routed (rank 0 here) makes EVERY rank raise at the
+    walk's first check (it still takes part in every exchange before it), instead of leaving the
+    others blocked in the next collective."""
     world = 2
     mp.start_processes(_rank_main, args=(world, _free_port(), "small51", str(tmp_path), None, None, 3),
                        nprocs=world, join=True, start_method="spawn")

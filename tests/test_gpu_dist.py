@@ -169,3 +169,28 @@ def test_sharded_stats_leave_no_hip_error():
     assert torch.ones(64, device="cuda").sum().item() == 64  # raises on a stale HIP error
     sh.table.close()
     assert torch.ones(64, device="cuda").sum().item() == 64
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_sharded_host_syncs_per_step(P):
+    """Device-resident rounds: fixed-size exchange slots (no host read per walk round), the
+    splitter chains ranked on the device from an all-gathered predecessor table (no jump rounds),
+    the walk's end checked where the last step ended. C3 shape (k=51, contigs U[8,200]) over P
+    logical ranks, second step (buffers sized by the first): at most 8 blocking host reads per
+    rank and step, this host's and the library's (kh_host_syncs), output == ground truth."""
+    from cs267_hw3_amd.dist import run_threaded
+    g = kh.SyntheticKmers(51, 4_000_000, 8, 200, 0, seed=51)
+    info = {}
+    check_ranks(g, run_threaded(51, g.records(), P, info=info, steps=2), P)
+    assert max(info["syncs"].values()) <= 8, info["syncs"]
+    assert max(info["checks"].values()) == 1, info["checks"]
+
+
+@pytest.mark.parametrize("P", [1, 3, 4])
+def test_sharded_tiny_slots_hold_messages_back(monkeypatch, P):
+    """Slots of 64 messages: most walkers are held back on their sender and go out in later rounds
+    (and at one rank, resent to itself); the walk still ends with every contig exact."""
+    from cs267_hw3_amd import dist
+    monkeypatch.setattr(dist.DistributedKmerHashMap, "SLOT_CAP_MAX", 64)
+    g = kh.SyntheticKmers(51, 300_000, 8, 200, 0, seed=7 + P)
+    check_ranks(g, dist.run_threaded(51, g.records(), P, steps=2), P)

@@ -87,7 +87,8 @@ int main(int argc, char** argv) {
     const uint64_t split = (n_total + P - 1) / P;  // read_kmers.hpp:55-58 block split
     std::vector<double> mean_s(P, 0.0);
     std::vector<std::vector<double>> step_ms(P);
-    std::vector<int> ok(P, 1), rounds(P, 0);
+    std::vector<int> ok(P, 1), rounds(P, 0), checks(P, 0);
+    std::vector<uint64_t> syncs(P, 0);
     std::vector<uint64_t> lookups(P, 0), contigs(P, 0);
     std::mutex em;
     std::exception_ptr first;
@@ -106,8 +107,11 @@ int main(int argc, char** argv) {
                 kh::hip_check(hipStreamSynchronize(sh.stream()), "hipStreamSynchronize");
                 auto step = [&] {
                     sh.clear();
+                    const uint64_t s0 = sh.host_syncs();
                     sh.insert_all_dev(recs, e - b);
                     rounds[r] = sh.assemble(n_total);
+                    syncs[r] = sh.host_syncs() - s0;  // blocking device reads of this step
+                    checks[r] = sh.checks();
                 };
                 for (int i = 0; i < o.warmup; ++i) step();
                 double sum = 0;
@@ -161,11 +165,13 @@ int main(int argc, char** argv) {
            "\"step_ms_rank0\": [%s], \"higher_is_better\": true, \"scaling\": \"weak\", \"dtype\": \"u64\", "
            "\"data\": \"synthetic\", \"config\": {\"workload\": \"contigs U[%u,%u] k-mers, %llu k-mers per rank\", "
            "\"k\": %d, \"n_kmers_total\": %llu, \"contigs\": %llu, \"lookups\": %llu, \"walk_rounds\": %d}, "
-           "\"verified_vs_truth\": %s, \"gen_s\": %.1f}\n",
+           "\"verified_vs_truth\": %s, \"host_syncs_per_step_max\": %llu, \"walk_checks\": %d, \"gen_s\": %.1f}\n",
            o.k, (double)(n_total + nl) / tmax, std::min(P, ngpu), P, rccl ? "rccl" : "thread", o.steps, o.warmup,
            1e3 * tmax, steps_s.c_str(), o.len_min, o.len_max, (unsigned long long)o.n, o.k,
            (unsigned long long)n_total, (unsigned long long)nc, (unsigned long long)nl, rounds[0],
-           o.verify ? (all_ok ? "true" : "false") : "null", gen_s);
+           o.verify ? (all_ok ? "true" : "false") : "null",
+           (unsigned long long)*std::max_element(syncs.begin(), syncs.end()),
+           *std::max_element(checks.begin(), checks.end()), gen_s);
     kh_gen_destroy(g);
     return all_ok ? 0 : 3;
 }
