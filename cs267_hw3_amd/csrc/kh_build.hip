@@ -135,7 +135,7 @@ bool part_usable(const KParams& p, uint64_t cap, uint64_t n) {
 // that one is remapped (hot_on: the table has remapped regions; one uniform test per block).
 __device__ __forceinline__ uint32_t part_region(uint32_t win, Key k, const KParams& p, bool hot_on) {
     const uint32_t r = mini_region(win, p);
-    return (hot_on && region_is_hot(p.hot, r)) ? hot_region(key_hash32(k), p) : r;
+    return (hot_on && region_is_hot(p.hot, r)) ? hot_region(k, win, p) : r;
 }
 
 // ---- record -> word conversion (k other than 51 / 19) ---------------------------------------------
@@ -638,6 +638,59 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
     }
 }
 
+// ---- sorted slice insert (balanced tables, load > 0.6) ----------------------------------------
+// At high load linear probing in the slice is the build's cost: an insert probes ~(1 + 1/(1-a)^2)/2
+// slots (23 at a = 0.85) and a wave waits for its lanes' longest run. Instead the slice is laid out
+// as sequential linear probing in home order would leave it: with c(h) keys of home h,
+// C(h) = c(0) + .. + c(h) and M(h) = max over h' <= h of (h' - C(h' - 1)), the keys of home h take
+// slots C(h - 1) + M(h) + 0, 1, .. (E(h) = C(h) + M(h) is the first free slot after them), so an
+// insert is one LDS atomic (its rank among its home's keys) and two block scans over the slots, with
+// no probing and no CAS; every key lies at or after its home with no EMPTY slot in between, which is
+// all a linear-probing lookup needs. Keys of one home are consecutive, so duplicates are found by
+// comparing with the earlier keys of the same home.
+// Thread t scans the slots [t*E, t*E + E) of the slice: returns through hist[i] the first slot of
+// home i (C(i-1) + M(i)); wsum / wmax: TB / 64 words of LDS scratch.
+template <int TB>
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t& total, uint32_t* wsum);
+template <int TB>
+__device__ __forceinline__ void sorted_starts(uint32_t* hist, uint32_t S, uint32_t* wsum, int32_t* wmax) {
+    const uint32_t E = (S + TB - 1) / TB;
+    const uint32_t i0 = min(threadIdx.x * E, S), i1 = min(i0 + E, S);
+    uint32_t tot = 0;
+    for (uint32_t i = i0; i < i1; ++i) tot += hist[i];
+    uint32_t all;
+    const uint32_t base = block_scan_u32<TB>(tot, all, wsum);  // C(i0 - 1)
+    // prefix max of v(i) = i - C(i - 1): this thread's run, then across threads (exclusive)
+    int32_t run = INT32_MIN;
+    uint32_t c = base;
+    for (uint32_t i = i0; i < i1; ++i) {
+        run = max(run, (int32_t)i - (int32_t)c);
+        c += hist[i];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int32_t x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = max(x, y);
+    }
+    if (lane == 63) wmax[w] = x;
+    lds_barrier();
+    int32_t pre = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < TB / 64; ++k)
+        if (k < w) pre = max(pre, wmax[k]);
+    const int32_t xin = __shfl_up(x, 1, 64);
+    int32_t m = max(pre, lane ? xin : INT32_MIN);  // max over the slots before i0
+    c = base;
+    for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t ci = hist[i];
+        m = max(m, (int32_t)i - (int32_t)c);
+        hist[i] = c + (uint32_t)m;
+        c += ci;
+    }
+}
+
 // Build from fixed region windows: each thread holds up to IPT words of the region it inserts;
 // region hand-offs use LDS-only barriers, so a block's window loads (issued right after the
 // previous region's write-out), LDS work and slice stores overlap across blocks.
@@ -649,7 +702,7 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
 // reload-and-rechain path compiled in, spills on that path made the compiler drain every
 // outstanding store (vmcnt(0)) at the top of each region; the fresh kernel has no spills and its
 // slice stores drain in the background (C3 build 4.31 -> 3.86 ms).
-template <int W, int IPT, int KT, bool FRESH>
+template <int W, int IPT, int KT, bool FRESH, bool SORT = false>
 __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_part_build_pf(KParams p_in, const uint64_t* __restrict__ buf2,
                                                                  uint64_t* slots, uint64_t cap,
                                                                  uint64_t* ovf, uint64_t ovf_cap,
@@ -700,6 +753,68 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         // load 0.85: build 21.3 -> 13.0 ms); slot steps below (C3 at 0.5: 3.71 vs 3.90 ms)
         const bool dense = KH_LDS_BLOCK && 3u * m_cur > 2u * S;
         if (threadIdx.x == 0) hcnt = 0;
+        int pos[IPT];  // LDS slot of each word inserted here (chains walk from these)
+        if constexpr (SORT) {
+            static_assert(FRESH && Slice<W>::SPLIT, "the sorted slice needs a fresh table and the split layout");
+            // sorted slice (FRESH only): word 0 EMPTY, the word-1 array holds the home counts
+            uint32_t* hist = reinterpret_cast<uint32_t*>(lt.p1(0));
+            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                *lt.p0(i) = EMPTY;
+                hist[i] = 0;
+            }
+            lds_barrier();
+            BPROF(0);
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {  // home | rank among the keys of that home << 16
+                pos[j] = LDS_DUP;
+                if (a[j] == EMPTY) continue;
+                const uint32_t h = (uint32_t)(home_in(lo, hi, key_hash32(slot_key(a[j], b[j], p))) - lo);
+                pos[j] = (int)(h | (atomicAdd(&hist[h], 1u) << 16));
+            }
+            lds_barrier();
+            __shared__ uint32_t wsum[BUILD_THREADS / 64];
+            __shared__ int32_t wmax[BUILD_THREADS / 64];
+            sorted_starts<BUILD_THREADS>(hist, S, wsum, wmax);
+            lds_barrier();
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                if (pos[j] < 0) continue;
+                const uint32_t slot = hist[(uint32_t)pos[j] & 0xFFFFu] + ((uint32_t)pos[j] >> 16);
+                if (slot >= S) {  // the run left the slice: global CAS insert after the build
+                    const unsigned long long idx = atomicAdd(&ctr[CT_OVF2], 1ull);
+                    if (idx < ovf_cap) {
+                        ovf[idx * W] = a[j];
+                        if (W == 2) ovf[idx * W + 1] = b[j];
+                    } else {
+                        atomicAdd(&stats[ST_FULL], 1ull);
+                    }
+                    pos[j] = LDS_OUT;
+                } else {
+                    pos[j] = (int)(slot | ((uint32_t)pos[j] & 0xFFFF0000u));  // slot | rank << 16
+                }
+            }
+            lds_barrier();  // every lane has read the starts before the word-1 array is written
+#pragma unroll
+            for (int j = 0; j < IPT; ++j)
+                if (pos[j] >= 0) lt.put((uint32_t)pos[j] & 0xFFFFu, slot_clean(a[j], p), b[j]);
+            lds_barrier();
+            // duplicates: the keys of one home are consecutive, so a key equal to this one is one of
+            // the `rank` keys right before it
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                if (pos[j] < 0) continue;
+                const uint32_t sl = (uint32_t)pos[j] & 0xFFFFu, rk = (uint32_t)pos[j] >> 16;
+                pos[j] = (int)sl;
+                const uint64_t want0 = slot_keybits(a[j], p);
+                for (uint32_t t = sl - rk; t < sl; ++t) {
+                    if (slot_keybits(lt.w0(t), p) == want0 && (W == 1 || lt.w1(t) == b[j])) {
+                        atomicAdd(&stats[ST_DUP], 1ull);
+                        break;
+                    }
+                }
+            }
+            BPROF(1);
+        } else {
         if (W == 2) {
             const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
             for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
@@ -718,7 +833,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         else
             __syncthreads();
         BPROF(0);
-        int pos[IPT];  // LDS slot of each word inserted here (chains walk from these)
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             pos[j] = LDS_DUP;
@@ -740,6 +854,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         }
         lds_barrier();
         BPROF(1);
+        }  // probing insert
         // The next region's window goes into a/b as soon as this region's words are consumed
         // (after the inserts, or after the links that read them), so its loads are in flight
         // during the remaining phases and never queue behind the write-out's stores.
@@ -782,6 +897,10 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 uint64_t x, y, x2, y2;
                 lt.get(i, x, y);
                 lt.get(two ? i2 : i, x2, y2);
+                if (SORT) {  // the word-1 array held the home counts: empty slots are all-ones
+                    y = x == EMPTY ? EMPTY : y;
+                    y2 = x2 == EMPTY ? EMPTY : y2;
+                }
                 if (hcap && x != EMPTY) clean_out<W>(x, y, p);
                 if (hcap && x2 != EMPTY) clean_out<W>(x2, y2, p);
                 dst[i] = make_ulonglong2(x, y);
@@ -814,7 +933,13 @@ static unsigned pf_grid() {
 }
 
 template <int W, int IPT, int KT, class... A>
-static void pf_launch(bool fresh, size_t lds, hipStream_t s, A... a) {
+static void pf_launch(bool fresh, bool sorted, size_t lds, hipStream_t s, A... a) {
+    if constexpr (W == 2 && Slice<W>::SPLIT) {
+        if (fresh && sorted) {
+            k_part_build_pf<W, IPT, KT, true, true><<<pf_grid(), BUILD_THREADS, lds, s>>>(a...);
+            return;
+        }
+    }
     if (fresh) {
         k_part_build_pf<W, IPT, KT, true><<<pf_grid(), BUILD_THREADS, lds, s>>>(a...);
     } else {
@@ -831,6 +956,9 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
     const uint32_t smax = (uint32_t)region_max_slots(p, t.cap);
     const uint32_t hcap = B.headrec ? B.hcap : 0u;
     const int prof = debug_flag("build_prof") ? 1 : 0;
+    // balanced (high-load) tables: sorted slice insert instead of probing (KH_DEBUG=probe_build: off)
+    // (word 1 array of the split layout holds the home counts: 16-B slots only)
+    const bool sorted = p.rb != nullptr && W == 2 && Slice<W>::SPLIT && !debug_flag("probe_build");
     if (prof) {
         static const unsigned long long zero[8] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_build_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, s);
@@ -839,13 +967,13 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
                                                          stats, RC, rcnt, B.headrec, hcap, smax, B.rbt);
     else if (RC <= 4u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 4, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 4, decltype(kt)::value>(table_empty, sorted, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
     else if (RC <= 6u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 6, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 6, decltype(kt)::value>(table_empty, sorted, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
     else if (RC <= 12u * BUILD_THREADS)
-        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 12, decltype(kt)::value>(table_empty, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
+        with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 12, decltype(kt)::value>(table_empty, sorted, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
                                                                 ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
     else
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
@@ -902,6 +1030,20 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t& total, 
     return pre + x - v;
 }
 
+#ifndef KH_STREAM_NT
+#define KH_STREAM_NT 0
+#endif
+// 16-B load of a streamed input (records, pass-1 / pass-2 windows), non-temporal under
+// KH_STREAM_NT: read once, it need not displace the windows' partly written lines in L2
+__device__ __forceinline__ ulonglong2 ld_stream16(const void* q) {
+    if (KH_STREAM_NT) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q));
+        return make_ulonglong2(v.x, v.y);
+    }
+    return *reinterpret_cast<const ulonglong2*>(q);
+}
+
 template <int W, int TB, int TILE>
 __device__ __forceinline__ void load_words_tb(const uint64_t* __restrict__ words, uint64_t base, uint64_t end,
                                               uint64_t last, uint64_t* a, uint64_t* b) {
@@ -912,7 +1054,7 @@ __device__ __forceinline__ void load_words_tb(const uint64_t* __restrict__ words
         const uint64_t ii = i < end ? i : last;
         uint64_t x0, x1 = 0;
         if (W == 2) {
-            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(words + 2 * ii);
+            const ulonglong2 v = ld_stream16(words + 2 * ii);
             x0 = v.x;
             x1 = v.y;
         } else {
@@ -942,7 +1084,7 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
         const uint64_t i = ok ? (uint64_t)(bk * S1 + w) * CAP1 + (v - pw) : (uint64_t)bk * S1 * CAP1;
         uint64_t x0, x1 = 0;
         if (W == 2) {
-            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(buf1 + 2 * i);
+            const ulonglong2 x = ld_stream16(buf1 + 2 * i);
             x0 = x.x;
             x1 = x.y;
         } else {
@@ -1196,7 +1338,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
             const uint64_t g = ((r0 * R) & ~15ull) + 16ull * lane;
             a[j] = b[j] = 0;
             if (r0 < end && lane < 62 && g < nbytes) {
-                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(recs + g);
+                const ulonglong2 v = ld_stream16(recs + g);
                 a[j] = v.x;
                 b[j] = v.y;
             }
@@ -1751,7 +1893,7 @@ __global__ __launch_bounds__(256) void k_region_count(KParams p, const uint8_t* 
 
 hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
                               uint64_t cap, uint32_t* rcnt, uint32_t* hot, uint32_t* hot_list,
-                              unsigned long long* ctr, hipStream_t s) {
+                              unsigned long long* ctr, hipStream_t s, uint64_t total) {
     hipError_t e;
     if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 16, s)) != hipSuccess) return e;
@@ -1765,11 +1907,15 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
             else k_region_count<1, false><<<grid, 256, 0, s>>>(p, nullptr, words, n, rcnt, 0);
         }
     }
-    // linear probing across region boundaries: remap what would fill more than 15/16 of a slice
+    // linear probing across region boundaries: remap what would fill more than 15/16 of a slice.
+    // The first of several staged batches (total > n) is a sample of the build: its counts are
+    // scaled up (with the sampled mark's noise guard) instead of compared with whole slices.
     KParams q = p;
     q.hot = hot;
-    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, 0xFFFFFFFFu, 1, 0, rcnt, hot, hot_list, ctr, 1, 0,
-                                                     balanced_T(p, cap, n));
+    int shift = 0;
+    while (n && total > n && ((uint64_t)n << (shift + 1)) <= total) ++shift;
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, 0xFFFFFFFFu, shift ? 0 : 1, shift, rcnt, hot, hot_list,
+                                                     ctr, 1, 0, balanced_T(p, cap, total > n ? total : n));
     if (p.rb) {  // balanced bounds from the counts after the remap (a second, hot-aware count)
         if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
         if (n) {

@@ -120,7 +120,7 @@ struct kh_table {
     DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
     // splitter segments of the migrating walk (kh_mseg.hip)
     DevBuf ms_len, ms_hi, ms_lo, ms_has, ms_done, ms_jump, ms_acc, ms_stab, ms_stab_id, ms_qsrc, ms_misc;
-    DevBuf mw_pack, mw_cnt, mw_list, mw_carry[2], mw_carry_dst[2];  // fixed-slot rounds
+    DevBuf mw_cnt, mw_list, mw_carry[2], mw_carry_dst[2];  // fixed-slot rounds
     DevBuf ms_res[6], ms_pend;               // pointer jumping over the gathered predecessor tables
     DevBuf route_spl;                        // splitter k-mers routed to each owner (MAX_RANKS words)
     int mw_cur = 0;                          // carry buffer written by the last round
@@ -283,14 +283,14 @@ bool balanced_bounds(const kh_table* t) {
 
 // CAS-path insert into an empty table: remap the minimizer regions the batch would overfill
 // (kh_build.hip launch_hot_prepass); later batches place keys with the same bitmap.
-int cas_hot_prepass(kh_table* t, const void* recs, const void* words, uint64_t n) {
+int cas_hot_prepass(kh_table* t, const void* recs, const void* words, uint64_t n, uint64_t total = 0) {
     if (t->n_inserted != 0 || kh::debug_flag("no_hot")) return KH_OK;
     if (int rc = t->pb_cnt.ensure(kh::part_count_words() * 8)) return rc;
     uint32_t* rcnt = t->pb_cnt.as<uint32_t>() + kh::PART_W1_COUNTERS;
     KH_HIP(hipMemsetAsync(t->hot.p, 0, kh::HOT_WORDS * 4, t->stream));
     KH_HIP(kh::launch_hot_prepass(t->kp, (const uint8_t*)recs, (const uint64_t*)words, n, t->cap, rcnt,
                                   t->hot.as<uint32_t>(), rcnt + kh::HOT_WORDS * 32, t->ctr.as<unsigned long long>(),
-                                  t->stream));
+                                  t->stream, total));
     return KH_OK;
 }
 
@@ -397,7 +397,7 @@ int kh_destroy(kh_table* t) {
                       &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
-                      &t->mw_pack, &t->mw_cnt, &t->mw_list, &t->mw_carry[0], &t->mw_carry[1], &t->mw_carry_dst[0],
+                      &t->mw_cnt, &t->mw_list, &t->mw_carry[0], &t->mw_carry[1], &t->mw_carry_dst[0],
                       &t->mw_carry_dst[1], &t->ms_res[0], &t->ms_res[1], &t->ms_res[2], &t->ms_res[3], &t->ms_res[4],
                       &t->ms_res[5], &t->ms_pend, &t->route_spl,
                       &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot, &t->rbounds, &t->start_rec};
@@ -475,8 +475,7 @@ int kh_set_stream(kh_table* t, void* s) {
 int kh_sync(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     if (int rc = set_device(t)) return rc;
-    KH_SYNC(t);
-    return check_stats(t);
+    return check_stats(t);  // one wait: the stats read is ordered after the queued work
 }
 
 uint64_t kh_capacity(const kh_table* t) { return t ? t->cap : 0; }
@@ -627,8 +626,7 @@ static int insert_chunked_upload(kh_table* t, const uint8_t* host_recs, uint64_t
     t->last_insert_part = true;
     t->n_inserted += n;
     t->assembled = false;
-    KH_SYNC(t);
-    return check_stats(t);
+    return check_stats(t);  // one wait: the stats read is ordered after the queued work
 }
 
 int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n) {
@@ -645,8 +643,7 @@ int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n) {
     if (int rc = t->stage.ensure(bytes)) return rc;
     KH_HIP(hipMemcpyAsync(t->stage.p, host_recs, bytes, hipMemcpyHostToDevice, t->stream));
     if (int rc = kh_insert_dev(t, t->stage.p, n)) return rc;
-    KH_SYNC(t);
-    return check_stats(t);
+    return check_stats(t);  // one wait: the stats read is ordered after the queued work
 }
 
 int kh_find_dev(kh_table* t, const void* dev_keys, uint64_t n, void* dev_out, void* dev_found) {
@@ -877,8 +874,7 @@ int kh_assemble_dev(kh_table* t) {
 
 int kh_assemble(kh_table* t, uint64_t* n_contigs, uint64_t* out_bytes) {
     if (int rc = kh_assemble_dev(t)) return rc;
-    KH_SYNC(t);
-    if (int rc = check_stats(t)) return rc;
+    if (int rc = check_stats(t)) return rc;  // one wait (ordered after the queued work)
     uint64_t ob = 0;
     if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
     if (n_contigs) *n_contigs = t->last_contigs;
@@ -1255,8 +1251,8 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
                                      t->stream, coll ? t->splits.as<uint64_t>() : nullptr,
                                      coll ? t->splits_cap : 0, t->stage_fresh && t->stage_n == 0, t->cap));
     } else {
-        if (t->stage_n == 0)
-            if (int rc = cas_hot_prepass(t, nullptr, words, m)) return rc;
+        if (t->stage_n == 0)  // the first staged batch stands for the whole build (stage_total)
+            if (int rc = cas_hot_prepass(t, nullptr, words, m, t->stage_total)) return rc;
         KH_HIP(kh::launch_insert_words(t->kp, (const uint64_t*)words, m, view(t),
                                        t->stats.as<unsigned long long>(), t->stream));
     }
@@ -1289,23 +1285,6 @@ int kh_insert_words_finish(kh_table* t) {
 }
 
 // ---- migrating-walker rounds --------------------------------------------------------------------
-namespace {
-// Grow b to >= want bytes keeping its first `used` bytes.
-int grow_keep(kh_table* t, DevBuf& b, uint64_t want, uint64_t used) {
-    if (want <= b.bytes && b.p) return KH_OK;
-    uint64_t nb = b.bytes + b.bytes / 2;
-    if (nb < want) nb = want;
-    DevBuf n;
-    if (int rc = n.ensure(nb)) return rc;
-    if (used) KH_HIP(hipMemcpyAsync(n.p, b.p, used, hipMemcpyDeviceToDevice, t->stream));
-    KH_SYNC(t);
-    b.release();
-    b.p = n.p;
-    b.bytes = n.bytes;
-    n.p = nullptr;
-    return KH_OK;
-}
-}  // namespace
 
 static kh::MSegState mseg_state(kh_table* t) {
     kh::MSegState st;
@@ -1349,8 +1328,12 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     const uint64_t nseg = ns + nsp;
     // walkers of every rank: a rank may host (and hold back) at most all of them in a round
     t->mw_wg = total_walkers > nseg ? total_walkers : nseg;
+    // text store: a walker appends each k-mer of this shard once, 32 bases per full word record,
+    // and leaves at most a partial word, its finish record and a 2-record link where it ends
+    // (held-back walkers flush nothing extra): shard / 32 + 4 per walker of every rank, doubled
+    const uint64_t store_cap = 2 * (t->n_inserted / 32 + 4 * t->mw_wg) + 4096;
     if ((rc = t->mw_init.ensure((nseg + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_misc.ensure(64)) ||
-        (rc = t->mw_store.ensure((nseg + 1024) * 16)))
+        (rc = t->mw_store.ensure(store_cap * 16)))
         return rc;
     t->ms_ns = ns;
     t->ms_nsp = nsp;
@@ -1375,7 +1358,7 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     t->rw_n = nseg;
     t->rw_total = total_kmers > ns ? total_kmers : ns;
     t->mw_store_n = 0;
-    t->mw_store_bound = 0;
+    t->mw_store_bound = store_cap;
     t->mw_store_known = false;
     t->mw_cur = 0;
     KH_HIP(hipMemsetAsync(mw_word(t, 2), 0, 8 * 4, t->stream));  // store count, walkers, carries
@@ -1442,7 +1425,7 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
     if ((rc = t->mw_tmp.ensure((nb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_dst.ensure(nb + 1)) ||
         (rc = t->mw_stage.ensure((nb + 1) * kh::MW_REC_SLOTS * 16)) || (rc = t->mw_nrec.ensure(nb + 1)) ||
         (rc = t->mw_off.ensure((nb + 1) * 8)) || (rc = t->scratch.ensure(kh::scan_scratch_words(nb) * 8 + 64)) ||
-        (rc = t->mw_pack.ensure((nb + cb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_cnt.ensure((P + 1) * 8)) ||
+        (rc = t->mw_cnt.ensure((2 * P + 2) * 8)) ||
         (rc = t->mw_carry[0].ensure((cb + 1) * kh::MSG_WORDS * 8)) ||
         (rc = t->mw_carry[1].ensure((cb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_carry_dst[0].ensure(cb + 1)) ||
         (rc = t->mw_carry_dst[1].ensure(cb + 1)) || (rc = ensure_route(t, nb + cb, (int)P)))
@@ -1464,13 +1447,11 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
     mw.nrec = t->mw_nrec.as<uint8_t>();
     KH_HIP(kh::launch_mw_run(t->kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
     // text records of this round -> the rank-local store at offsets continuing its device-side
-    // count (the store is sized from an upper bound: MW_REC_SLOTS per walker and round)
+    // count (sized at begin; a walk that would pass it fails instead of overrunning it)
     unsigned long long* store_n = mw_word(t, 2);
-    const uint64_t add = nb * (uint64_t)kh::MW_REC_SLOTS;
-    if ((rc = grow_keep(t, t->mw_store, (t->mw_store_bound + add) * 16 + 16, t->mw_store_bound * 16))) return rc;
     KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), store_n, t->stream));
-    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>(), t->stream));
-    t->mw_store_bound += add;
+    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>(), t->mw_store_bound,
+                                 t->stats.as<unsigned long long>(), t->stream));
     // outgoing walkers (+ the ones held back last round) -> P slots of out_cap; overflow held back
     const int cur = t->mw_cur, nxt = 1 - cur;
     kh::SlotRound r;
@@ -1489,7 +1470,6 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
     r.carry_dst_out = t->mw_carry_dst[nxt].as<uint8_t>();
     r.carry_n_out = mw_word(t, 4 + nxt);
     r.live = (unsigned long long*)dev_live;
-    r.pack = t->mw_pack.as<uint64_t>();
     r.cnt = t->mw_cnt.as<uint64_t>();
     KH_HIP(kh::launch_slot_round(r, t->route_hist.as<uint64_t>(), t->route_off.as<uint64_t>(),
                                  t->route_scratch.as<uint64_t>(), t->stream));

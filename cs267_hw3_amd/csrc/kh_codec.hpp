@@ -335,14 +335,33 @@ struct Place {
 };
 // Hot regions (a repeat family, a low-complexity run, the C5 hot-bucket set: one minimizer window
 // shared by far more k-mers than a region holds) are remapped as a whole: their keys go to the
-// region of a second mix of the key hash, so they spread evenly over every region (the home
-// inside it is still home_in(.., key_hash32): the extra mix keeps region and home independent).
-KH_HD uint32_t hot_region(uint32_t h, const KParams& p) { return mix32(h ^ 0x2545F491u) >> (32 - p.rbits); }
+// region of a hash of (the minimizer window, the k-mer's secondary window: the smallest-order
+// window whose content differs from the minimizer's). Consecutive k-mers of a contig keep their
+// secondary window for ~18 steps at K=51, M=16 (it changes when it drops out or a smaller one
+// enters), so runs of a hot family still land in one region and keep their chains, while the
+// family spreads over ~family size / 18 regions (a hash of the whole key spread it too, but broke
+// every run: the C5 hot-bucket walk was one lookup per k-mer). The home inside the region is still
+// home_in(.., key_hash32).
+KH_HD uint32_t second_window(Key k, uint32_t win, const KParams& p) {
+    uint32_t best = 0xFFFFFFFFu, bw = win;
+    for (int j = 0; j <= p.K - p.M; ++j) {
+        const uint32_t w = win_bits(k, j, p);
+        const uint32_t o = (win_order(w) << 6) | (uint32_t)j;
+        if (w != win && o < best) {
+            best = o;
+            bw = w;
+        }
+    }
+    return bw;
+}
+KH_HD uint32_t hot_region(Key k, uint32_t win, const KParams& p) {
+    return mix32((win * 0x9E3779B1u) ^ second_window(k, win, p) ^ 0x2545F491u) >> (32 - p.rbits);
+}
 KH_HD bool region_is_hot(const uint32_t* hot, uint32_t r) { return hot && ((hot[r >> 5] >> (r & 31u)) & 1u); }
 KH_HD Place place_w(uint32_t win, Key k, const KParams& p) {
     uint32_t r = mini_region(win, p);
     const uint32_t h = key_hash32(k);
-    if (region_is_hot(p.hot, r)) r = hot_region(h, p);
+    if (region_is_hot(p.hot, r)) r = hot_region(k, win, p);
     return Place{r, h};
 }
 KH_HD Place place(Key k, const KParams& p) { return place_w(mini_window(k, mini_scan(k, p), p), k, p); }

@@ -218,8 +218,7 @@ hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, u
                               unsigned long long* n, hipStream_t s);
 // this round's outgoing messages (walk outputs j < *n_dev with a destination, then the messages
 // held back last round) -> P slots of cap (overflow held back in carry_out / carry_dst_out,
-// *carry_n_out); live = [messages in flight, largest per-destination count]. pack / cnt: scratch
-// of (nb + cb) messages / P + 1 words.
+// *carry_n_out); live = [messages in flight, largest per-destination count].
 struct SlotRound {
     uint32_t P;
     uint64_t nb;                     // walk outputs (bound)
@@ -236,8 +235,7 @@ struct SlotRound {
     uint8_t* carry_dst_out;
     unsigned long long* carry_n_out;
     unsigned long long* live;        // 2 words
-    uint64_t* pack;                  // (nb + cb) * MSG_WORDS
-    uint64_t* cnt;                   // P + 1
+    uint64_t* cnt;                   // 2P + 1 words of scratch
 };
 hipError_t launch_slot_round(const SlotRound& r, uint64_t* hist, uint64_t* off, uint64_t* scratch, hipStream_t s);
 // *out = a + min(*b, bmax) (the first round's live walkers: starts + collected splitters)
@@ -246,7 +244,9 @@ hipError_t launch_add_count(unsigned long long* out, uint64_t a, const unsigned 
 // text records of this round: absolute store offsets continuing *store_n (device counter, updated)
 hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
                                   unsigned long long* store_n, hipStream_t s);
-hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, hipStream_t s);
+// store_cap: the store's records; a round that would pass it fails the walk (ST_CHUNK_OVF)
+hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, uint64_t store_cap,
+                             unsigned long long* stats, hipStream_t s);
 hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, uint64_t* scratch,
                            uint64_t* out, uint64_t* counts, hipStream_t s);
 hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
@@ -348,9 +348,11 @@ void launch_bounds(const KParams& p, uint64_t cap, const uint32_t* counts, uint3
 // CAS-path inserts into an empty table (batches too small for the partitioned build): count the
 // batch's keys per minimizer region and remap the regions that cannot hold theirs (records or
 // routed words), so a repeat family does not pile up one linear-probing run.
+// total: the whole build when this batch is the first of several staged ones (its counts are then
+// scaled up to it); 0 = this batch is the build
 hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
                               uint64_t cap, uint32_t* rcnt, uint32_t* hot, uint32_t* hot_list,
-                              unsigned long long* ctr, hipStream_t s);
+                              unsigned long long* ctr, hipStream_t s, uint64_t total = 0);
 // chain head records per region for a table of cap slots (0: K or LDS leave no room for chains)
 uint32_t part_head_cap(const KParams& p, uint64_t cap);
 

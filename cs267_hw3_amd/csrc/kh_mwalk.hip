@@ -309,10 +309,15 @@ struct NrecF {
 
 __global__ __launch_bounds__(BLOCK) void k_mw_compact(const uint64_t* stage, const uint8_t* nrec,
                                                       const uint64_t* off, uint64_t nb, uint64_t* store,
-                                                      const unsigned long long* n_dev) {
+                                                      const unsigned long long* n_dev, uint64_t store_cap,
+                                                      unsigned long long* stats) {
     const uint64_t n = n_dev ? min((uint64_t)*n_dev, nb) : nb;
     for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
         const uint32_t c = nrec[j];
+        if (off[j] + c > store_cap) {  // the store's bound was wrong (a cycle?): fail, never overrun
+            atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+            continue;
+        }
         const ulonglong2* src = reinterpret_cast<const ulonglong2*>(stage + j * (MW_REC_SLOTS * 2));
         ulonglong2* dst = reinterpret_cast<ulonglong2*>(store + off[j] * 2);
         for (uint32_t r = 0; r < c; ++r) dst[r] = src[r];
@@ -422,9 +427,11 @@ hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t*
     return scan_exclusive(NrecF{mw.nrec, mw.n_dev}, mw.n_in, off, scratch, store_n, (unsigned long long*)nullptr, s);
 }
 
-hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, hipStream_t s) {
+hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, uint64_t store_cap,
+                             unsigned long long* stats, hipStream_t s) {
     if (mw.n_in == 0) return hipSuccess;
-    k_mw_compact<<<grid_for(mw.n_in, 8192), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store, mw.n_dev);
+    k_mw_compact<<<grid_for(mw.n_in, 8192), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store, mw.n_dev, store_cap,
+                                                           stats);
     return hipGetLastError();
 }
 
@@ -481,9 +488,13 @@ hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, u
 }
 
 // outgoing messages of a round: last round's held-back ones first (they go out before newer
-// ones to the same destination), then the walk outputs with a destination
+// ones to the same destination), then the walk outputs with a destination; each lands straight in
+// its destination's slot, or past the slot's capacity in the held-back list
 struct SlotMsgOp {
     SlotRound r;
+    const uint64_t* off;   // owner-major exclusive scan of the per-block counts (start of q's run)
+    uint64_t nbk;          // blocks of the grouping
+    const uint64_t* cbase; // held-back list position of each destination's overflow
     __device__ int owner(uint64_t i) const {
         if (i < r.cb) return i < *r.carry_n ? (int)r.carry_dst[i] : -1;
         const uint64_t j = i - r.cb;
@@ -492,63 +503,59 @@ struct SlotMsgOp {
     __device__ void emit(uint64_t i, int q, uint64_t d) const {
         if (q < 0) return;
         const uint64_t* a = i < r.cb ? r.carry + i * MSG_WORDS : r.tmp + (i - r.cb) * MSG_WORDS;
-        uint64_t* b = r.pack + d * MSG_WORDS;
-#pragma unroll
-        for (int w = 0; w < MSG_WORDS; ++w) b[w] = a[w];
-    }
-};
-
-// packed (grouped by destination, cnt[P+1]) -> slots of cap; the rest is held back for the next round
-__global__ __launch_bounds__(BLOCK) void k_slot_pack(SlotRound r) {
-    __shared__ uint64_t pre[MAX_RANKS + 1];
-    if (threadIdx.x == 0) {
-        uint64_t a = 0;
-        for (uint32_t q = 0; q < r.P; ++q) {
-            pre[q] = a;
-            a += r.cnt[q];
-        }
-        pre[r.P] = a;
-    }
-    __syncthreads();
-    const uint64_t tot = pre[r.P];
-    if (blockIdx.x == 0) {
-        if (threadIdx.x < r.P) {
-            const uint64_t c = r.cnt[threadIdx.x];
-            r.out[threadIdx.x * slot_words(r.cap)] = c < r.cap ? c : r.cap;
-            r.out[threadIdx.x * slot_words(r.cap) + 1] = 0;
-        }
-        if (threadIdx.x == 0) {
-            uint64_t mx = 0;
-            for (uint32_t q = 0; q < r.P; ++q) mx = r.cnt[q] > mx ? r.cnt[q] : mx;
-            r.live[0] = tot;
-            r.live[1] = mx;
-        }
-    }
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * BLOCK) {
-        uint32_t q = 0;
-        while (q + 1 < r.P && pre[q + 1] <= i) ++q;
-        const uint64_t k = i - pre[q];
-        const uint64_t* a = r.pack + i * MSG_WORDS;
+        const uint64_t k = d - off[(uint64_t)q * nbk];  // rank among the messages to q
         uint64_t* b;
         if (k < r.cap) {
-            b = r.out + q * slot_words(r.cap) + 2 + k * MSG_WORDS;
-        } else {  // slot full: held back (rare; carry capacity = every message of the round)
-            const unsigned long long c = atomicAdd(r.carry_n_out, 1ull);
+            b = r.out + (uint64_t)q * slot_words(r.cap) + 2 + k * MSG_WORDS;
+        } else {  // slot full: held back for a later round (rare)
+            const uint64_t c = cbase[q] + (k - r.cap);
             b = r.carry_out + c * MSG_WORDS;
             r.carry_dst_out[c] = (uint8_t)q;
         }
 #pragma unroll
         for (int w = 0; w < MSG_WORDS; ++w) b[w] = a[w];
     }
+};
+
+// slot headers, the held-back list's per-destination bases and its length, live = [messages in
+// flight, largest per-destination count]
+__global__ void k_slot_heads(SlotRound r, uint64_t* cbase) {
+    if (threadIdx.x == 0) {
+        uint64_t tot = 0, mx = 0, over = 0;
+        for (uint32_t q = 0; q < r.P; ++q) {
+            const uint64_t c = r.cnt[q];
+            r.out[q * slot_words(r.cap)] = c < r.cap ? c : r.cap;
+            r.out[q * slot_words(r.cap) + 1] = 0;
+            cbase[q] = over;
+            over += c > r.cap ? c - r.cap : 0;
+            tot += c;
+            mx = c > mx ? c : mx;
+        }
+        *r.carry_n_out = over;
+        r.live[0] = tot;
+        r.live[1] = mx;
+    }
 }
 
 hipError_t launch_slot_round(const SlotRound& r, uint64_t* hist, uint64_t* off, uint64_t* scratch, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(r.carry_n_out, 0, 8, s);
-    if (e != hipSuccess) return e;
+    const uint64_t n = r.nb + r.cb;
+    const uint64_t nbk = route_blocks(n);
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    if ((e = group_by_owner(SlotMsgOp{r}, r.nb + r.cb, r.P, hist, off, scratch + 1, r.cnt, total, s)) != hipSuccess)
-        return e;
-    k_slot_pack<<<grid_for(r.nb + r.cb, 4096), BLOCK, 0, s>>>(r);
+    uint64_t* cbase = r.cnt + r.P + 1;  // cnt holds 2P + 1 words
+    SlotMsgOp op{r, off, nbk, cbase};
+    if (nbk == 0) {  // nothing in flight: empty slots
+        hipError_t e = hipMemsetAsync(r.cnt, 0, (r.P + 1) * 8, s);
+        if (e != hipSuccess) return e;
+        k_slot_heads<<<1, 64, 0, s>>>(r, cbase);
+        return hipGetLastError();
+    }
+    k_group_hist<SlotMsgOp><<<(unsigned)nbk, BLOCK, 0, s>>>(op, n, r.P, hist);
+    hipError_t e = scan_exclusive(HistF{hist, nbk, r.P}, nbk * r.P, off, scratch + 1, (unsigned long long*)nullptr,
+                                  total, s);
+    if (e != hipSuccess) return e;
+    k_route_counts<0><<<1, MAX_RANKS, 0, s>>>(off, nbk, r.P, total, r.cnt);
+    k_slot_heads<<<1, 64, 0, s>>>(r, cbase);
+    k_group_scatter<SlotMsgOp><<<(unsigned)nbk, BLOCK, 0, s>>>(op, n, r.P, off, nbk);
     return hipGetLastError();
 }
 

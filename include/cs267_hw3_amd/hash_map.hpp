@@ -15,6 +15,7 @@
 #pragma once
 #include <memory>
 #include <stdexcept>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -80,7 +81,9 @@ private:
     }
     void flush() {
         if (pending_.empty()) return;
-        if (inserted_ == 0) grow(pending_.size());
+        // the first flush sizes the table for everything insert() may still accept (size_):
+        // a table holding k-mers cannot grow (kh_reserve), so a later flush must fit
+        if (inserted_ == 0) grow(std::max<uint64_t>(pending_.size(), size_));
         kh_detail::check(kh_insert(t_, reinterpret_cast<const uint8_t*>(pending_.data()), pending_.size()));
         inserted_ += pending_.size();
         pending_.clear();

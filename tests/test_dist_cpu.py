@@ -22,7 +22,7 @@ def _free_port():
 
 
 def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, insert_chunks=None, max_kmers=None,
-               windows=False):
+               windows=False, slot_cap=None, steps=1):
     import sys
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -43,9 +43,14 @@ def _rank_main(rank, world, port, name, outdir, chunk_bytes=None, insert_chunks=
         dm.PIPELINE_MIN = 0
     if chunk_bytes:
         dm.A2A_CHUNK_BYTES = chunk_bytes   # force the chunked all-to-all path
+    if slot_cap:
+        dm.SLOT_CAP_MAX = slot_cap         # tiny exchange slots: walkers held back on their sender
     try:
-        dm.insert_all(torch.from_numpy(recs))
-        rounds = dm.assemble(MANIFEST[name]["n"])
+        for step in range(steps):          # later steps size slots from the previous walk
+            if step:
+                shard.clear()
+            dm.insert_all(torch.from_numpy(recs))
+            rounds = dm.assemble(MANIFEST[name]["n"])
     except Exception as ex:                # every rank must fail together (no rank left waiting)
         with open(os.path.join(outdir, f"err_{rank}"), "w") as f:
             f.write(str(ex))
@@ -114,6 +119,22 @@ def test_sharded_route_windows_gloo(tmp_path, name, world, chunk, chunks):
     """The one-pass route's layout (each owner's words in its own window, not back to back):
     single and chunked all-to-all, and the pipelined insert, over gloo."""
     mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), chunk, chunks, None, True),
+                       nprocs=world, join=True, start_method="spawn")
+    import cs267_hw3_amd as kh
+    m = MANIFEST[name]
+    g = kh.SyntheticKmers(m["k"], m["n"], m["len_min"], m["len_max"], m["single_permille"],
+                          seed=m["seed"])
+    for r in range(world):
+        b, e = g.block(world, r)
+        assert open(tmp_path / f"test_{r}.dat", "rb").read() == g.truth(b, e)
+
+
+@pytest.mark.parametrize("name,world,cap", [("small51", 3, 2), ("mixed19", 2, 5), ("small51", 4, 64)])
+def test_sharded_tiny_slots_gloo(tmp_path, name, world, cap):
+    """Exchange slots of a few messages: walkers past a slot's capacity are held back on their
+    sender and go out in later rounds; two steps (the second sizes its slots from the first walk's
+    per-round counts, still capped); every rank's text equals its block's truth."""
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, str(tmp_path), None, None, None, False, cap, 2),
                        nprocs=world, join=True, start_method="spawn")
     import cs267_hw3_amd as kh
     m = MANIFEST[name]

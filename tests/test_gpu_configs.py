@@ -190,13 +190,6 @@ def test_c5_hot_bucket_200m_8_ranks(load):
     assert sum(s["n_inserted"] for s in info["stats"].values()) == 200_000_000
 
 
-def test_c5_skewed_1b_8_ranks():
-    """BASELINE configs[4] at SURVEY §8(d)'s size: the skewed set (walker skew: long chains, every
-    start k-mer in rank 0's block) at 1B k-mers over 8 ranks (logical, one GPU)."""
-    info = _sharded(_gen(C5, 1_000_000_000), 8)
-    assert sum(s["n_inserted"] for s in info["stats"].values()) == 1_000_000_000
-
-
 @pytest.mark.parametrize("load", [0.5, 0.85])
 def test_c5_hot_bucket_1b_8_ranks(load):
     """BASELINE configs[4] at SURVEY §8(d)'s size: the hot-bucket set (30 % of the contigs on 8

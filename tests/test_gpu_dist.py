@@ -188,9 +188,9 @@ def test_sharded_host_syncs_per_step(P):
 
 @pytest.mark.parametrize("P", [1, 3, 4])
 def test_sharded_tiny_slots_hold_messages_back(monkeypatch, P):
-    """Slots of 64 messages: most walkers are held back on their sender and go out in later rounds
-    (and at one rank, resent to itself); the walk still ends with every contig exact."""
+    """Slots of 256 messages: most walkers are held back on their sender and go out in later
+    rounds (and at one rank, resent to itself); the walk still ends with every contig exact."""
     from cs267_hw3_amd import dist
-    monkeypatch.setattr(dist.DistributedKmerHashMap, "SLOT_CAP_MAX", 64)
-    g = kh.SyntheticKmers(51, 300_000, 8, 200, 0, seed=7 + P)
+    monkeypatch.setattr(dist.DistributedKmerHashMap, "SLOT_CAP_MAX", 256)
+    g = kh.SyntheticKmers(51, 60_000, 8, 200, 0, seed=7 + P)
     check_ranks(g, dist.run_threaded(51, g.records(), P, steps=2), P)

@@ -16,7 +16,7 @@ for step in "$@"; do
     tests)
       K=()
       [ -n "$rest" ] && [ "$rest" != "tests" ] && K=(-k "$rest")
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --durations=15 --timeout 600 \
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 300 \
         --timeout-method thread "${K[@]}" > gpurun_out/t_gpu.log 2>&1 ;;
     bench)
       name=${rest%%:*}; args=${rest#*:}
