@@ -133,9 +133,9 @@ bool part_usable(const KParams& p, uint64_t cap, uint64_t n) {
 
 // Region of a partition word in passes 1 and 2: the minimizer region, or the key-hash region when
 // that one is remapped (hot_on: the table has remapped regions; one uniform test per block).
-__device__ __forceinline__ uint32_t part_region(uint32_t win, Key k, const KParams& p, bool hot_on) {
+__device__ __forceinline__ uint32_t part_region(uint32_t win, Key k, const KParams& p, bool hot_on, int js = -1) {
     const uint32_t r = mini_region(win, p);
-    return (hot_on && region_is_hot(p.hot, r)) ? hot_region(k, win, p) : r;
+    return (hot_on && region_is_hot(p.hot, r)) ? hot_region(k, win, p, js) : r;
 }
 
 // ---- record -> word conversion (k other than 51 / 19) ---------------------------------------------
@@ -438,7 +438,8 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const Slice<W>&
     }
     const uint32_t hy = key_hash32(y);
     if (is_splitter(hy, p)) return NO_SUCC;
-    const uint64_t home = MTOP ? home_in(lo, lo + S, hy) : home_of(place_w(mw, y, p), cap, p);
+    // (y holds x's minimizer one window further: j* + 1)
+    const uint64_t home = MTOP ? home_in(lo, lo + S, hy) : home_of(place_w(mw, y, p, (int)j + 1), cap, p);
     if (home < lo || home >= lo + S) return NO_SUCC;
     const uint64_t want0 = W == 1 ? y.lo : y.hi;
 #ifndef KH_LINK_MODE
@@ -517,7 +518,7 @@ __device__ __forceinline__ void chain_heads(const KParams& p, const Slice<W>& lt
             // the walker reads a record at the region of the key it looked up: in a slice reloaded
             // from the table only keys of this region may own one (others may have spilled in)
             const Key hk = slot_key(w0, W == 2 ? lt.w1(i) & LO_MASK : 0ull, p);
-            own = place_w(mini_window(hk, mini_scan(hk, p), p), hk, p).r == r;
+            own = place(hk, p).r == r;
         }
         if (!own) {
             *lt.p0(i) = slot_clean(w0, p);  // no record: the walker steps this k-mer itself
@@ -1234,7 +1235,7 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p_in, const uint64_t* __res
             const Key kk = slot_key(a[j], b[j], p);
             // words of k_part1_convert carry j*; routed words do not
             const uint32_t mn = jstar_in ? slot_jstar(a[j]) : mini_scan(kk, p);
-            bin[j] = part_region(mini_window(kk, mn, p), kk, p, hot_on) >> (p.rbits - B1);
+            bin[j] = part_region(mini_window(kk, mn, p), kk, p, hot_on, (int)(mn & 63u)) >> (p.rbits - B1);
             const bool live = a[j] != EMPTY;
             // splitter k-mers this shard owns (they head migrating-walk segments, kh_mseg.hip)
             if (COLLECT && live && ext_bwd(slot_ext(a[j])) != EXT_F && is_splitter(key_hash32(kk), p)) {
@@ -1395,7 +1396,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
                 if (spl && valid && ext_bwd(ext) != EXT_F && is_splitter(key_hash32(k), p))
                     atomicAdd(&rspl[bin[j]], 1u);
             } else
-                bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on) >> (p.rbits - B1);
+                bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on, (int)(mn & 63u)) >> (p.rbits - B1);
         }
         const uint64_t nt = t + gridDim.x, nbase = nt * TILE;
         if constexpr (ROUTE) {
@@ -1472,8 +1473,11 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p_in, const uint64_t* __res
         uint32_t bin[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
-            bin[j] = part_region(word_mini_window(a[j], b[j], p), slot_key(a[j], b[j], p), p, hot_on) &
-                     ((1u << b2) - 1u);
+        {
+            const Key kk = slot_key(a[j], b[j], p);
+            const int js = p.chain ? (int)slot_jstar(a[j]) : (int)(mini_scan(kk, p) & 63u);
+            bin[j] = part_region(win_bits(kk, js, p), kk, p, hot_on, js) & ((1u << b2) - 1u);
+        }
         sort_reserve_write<W, TB, NB2, TILE>(
             a, b, bin, items, sbin, hist, start, gpos, wsum,
             [&](uint32_t q) { return &rcnt[(bk << b2) | q]; },
@@ -1846,6 +1850,11 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
     if ((e = with_kt<W>(p.K, [&](auto kt) {
              constexpr int KT = decltype(kt)::value;
              hipError_t x;
+             if constexpr (W == 2 && Slice<W>::SPLIT) {  // the sorted-slice variants (pf_launch)
+                 if ((x = allow_lds(k_part_build_pf<W, 4, KT, true, true>, lds)) != hipSuccess) return x;
+                 if ((x = allow_lds(k_part_build_pf<W, 6, KT, true, true>, lds)) != hipSuccess) return x;
+                 if ((x = allow_lds(k_part_build_pf<W, 12, KT, true, true>, lds)) != hipSuccess) return x;
+             }
              if ((x = allow_lds(k_part_build_pf<W, 4, KT, true>, lds)) != hipSuccess) return x;
              if ((x = allow_lds(k_part_build_pf<W, 6, KT, true>, lds)) != hipSuccess) return x;
              if ((x = allow_lds(k_part_build_pf<W, 12, KT, true>, lds)) != hipSuccess) return x;

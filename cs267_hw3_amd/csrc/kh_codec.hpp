@@ -335,36 +335,44 @@ struct Place {
 };
 // Hot regions (a repeat family, a low-complexity run, the C5 hot-bucket set: one minimizer window
 // shared by far more k-mers than a region holds) are remapped as a whole: their keys go to the
-// region of a hash of (the minimizer window, the k-mer's secondary window: the smallest-order
-// window whose content differs from the minimizer's). Consecutive k-mers of a contig keep their
-// secondary window for ~18 steps at K=51, M=16 (it changes when it drops out or a smaller one
-// enters), so runs of a hot family still land in one region and keep their chains, while the
-// family spreads over ~family size / 18 regions (a hash of the whole key spread it too, but broke
-// every run: the C5 hot-bucket walk was one lookup per k-mer). The home inside the region is still
-// home_in(.., key_hash32).
-KH_HD uint32_t second_window(Key k, uint32_t win, const KParams& p) {
-    uint32_t best = 0xFFFFFFFFu, bw = win;
-    for (int j = 0; j <= p.K - p.M; ++j) {
-        const uint32_t w = win_bits(k, j, p);
-        const uint32_t o = (win_order(w) << 6) | (uint32_t)j;
-        if (w != win && o < best) {
-            best = o;
-            bw = w;
-        }
+// region of a hash of (the minimizer window, the k-mer's secondary window: the M bases next to the
+// minimizer's occurrence on the side of window index j* + M when they fit in the k-mer, else on the
+// other side). The secondary window is a fixed stretch of the contig next to the shared one: along
+// a run the occurrence moves up one window index per step and the neighbour with it, so a run keeps
+// it (it changes at most once, where the first side stops fitting and the other starts) and a
+// run still lands in one region and keeps its chain, while the family spreads over one region per
+// distinct neighbour (a hash of the whole key spread it too, but broke every run: the C5
+// hot-bucket walk was one lookup per k-mer). The neighbour never overlaps the shared window: a
+// window overlapping it (the lowest-order other window, say) takes few distinct values over a
+// family and piles it into a few regions again. The home inside the region is home_in(.., key_hash32).
+// js: the occurrence's window index j* (mini_scan's low 6 bits: the first window of the smallest
+// order, so the first with the minimizer's content), or -1 to find it from win
+KH_HD uint32_t second_window(Key k, uint32_t win, const KParams& p, int js = -1) {
+    if (js < 0) {
+        js = 0;
+        for (int j = 0; j <= p.K - p.M; ++j)
+            if (win_bits(k, j, p) == win) {
+                js = j;
+                break;
+            }
     }
-    return bw;
+    const int j2 = js + 2 * p.M <= p.K ? js + p.M : (js >= p.M ? js - p.M : (2 * js < p.K - p.M ? p.K - p.M : 0));
+    return win_bits(k, j2, p);
 }
-KH_HD uint32_t hot_region(Key k, uint32_t win, const KParams& p) {
-    return mix32((win * 0x9E3779B1u) ^ second_window(k, win, p) ^ 0x2545F491u) >> (32 - p.rbits);
+KH_HD uint32_t hot_region(Key k, uint32_t win, const KParams& p, int js = -1) {
+    return mix32((win * 0x9E3779B1u) ^ second_window(k, win, p, js) ^ 0x2545F491u) >> (32 - p.rbits);
 }
 KH_HD bool region_is_hot(const uint32_t* hot, uint32_t r) { return hot && ((hot[r >> 5] >> (r & 31u)) & 1u); }
-KH_HD Place place_w(uint32_t win, Key k, const KParams& p) {
+KH_HD Place place_w(uint32_t win, Key k, const KParams& p, int js = -1) {
     uint32_t r = mini_region(win, p);
     const uint32_t h = key_hash32(k);
-    if (region_is_hot(p.hot, r)) r = hot_region(k, win, p);
+    if (region_is_hot(p.hot, r)) r = hot_region(k, win, p, js);
     return Place{r, h};
 }
-KH_HD Place place(Key k, const KParams& p) { return place_w(mini_window(k, mini_scan(k, p), p), k, p); }
+KH_HD Place place(Key k, const KParams& p) {
+    const uint32_t mn = mini_scan(k, p);
+    return place_w(mini_window(k, mn, p), k, p, (int)(mn & 63u));
+}
 KH_HD uint64_t home_of(Place pl, uint64_t cap, const KParams& p) {
     return home_in(region_lo(pl.r, cap, p), region_lo(pl.r + 1, cap, p), pl.h);
 }
@@ -442,7 +450,9 @@ KH_HD uint32_t word_mini_window(uint64_t w0, uint64_t w1, const KParams& p) {
     return win_bits(k, p.chain ? (int)slot_jstar(w0) : (int)(mini_scan(k, p) & 63u), p);
 }
 KH_HD Place word_place(uint64_t w0, uint64_t w1, const KParams& p) {
-    return place_w(word_mini_window(w0, w1, p), slot_key(w0, w1, p), p);
+    const Key k = slot_key(w0, w1, p);
+    const int js = p.chain ? (int)slot_jstar(w0) : (int)(mini_scan(k, p) & 63u);
+    return place_w(win_bits(k, js, p), k, p, js);
 }
 // Partition words also carry the top bits of their minimizer order in the (then unused)
 // head-index field, so the region build's link test needs no window extraction.

@@ -261,29 +261,43 @@ int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_
     const double expect = (double)n * (double)n / 2.0 / __builtin_powi(4.0, k);
     double expect_hot = 0.0;
     if (v.hot_pm) {
+        // a k-mer of a hot contig spans one period plus K - period bases that may repeat motif
+        // bases: the phase with the most motif bases leaves the fewest free ones (k=51: 20, not
+        // K - M = 35; 12 repeated hot k-mers at 1B before this was counted)
+        int free_min = k;
+        for (uint32_t t = 0; t < v.period; ++t) {
+            int fixed = 0;
+            for (int q = 0; q < k; ++q) fixed += (t + (uint32_t)q) % v.period < v.M;
+            free_min = k - fixed < free_min ? k - fixed : free_min;
+        }
         const double nh = (double)n * v.hot_pm / 1000.0;
-        expect_hot = nh * nh / 2.0 / ((double)v.n_motifs * v.period * __builtin_powi(4.0, k - (int)v.M));
+        expect_hot = nh * nh / 2.0 / ((double)v.n_motifs * v.period * __builtin_powi(4.0, free_min));
     }
     if ((expect > 1e-9 || expect_hot > 1e-6) && n > 1) {
         const uint64_t C = g->len.size();
+        // only hot contigs can repeat a k-mer when the whole set cannot (k=51): check just those
+        const bool hot_only = expect <= 1e-9;
+        std::vector<uint64_t> koff(C + 1, 0);
+        for (uint64_t i = 0; i < C; ++i) koff[i + 1] = koff[i] + ((!hot_only || v.hot_motif(i) >= 0) ? g->len[i] : 0);
+        const uint64_t nk = koff[C];
         std::vector<uint8_t> redo(C, 1);
         for (int round = 0; round < 256; ++round) {
-            std::vector<KeyRef> keys(n);
+            std::vector<KeyRef> keys(nk);
             parallel_for(C, g->threads, [&](uint64_t b, uint64_t e) {
                 for (uint64_t i = b; i < e; ++i)
-                    for (uint64_t t = 0; t < g->len[i]; ++t) {
+                    for (uint64_t t = 0; t < koff[i + 1] - koff[i]; ++t) {
                         kh::Key kk;
                         uint32_t ext;
                         v.kmer(i, t, kk, ext);
-                        keys[g->off[i] + t] = KeyRef{kk.hi, kk.lo, (uint32_t)i};
+                        keys[koff[i] + t] = KeyRef{kk.hi, kk.lo, (uint32_t)i};
                     }
             });
             psort(keys, g->threads);
             std::fill(redo.begin(), redo.end(), 0);
             uint64_t bad = 0;
-            for (uint64_t a = 0; a < n;) {
+            for (uint64_t a = 0; a < nk;) {
                 uint64_t b = a + 1;
-                while (b < n && keys[b].hi == keys[a].hi && keys[b].lo == keys[a].lo) ++b;
+                while (b < nk && keys[b].hi == keys[a].hi && keys[b].lo == keys[a].lo) ++b;
                 if (b - a > 1)
                     for (uint64_t q = a; q < b; ++q) {
                         if (!redo[keys[q].contig]) ++bad;

@@ -124,12 +124,13 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                     fin = true;
                 }
                 // one minimizer scan gives both the owner rank and the placement region
-                const uint32_t mv = fin ? 0u : mini_window(k, mini_scan(k, p), p);
+                const uint32_t mn = fin ? 0u : mini_scan(k, p);
+                const uint32_t mv = fin ? 0u : mini_window(k, mn, p);
                 const uint32_t q = fin ? mw.rank
                                        : (mw.P == 1 ? 0u
                                                     : (p.owner_mode == 1 ? owner_key(k, p, mw.P)
                                                                          : owner_of_mini(mv, mw.P)));
-                const Place pl = place_w(mv, k, p);
+                const Place pl = place_w(mv, k, p, (int)(mn & 63u));
                 if (fin) {
                     // finished below (length record, no message)
                 } else if (q != mw.rank || nwords >= MW_RUN_WORDS) {

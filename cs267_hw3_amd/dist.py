@@ -781,7 +781,12 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
     `info` (a dict) receives the round count, per-rank table stats and, per rank, the blocking
     host reads of the last step (insert_all + assemble: this host's and the library's).
     steps > 1 repeats clear + insert + assemble on the same records (buffers sized by step 1)."""
+    import gc
     import numpy as np
+    # the shards allocate through hipMalloc, not torch's caching allocator: blocks torch still
+    # caches from earlier runs in this process are returned to the device first
+    gc.collect()
+    torch.cuda.empty_cache()
     comms = ThreadComm.group(nranks)
     gen = recs if hasattr(recs, "records_dev") else None
     n = gen.n if gen is not None else recs.shape[0]
