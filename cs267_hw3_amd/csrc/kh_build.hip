@@ -35,15 +35,19 @@
 namespace kh {
 
 static constexpr int PB = 256;                    // threads per block of the small kernels
-static constexpr int B1 = 9, B2 = 8;              // radix bits per pass (pass 2: up to B2, p.rbits - B1)
+#ifndef KH_B1
+#define KH_B1 9
+#endif
+static constexpr int B1 = KH_B1, B2 = REGION_BITS_MAX - KH_B1;  // radix bits per pass (pass 2: p.rbits - B1)
 static constexpr int NB1 = 1 << B1, NB2 = 1 << B2;
+static constexpr int NBX = NB1 > NB2 ? NB1 : NB2;  // bins of the larger pass (LDS layout)
 static constexpr uint32_t NREG_MAX = 1u << (B1 + B2);
-static_assert(B1 == REGION_BITS_MIN && B1 + B2 == REGION_BITS_MAX, "regions of the placement hash");
+static_assert(B1 <= REGION_BITS_MIN && B1 + B2 == REGION_BITS_MAX && NBX <= 512, "regions of the placement hash");
 static constexpr int BUILD_THREADS = 512;
 static constexpr int T1 = 2;                      // consecutive tiles per pass-1 block
 static constexpr uint32_t S1 = 8;                 // pass-1 windows (atomic counters) per bucket
 static constexpr uint32_t NW1 = NB1 * S1;
-static_assert(NW1 == PART_W1_COUNTERS, "counter layout");
+static_assert(NW1 <= PART_W1_COUNTERS, "counter layout");
 // splitter buffer of k_win1 in the dynamic-LDS tail: (4 KB - 2 KB gpos - wsum - counter) / 16 B
 static constexpr uint32_t WIN_SPLIT_LCAP = 120;
 static_assert(PART_TILE * 18 + 3 * 512 * 4 + 8 + WIN_SPLIT_LCAP * 16 + 8 <= PART_TILE * 16 + PART_TILE * 2 + 512 * 16,
@@ -52,7 +56,7 @@ static constexpr uint64_t LDS_BYTES = 160 * 1024;
 // the windowed passes (k_win1 / k_win2) sort tiles of WIN_TILE words: 8192 doubles the runs each
 // bin gets per tile (C3 pass 1: 16 words = 256 B instead of 128 B) in 152 KiB of LDS
 static constexpr int WIN_TILE = 8192;
-constexpr size_t sort_lds(int tile) { return (size_t)tile * 16 + tile * 2 + 2 * NB1 * 4 + NB1 * 8; }
+constexpr size_t sort_lds(int tile) { return (size_t)tile * 16 + tile * 2 + 2 * NBX * 4 + NBX * 8; }
 constexpr size_t sort_lds_nb(int tile, int nb) { return (size_t)tile * 16 + tile * 2 + 2 * nb * 4 + nb * 8; }
 static_assert(sort_lds(WIN_TILE) + 64 <= 160 * 1024, "k_win LDS");
 static constexpr int REC_TILE = 3584;  // records pass 1 (k_win1_rec): two blocks per CU
@@ -639,9 +643,10 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
     }
 }
 
-// ---- sorted slice insert (balanced tables, load > 0.6) ----------------------------------------
-// At high load linear probing in the slice is the build's cost: an insert probes ~(1 + 1/(1-a)^2)/2
-// slots (23 at a = 0.85) and a wave waits for its lanes' longest run. Instead the slice is laid out
+// ---- sorted slice insert (fresh 16-B slices) -----------------------------------------------------
+// Linear probing in the slice costs random LDS CAS (bank conflicts) and, at high load, long probe
+// runs: ~(1 + 1/(1-a)^2)/2 slots per insert (23 at a = 0.85), and a wave waits for its lanes'
+// longest run. Instead the slice is laid out
 // as sequential linear probing in home order would leave it: with c(h) keys of home h,
 // C(h) = c(0) + .. + c(h) and M(h) = max over h' <= h of (h' - C(h' - 1)), the keys of home h take
 // slots C(h - 1) + M(h) + 0, 1, .. (E(h) = C(h) + M(h) is the first free slot after them), so an
@@ -957,9 +962,10 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
     const uint32_t smax = (uint32_t)region_max_slots(p, t.cap);
     const uint32_t hcap = B.headrec ? B.hcap : 0u;
     const int prof = debug_flag("build_prof") ? 1 : 0;
-    // balanced (high-load) tables: sorted slice insert instead of probing (KH_DEBUG=probe_build: off)
-    // (word 1 array of the split layout holds the home counts: 16-B slots only)
-    const bool sorted = p.rb != nullptr && W == 2 && Slice<W>::SPLIT && !debug_flag("probe_build");
+    // fresh slices: sorted slice insert instead of LDS CAS probing (KH_DEBUG=probe_build: off); the
+    // word-1 array of the split layout holds the home counts, so 16-B slots only. C3 build at load
+    // 0.5: 3.63 -> 2.96 ms; at 0.85 (balanced bounds): 12.5 -> 5.0 ms
+    const bool sorted = W == 2 && Slice<W>::SPLIT && !debug_flag("probe_build");
     if (prof) {
         static const unsigned long long zero[8] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_build_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, s);
@@ -1099,6 +1105,9 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
 #ifndef KH_SORT_SPLIT
 #define KH_SORT_SPLIT 1
 #endif
+#ifndef KH_DIRECT_SCATTER
+#define KH_DIRECT_SCATTER 0
+#endif
 // Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
 // with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
 // out[window(bin) + reserved + rank] (positions past cap -> overflow list).
@@ -1111,6 +1120,68 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
                                                    unsigned long long* ctr, unsigned long long* stats, NextF next) {
     constexpr int IPT = TILE / TB;
     static_assert(NB <= TB, "one bin per thread");
+    if constexpr (KH_DIRECT_SCATTER != 0 && !WRANK) {
+        // no LDS staging: every lane stores its word at its run position (L2 merges a run's
+        // stores; runs of one window come from blocks of one XCD)
+        __shared__ uint32_t spill_d;
+        if (threadIdx.x < NB) hist[threadIdx.x] = 0;
+        if (threadIdx.x == 0) spill_d = 0;
+        lds_barrier();
+        uint32_t rank[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
+        lds_barrier();
+        const uint32_t hv = threadIdx.x < NB ? hist[threadIdx.x] : 0u;
+        if (threadIdx.x < NB) {
+            const uint32_t g = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
+            gpos[threadIdx.x] = g;
+            if (hv && g + hv > cap) spill_d = 1;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            if (a[j] == EMPTY) continue;
+            const uint32_t w = gpos[bin[j]] + rank[j];
+            if (w < cap) {
+                const uint64_t g = window(bin[j]) + w;
+                if (W == 2)
+                    *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(a[j], b[j]);
+                else
+                    out[g] = a[j];
+            }
+        }
+        if (spill_d) {  // as below: one overflow-list reservation per tile
+            __shared__ uint32_t keepd[NB];
+            __shared__ unsigned long long sbased;
+            uint32_t sp = 0;
+            if (threadIdx.x < NB) {
+                const uint32_t g = gpos[threadIdx.x];
+                const uint32_t keep = g >= cap ? 0u : min(hv, cap - g);
+                keepd[threadIdx.x] = keep;
+                sp = hv - keep;
+            }
+            uint32_t stot;
+            const uint32_t so = block_scan_u32<TB>(sp, stot, wsum);
+            if (threadIdx.x < NB) start[threadIdx.x] = so;
+            if (threadIdx.x == 0) sbased = atomicAdd(&ctr[CT_OVF], (unsigned long long)stot);
+            lds_barrier();
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                if (a[j] == EMPTY || rank[j] < keepd[bin[j]]) continue;
+                const uint64_t d = sbased + start[bin[j]] + (rank[j] - keepd[bin[j]]);
+                if (d < ovf_cap) {
+                    ovf[d * W] = a[j];
+                    if (W == 2) ovf[d * W + 1] = b[j];
+                } else {
+                    atomicAdd(&stats[ST_FULL], 1ull);
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        next();
+        lds_barrier();  // hist / gpos / start are rewritten by the next tile
+        return;
+    }
     __shared__ uint32_t spill;  // some bin's run passes its window's end (block-uniform after the barrier)
     if (threadIdx.x < NB) hist[threadIdx.x] = 0;
     if (threadIdx.x == 0) spill = 0;
@@ -1211,13 +1282,13 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p_in, const uint64_t* __res
     uint64_t* items = smem;
     uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + TILE * 2);
     uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + TILE);
-    uint32_t* start = hist + NB1;
-    uint32_t* gpos = start + NB1;
+    uint32_t* start = hist + NBX;
+    uint32_t* gpos = start + NBX;
     // block-scan partials in static LDS: 80 KB + a few bytes keeps these kernels at one block
     // (8 waves) per CU, measured faster than two (C3: pass 1 1.79-1.89 vs 1.98 ms, pass 2
     // 1.61-1.67 vs 1.69); the splitter buffer (COLLECT) uses the dynamic region's unused tail
     __shared__ uint32_t wsum[TB / 64];
-    uint32_t* scount = gpos + NB1;
+    uint32_t* scount = gpos + NBX;
     uint64_t* sbuf = reinterpret_cast<uint64_t*>(scount + 2);
     const uint32_t sub = blockIdx.x % S1;
     const uint64_t b0 = (uint64_t)blockIdx.x * T1 * TILE;
@@ -1453,8 +1524,8 @@ __global__ __launch_bounds__(TB) void k_win2(KParams p_in, const uint64_t* __res
     uint64_t* items = smem;
     uint16_t* sbin = reinterpret_cast<uint16_t*>(smem + TILE * 2);
     uint32_t* hist = reinterpret_cast<uint32_t*>(sbin + TILE);
-    uint32_t* start = hist + NB1;
-    uint32_t* gpos = start + NB1;
+    uint32_t* start = hist + NBX;
+    uint32_t* gpos = start + NBX;
     __shared__ uint32_t wsum[TB / 64];  // static: one block per CU (see k_win1)
     const uint32_t bk = blockIdx.x / (uint32_t)G, g = blockIdx.x % (uint32_t)G;
     const uint32_t b2 = (uint32_t)(p.rbits - B1);  // pass-2 bits: regions per bucket = 2^b2
