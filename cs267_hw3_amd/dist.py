@@ -430,15 +430,16 @@ class DistributedKmerHashMap:
         learns every rank's total and largest split (chunk count), and `extra` (a device int64
         scalar of this rank, e.g. its splitter count) of every rank."""
         P = self.P
+        if P == 1 and not self.SELF_EXCHANGE:
+            # one rank: the exchange is the identity; read the counts (and extra) as they are
+            h = self._host(counts[:2] if extra is None else torch.cat([counts[:2], extra.reshape(1)])).tolist()
+            return [h[0]], [h[0]], [h[1]], h[0], [h[2] if extra is not None else 0]
         mx = counts[:P].max().reshape(1)
         ex = extra.reshape(1) if extra is not None else mx.new_zeros(1)
         send = torch.stack([counts[:P], counts[P:P + 1].expand(P), mx.expand(P), ex.expand(P)], 1)
         send = send.contiguous().view(-1)
-        if P == 1 and not self.SELF_EXCHANGE:
-            recv = send  # one rank: the exchange is the identity (no collective launch)
-        else:
-            recv = torch.empty_like(send)
-            self.comm.all_to_all(recv, send, [4] * P, [4] * P)
+        recv = torch.empty_like(send)
+        self.comm.all_to_all(recv, send, [4] * P, [4] * P)
         host = self._host(torch.cat([send, recv])).view(2, P, 4)
         send_splits = host[0, :, 0].tolist()
         recv_splits = host[1, :, 0].tolist()
@@ -688,15 +689,19 @@ class DistributedKmerHashMap:
             self.rounds += 1
             if self.rounds >= check_at or self.rounds * 2 + 2 > live.numel():
                 # global max of every round's [in flight, largest per-destination] so far + errors
-                err = torch.tensor([1 if self._err is not None else 0], dtype=torch.int64, device=dev)
-                h = self.comm.max_to_host(torch.cat([live[:2 * self.rounds], err]))
+                if local:  # one rank: no reduction, the error is this rank's own
+                    h = self._host(live[:2 * self.rounds]).tolist() + [1 if self._err is not None else 0]
+                    self.syncs -= 1  # counted below
+                else:
+                    err = torch.tensor([1 if self._err is not None else 0], dtype=torch.int64, device=dev)
+                    h = self.comm.max_to_host(torch.cat([live[:2 * self.rounds], err]))
                 self.checks += 1
                 self.syncs += 1
                 if int(h[-1]):
                     if self._err is not None:
                         raise self._err
                     raise _lib.KmerHashError(_lib.KH_ERR_FULL, "another rank failed to size its shard")
-                maxes = h[1:2 * self.rounds:2].tolist()
+                maxes = [int(x) for x in h[1:2 * self.rounds:2]]
                 if int(h[2 * self.rounds - 2]) == 0:
                     break
                 if self.rounds * 2 + 2 > live.numel():
@@ -736,8 +741,12 @@ class DistributedKmerHashMap:
         local = P == 1 and not self.SELF_EXCHANGE  # one rank: every exchange is the identity
         lout = self._grow("_ms_links", max(nseg, 1) * L, torch.int64, dev)
         counts = sh.mw_link(trecv, r, lout)
-        nsp = torch.tensor([self._nsp], dtype=torch.int64, device=dev)
-        send_splits, recv_splits, _, gmax, nsps = self._exchange_counts(counts, nsp)
+        if local:
+            send_splits, recv_splits, _, gmax, _ = self._exchange_counts(counts)
+            nsps = [self._nsp]
+        else:
+            nsp = torch.tensor([self._nsp], dtype=torch.int64, device=dev)
+            send_splits, recv_splits, _, gmax, nsps = self._exchange_counts(counts, nsp)
         m = sum(recv_splits)
         if local:
             lin = lout
