@@ -66,7 +66,7 @@ typedef struct kh_stats {
     uint64_t n_bad_base;     /* kh_pack_text_dev lines with a k-mer base outside {A,C,G,T} */
     double ms_build;         /* device ms, region build + overflow inserts of the last partitioned insert */
     double ms_walk_kernel;   /* device ms, k_walk_q alone, last assemble */
-    uint64_t n_hot_regions;  /* placement regions remapped by key hash (shared minimizers overfilled them) */
+    uint64_t n_hot_regions;  /* placement regions remapped (shared minimizers overfilled them): keys by (minimizer, neighbour window) */
     uint64_t n_overflow;     /* keys of the last partitioned build inserted by global CAS (full windows,
                                 probe runs that left their region slice) */
 } kh_stats;
