@@ -317,6 +317,9 @@ __device__ __forceinline__ int lds_insert(const KParams& p, const Slice<W>& lt, 
 #ifndef KH_LDS_BLOCK
 #define KH_LDS_BLOCK 1
 #endif
+#ifndef KH_FUSE_INIT
+#define KH_FUSE_INIT 1
+#endif
 template <int W>
 __device__ __forceinline__ int lds_insert_blk(const KParams& p, const Slice<W>& lt, uint32_t S, uint32_t loc,
                                               uint64_t w0, uint64_t w1, unsigned long long* stats) {
@@ -751,6 +754,11 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
     uint32_t m_cur = fill(r);
     load(r, m_cur, a, b);
     const uint32_t NR = nreg(p);
+    if (SORT && KH_FUSE_INIT)  // the whole LDS slice reset once (see the sorted insert below)
+        for (uint32_t i = threadIdx.x; i < smax; i += BUILD_THREADS) {
+            *lt.p0(i) = EMPTY;
+            *lt.p1(i) = 0ull;
+        }
     for (; r < NR; r += gridDim.x) {
         const uint64_t lo = rbt[r], hi = rbt[r + 1];
         const uint32_t S = (uint32_t)(hi - lo);
@@ -762,11 +770,17 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         int pos[IPT];  // LDS slot of each word inserted here (chains walk from these)
         if constexpr (SORT) {
             static_assert(FRESH && Slice<W>::SPLIT, "the sorted slice needs a fresh table and the split layout");
-            // sorted slice (FRESH only): word 0 EMPTY, the word-1 array holds the home counts
+            // sorted slice (FRESH only): word 0 EMPTY, the word-1 array holds the home counts. With
+            // KH_FUSE_INIT every slot of the LDS slice is already reset (word 0 EMPTY, word 1 zero:
+            // zero home counts): before the first region, then by each write-out for the slots it
+            // reads; slots past a region's S are never written. The write-out then needs no
+            // barrier of its own: this one orders it before the next region's count atomics.
             uint32_t* hist = reinterpret_cast<uint32_t*>(lt.p1(0));
-            for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                *lt.p0(i) = EMPTY;
-                hist[i] = 0;
+            if (!KH_FUSE_INIT) {
+                for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
+                    *lt.p0(i) = EMPTY;
+                    hist[i] = 0;
+                }
             }
             lds_barrier();
             BPROF(0);
@@ -897,7 +911,11 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         if (W == 2) {
             // two slots per step: both LDS reads are in flight before either store
             ulonglong2* dst = reinterpret_cast<ulonglong2*>(slots + lo * 2);
-            for (uint32_t i = threadIdx.x; i < S; i += 2 * BUILD_THREADS) {
+            for (uint32_t i0 = threadIdx.x; i0 < S; i0 += 2 * BUILD_THREADS) {
+                // opaque to the optimiser: no per-thread 64-bit store base hoisted out of the region
+                // loop (it was spilled, and its reload waited for every load in flight: vmcnt(0))
+                uint32_t i = i0;
+                asm volatile("" : "+v"(i));
                 const uint32_t i2 = i + BUILD_THREADS;
                 const bool two = i2 < S;
                 uint64_t x, y, x2, y2;
@@ -909,6 +927,14 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 }
                 if (hcap && x != EMPTY) clean_out<W>(x, y, p);
                 if (hcap && x2 != EMPTY) clean_out<W>(x2, y2, p);
+                if (SORT && KH_FUSE_INIT) {  // this thread's slots, read above: reset for the next region
+                    *lt.p0(i) = EMPTY;
+                    *lt.p1(i) = 0ull;
+                    if (two) {
+                        *lt.p0(i2) = EMPTY;
+                        *lt.p1(i2) = 0ull;
+                    }
+                }
                 dst[i] = make_ulonglong2(x, y);
                 if (two) dst[i2] = make_ulonglong2(x2, y2);
             }
@@ -919,7 +945,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 slots[lo + i] = v;
             }
         }
-        lds_barrier();
+        if (!(SORT && KH_FUSE_INIT)) lds_barrier();  // fused: the next region's first barrier orders it
         BPROF(5);
         m_cur = m_next;
     }
