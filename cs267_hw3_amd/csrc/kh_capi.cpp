@@ -139,6 +139,8 @@ struct kh_table {
     uint64_t starts_cap = 0;                 // start entries the starts buffer holds
     uint64_t splits_cap = 0, splits_w_cap = 0;
     bool split_ok = true;                    // every inserted k-mer was checked for splitters
+    bool starts_explicit = false;            // kh_set_starts: walks may overlap (text not bounded)
+    bool text_sync = false;                  // the next assemble sizes the text from the scanned total
     uint64_t chunk_cap = 0;
 
     uint64_t n_inserted = 0;                 // host-side count (what was submitted)
@@ -459,6 +461,7 @@ int kh_clear(kh_table* t) {
     t->n_inserted = 0;
     t->assembled = false;
     t->split_ok = true;
+    t->starts_explicit = false;
     t->staging = false;
     t->stage_n = 0;
     t->collected_n = 0;
@@ -689,6 +692,7 @@ int kh_set_starts(kh_table* t, const uint8_t* recs, uint64_t n) {
     KH_SYNC(t);
     t->assembled = false;
     t->split_ok = false;  // caller's starts may share segments (e.g. two starts on one contig)
+    t->starts_explicit = true;
     return KH_OK;
 }
 
@@ -796,10 +800,20 @@ int kh_assemble_dev(kh_table* t) {
     }
     unsigned long long* ctr = t->ctr.as<unsigned long long>();
     unsigned long long* stats = t->stats.as<unsigned long long>();
-    // Walk, then the offsets scan; the text is sized from the scanned total (walks that overlap,
-    // e.g. two explicit starts on one contig, make it longer than the k-mer count). The chunk
-    // pool is an upper bound for disjoint walks; if overlapping walks exhaust it the walk is
-    // redone once with the pool the first attempt asked for.
+    // Walks from the table's own start k-mers are disjoint: the text is at most K + 1 bytes per
+    // contig plus one per k-mer, and the chunk pool holds them, so the text is sized before the
+    // walk and nothing is read back between walk and text (one host round trip less per assemble;
+    // a total past the bound, only possible on malformed input, is not written and kh_assemble
+    // redoes the walk the slow way). Otherwise (explicit starts: walks that overlap, e.g. two
+    // starts on one contig, make the text longer than the k-mer count) the text is sized from the
+    // scanned total, and if overlapping walks exhaust the chunk pool the walk is redone once with
+    // the pool the first attempt asked for.
+    const bool bounded = !t->starts_explicit && !t->text_sync && !kh::debug_flag("text_sync");
+    t->text_sync = false;
+    if (bounded) {
+        if ((rc = t->text.ensure(ns * (uint64_t)(t->kp.K + 1) + n + 64))) return rc;
+        wb.text_cap = t->text.bytes;
+    }
     for (int attempt = 0;; ++attempt) {
         KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
         KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
@@ -838,6 +852,7 @@ int kh_assemble_dev(kh_table* t) {
         else
             KH_HIP(kh::launch_materialize(kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
                                           nullptr, ctr, t->stream, kh::MAT_SCAN));
+        if (bounded) break;
         unsigned long long hv[2], ovf = 0;
         KH_HIP(hipMemcpyAsync(hv, ctr + kh::CT_CHUNK_NEXT, sizeof hv, hipMemcpyDeviceToHost, t->stream));
         KH_HIP(hipMemcpyAsync(&ovf, stats + kh::ST_CHUNK_OVF, 8, hipMemcpyDeviceToHost, t->stream));
@@ -877,6 +892,12 @@ int kh_assemble(kh_table* t, uint64_t* n_contigs, uint64_t* out_bytes) {
     if (int rc = check_stats(t)) return rc;  // one wait (ordered after the queued work)
     uint64_t ob = 0;
     if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
+    if (t->last_contigs && ob > t->text.bytes) {  // past the bound (malformed input): sized walk
+        t->text_sync = true;
+        if (int rc = kh_assemble_dev(t)) return rc;
+        if (int rc = check_stats(t)) return rc;
+        if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
+    }
     if (n_contigs) *n_contigs = t->last_contigs;
     if (out_bytes) *out_bytes = ob;
     return KH_OK;
@@ -887,6 +908,10 @@ int kh_contigs_text_dev(kh_table* t, const char** dev_text, uint64_t* bytes) {
     if (!t->assembled) return fail(KH_ERR_STATE, "no assemble since the last insert/clear");
     uint64_t ob = 0;
     if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
+    if (t->last_contigs && ob > t->text.bytes)
+        return fail(KH_ERR_STATE, "contig text of %llu bytes passed its %llu-byte bound (malformed input?): "
+                                  "kh_assemble redoes the walk sized", (unsigned long long)ob,
+                    (unsigned long long)t->text.bytes);
     *dev_text = t->text.as<const char>();
     *bytes = t->last_contigs ? ob : 0;
     return KH_OK;

@@ -664,7 +664,7 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_write_heads(KParams p, const uint64_t* starts, uint64_t nc,
                                                        const uint32_t* len, const uint64_t* off,
-                                                       char* out) {
+                                                       char* out, uint64_t cap) {
     // 16 lanes per contig: lane l owns the aligned dword at (o & ~3) + 4l of the contig's K head
     // characters (o = its text offset), so a store instruction writes four contigs' heads as
     // contiguous runs; the first and last dword of a head are shared with the neighbouring text
@@ -678,6 +678,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_heads(KParams p, const uint64_t
         const uint64_t w1 = (W == 2) ? starts[c * W + 1] : 0;
         const Key k = slot_key(w0, w1, p);
         const uint64_t o = off[c];
+        if (o + (uint64_t)p.K + len[c] > cap) continue;  // past the buffer: not written
         const uint32_t a = (uint32_t)(o & 3u);
         const int c0 = (int)(4 * l) - (int)a;  // first character of this lane's dword
         if (c0 < p.K) {
@@ -705,7 +706,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* c
                                                         const unsigned long long* ctr,
                                                         uint64_t chunk_cap, uint64_t n_first,
                                                         const uint32_t* len,
-                                                        const uint64_t* off, char* out) {
+                                                        const uint64_t* off, char* out, uint64_t cap) {
     // Chunks [0, n_first) are the contigs' own first chunks; the extra-chunk count is only known
     // on the device (walker allocation head), so the grid is sized for the capacity and bounded
     // here.
@@ -720,6 +721,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* c
         const uint64_t app = (uint64_t)len[c] - 1;
         if (j0 >= app) continue;
         const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
+        if (off[c] + K + j0 + cntb > cap) continue;
         const uint64_t word = chunk_data[t];
         char* o = out + off[c] + K + j0;
         store_chars(o, cntb, [&](uint32_t i) { return codes4_chars((uint32_t)(word >> (8 * i)) & 0xFFu); });
@@ -800,13 +802,13 @@ hipError_t launch_contig_offsets(int K, const uint32_t* len, uint64_t nc, uint64
 }
 
 hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t nc, const uint32_t* len,
-                              const uint64_t* offsets, char* out, hipStream_t s) {
+                              const uint64_t* offsets, char* out, hipStream_t s, uint64_t cap) {
     if (nc == 0) return hipSuccess;
     const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
     if (p.W == 1)
-        k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, starts, nc, len, offsets, out);
+        k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, starts, nc, len, offsets, out, cap);
     else
-        k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, starts, nc, len, offsets, out);
+        k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, starts, nc, len, offsets, out, cap);
     return hipGetLastError();
 }
 
@@ -821,15 +823,16 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
         if (e != hipSuccess) return e;
     }
     if (!(phases & MAT_WRITE)) return hipSuccess;
+    const uint64_t cap = wb.text_cap ? wb.text_cap : ~0ull;
     const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
     if (p.W == 1)
-        k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out);
+        k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
     else
-        k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out);
+        k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
     const unsigned gc =
         (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr,
-                                        wb.chunk_cap, nc, wb.contig_len, offsets, out);
+                                        wb.chunk_cap, nc, wb.contig_len, offsets, out, cap);
     return hipGetLastError();
 }
 
@@ -1036,7 +1039,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
                                                             const unsigned long long* nsp_dev, uint64_t nsp,
                                                             const uint32_t* seg_len, const uint32_t* seg_contig,
                                                             const uint32_t* seg_off, const uint64_t* off,
-                                                            char* out) {
+                                                            char* out, uint64_t cap) {
     const uint64_t nseg = n_starts + (nsp_dev ? (uint64_t)*nsp_dev : nsp);
     const uint64_t nchunks = min(nseg + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
     const uint64_t nt = nchunks * WC_TPC;
@@ -1050,6 +1053,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
         const uint64_t app = (uint64_t)seg_len[g] - 1;
         if (cb + 32 * q >= app) continue;
         const uint32_t cnt = (uint32_t)min<uint64_t>(CHUNK_BASES, app - cb);
+        if (off[c] + K + seg_off[g] + cb + cnt > cap) continue;  // past the buffer: not written
         char* o = out + off[c] + K + seg_off[g] + cb;
         for (uint32_t w = q; 32 * w < cnt; w += WC_TPC) {
             const uint64_t word = chunk_data[ch * CHUNK_WORDS + w];
@@ -1071,11 +1075,12 @@ hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const
         if (e != hipSuccess) return e;
     }
     if (!(phases & MAT_WRITE)) return hipSuccess;
-    if ((e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s)) != hipSuccess) return e;
+    const uint64_t cap = wb.text_cap ? wb.text_cap : ~0ull;
+    if ((e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s, cap)) != hipSuccess) return e;
     const unsigned gc = (unsigned)hmin((wb.chunk_cap * WC_TPC + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks_seg<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr, wb.chunk_cap,
                                             nc, wb.n_splits_dev, wb.n_splits, wb.contig_len, sb.seg_contig,
-                                            sb.seg_off, offsets, out);
+                                            sb.seg_off, offsets, out, cap);
     return hipGetLastError();
 }
 

@@ -91,6 +91,9 @@ struct WalkBuffers {
     // per walker (start, then walked splitter): its own head record's global index + 1, 0 = look
     // the k-mer up (k_start_rec; null = every walker looks its k-mer up)
     uint32_t* start_rec = nullptr;
+    // bytes of the text buffer the materialisation writes into (0: sized from the scanned total);
+    // a contig that would pass it is not written (the caller compares the total with it)
+    uint64_t text_cap = 0;
 };
 
 // Persistent per-lane walker (single GPU): every lane walks whole contigs, pulling start k-mers
@@ -269,8 +272,9 @@ hipError_t launch_pack_text(const KParams& p, const char* text, uint64_t n, uint
 // (with the trailing '\n' at off + K + len - 1).
 hipError_t launch_contig_offsets(int K, const uint32_t* len, uint64_t nc, uint64_t* offsets,
                                  uint64_t* scratch, unsigned long long* total, hipStream_t s);
+// cap: bytes of `out` (contigs past it are skipped; default: unbounded)
 hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t nc, const uint32_t* len,
-                              const uint64_t* offsets, char* out, hipStream_t s);
+                              const uint64_t* offsets, char* out, hipStream_t s, uint64_t cap = ~0ull);
 
 // Scratch words needed by the scans for m elements.
 uint64_t scan_scratch_words(uint64_t m);
