@@ -320,6 +320,9 @@ __device__ __forceinline__ int lds_insert(const KParams& p, const Slice<W>& lt, 
 #ifndef KH_FUSE_INIT
 #define KH_FUSE_INIT 1
 #endif
+#ifndef KH_LINK_STORE
+#define KH_LINK_STORE 0
+#endif
 template <int W>
 __device__ __forceinline__ int lds_insert_blk(const KParams& p, const Slice<W>& lt, uint32_t S, uint32_t loc,
                                               uint64_t w0, uint64_t w1, unsigned long long* stats) {
@@ -455,15 +458,31 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const Slice<W>&
     // block steps (see lds_insert_blk): ~d/4 steps for a run of d slots (KH_LINK_MODE: 0 slot
     // steps, 1 block steps, 2 block steps in dense slices)
     if (KH_LDS_BLOCK && MTOP && (KH_LINK_MODE == 1 || (KH_LINK_MODE == 2 && dense))) {
+#ifndef KH_LINK_BLK
+#define KH_LINK_BLK 4
+#endif
+#ifndef KH_LINK_B128
+#define KH_LINK_B128 0
+#endif
+        constexpr int BLK = KH_LINK_BLK;  // slots per step (word 0 of each)
         for (uint32_t t = (uint32_t)(home - lo); t < S;) {
-            const uint32_t base = t & ~3u;
-            uint64_t v[4];
+            const uint32_t base = t & ~(uint32_t)(BLK - 1);
+            uint64_t v[BLK];
+            if constexpr (KH_LINK_B128 && Slice<W>::SPLIT && BLK % 2 == 0) {  // 16-B LDS reads
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = lt.w0(base + q);
+                for (int q = 0; q < BLK; q += 2) {
+                    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(lt.p0(base + q));
+                    v[q] = x.x;
+                    v[q + 1] = x.y;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < BLK; ++q) v[q] = lt.w0(base + q);
+            }
             int hit = -1;
             bool key = false;
 #pragma unroll
-            for (int q = 3; q >= 0; --q) {
+            for (int q = BLK - 1; q >= 0; --q) {
                 const uint32_t i = base + q;
                 const bool e = v[q] == EMPTY, m = !e && slot_keybits(v[q], p) == want0;
                 if (i >= t && i < S && (e || m)) {
@@ -472,7 +491,7 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const Slice<W>&
                 }
             }
             if (hit < 0) {
-                t = base + 4;
+                t = base + BLK;
                 continue;
             }
             const uint32_t i = base + (uint32_t)hit;
@@ -887,7 +906,17 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
 #pragma unroll
             for (int j = 0; j < IPT; ++j)
                 if (pos[j] >= 0)
-                    put_link<W>(lt, (uint32_t)pos[j], chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j], dense), p);
+                {
+                    const uint32_t nx = chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j], dense);
+                    if (KH_LINK_STORE && W == 2 && nx != NO_SUCC) {
+                        // only this key's thread writes its word 0 in this phase (predecessor bits go
+                        // to word 1 at W=2): a plain store of the word it inserted, with the link
+                        *lt.p0((uint32_t)pos[j]) = slot_clean(a[j], p) | ((unsigned long long)(nx + 1) << p.idx_lo);
+                        atomicOr(pred_word<W>(lt, nx), PRED);
+                    } else {
+                        put_link<W>(lt, (uint32_t)pos[j], nx, p);
+                    }
+                }
             load(r + gridDim.x, m_next, a, b);
             lds_barrier();
             BPROF(2);
