@@ -320,8 +320,8 @@ __device__ __forceinline__ int lds_insert(const KParams& p, const Slice<W>& lt, 
 #ifndef KH_FUSE_INIT
 #define KH_FUSE_INIT 1
 #endif
-#ifndef KH_LINK_STORE
-#define KH_LINK_STORE 0
+#ifndef KH_HEAD_REG
+#define KH_HEAD_REG 1
 #endif
 template <int W>
 __device__ __forceinline__ int lds_insert_blk(const KParams& p, const Slice<W>& lt, uint32_t S, uint32_t loc,
@@ -915,31 +915,30 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         } else if (hcap) {
             // fresh slice: its keys are exactly this thread's words, so links are computed from
             // registers (no pass over empty slots) and every key knows its slot
+            // (pos[j] | HAS_SUCC: the key was linked, so a head needs only its predecessor bit read)
+            constexpr int HAS_SUCC = 1 << 30;
 #pragma unroll
             for (int j = 0; j < IPT; ++j)
-                if (pos[j] >= 0)
-                {
+                if (pos[j] >= 0) {
                     const uint32_t nx = chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j], dense);
-                    if (KH_LINK_STORE && W == 2 && nx != NO_SUCC) {
-                        // only this key's thread writes its word 0 in this phase (predecessor bits go
-                        // to word 1 at W=2): a plain store of the word it inserted, with the link
-                        *lt.p0((uint32_t)pos[j]) = slot_clean(a[j], p) | ((unsigned long long)(nx + 1) << p.idx_lo);
-                        atomicOr(pred_word<W>(lt, nx), PRED);
-                    } else {
-                        put_link<W>(lt, (uint32_t)pos[j], nx, p);
-                    }
+                    put_link<W>(lt, (uint32_t)pos[j], nx, p);
+                    if (KH_HEAD_REG && nx != NO_SUCC) pos[j] |= HAS_SUCC;
                 }
             load(r + gridDim.x, m_next, a, b);
             lds_barrier();
             BPROF(2);
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
-                if (pos[j] < 0 || !is_head<W>(lt, (uint32_t)pos[j], p)) continue;
+                if (pos[j] < 0) continue;
+                const uint32_t sl = (uint32_t)pos[j] & 0xFFFFu;
+                if (KH_HEAD_REG ? (!(pos[j] & HAS_SUCC) || (*pred_word<W>(lt, sl) & PRED))
+                                : !is_head<W>(lt, sl, p))
+                    continue;
                 const uint32_t id = atomicAdd(&hcnt, 1u);
                 if (id < hcap)
-                    hlist[id] = (uint16_t)pos[j];
+                    hlist[id] = (uint16_t)sl;
                 else
-                    *lt.p0((uint32_t)pos[j]) = slot_clean(lt.w0((uint32_t)pos[j]), p);  // no record room: no index
+                    *lt.p0(sl) = slot_clean(lt.w0(sl), p);  // no record room: no index
             }
             lds_barrier();
             BPROF(3);
