@@ -840,7 +840,8 @@ int kh_assemble_dev(kh_table* t) {
             KH_HIP(kh::launch_rec_succ(kp, view(t), t->headrec.as<uint64_t>(), wb.hcap, rs, blocks));
             if (succ_side) KH_HIP(hipEventRecord(t->ev_conv, t->side));
         }
-        KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, 0, t->stream));
+        // three walker blocks per CU for 16-B slots at load <= 0.6, else two (kh_kernels.hip)
+        KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, (kp.W == 2 && t->load <= 0.6) ? -3 : -2, t->stream));
         if (succ_side) KH_HIP(hipStreamWaitEvent(t->stream, t->ev_conv, 0));
         KH_HIP(hipEventRecord(t->ev_wk1, t->stream));
         t->wk_timed = true;

@@ -649,8 +649,16 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     if (nw == 0) return hipSuccess;
     // two blocks per CU (512 on MI355X): with non-temporal probes fewer walkers in flight contend
     // less (C3 walk 5.71 -> 5.48-5.54 ms vs 2048 blocks, C2 0.67 -> 0.54; 384: 6.10)
+    // grid_blocks <= 0: -grid_blocks blocks per CU (0: two). Walker blocks per CU, C3 walk ms:
+    // 1: 1.78, 2: 1.32, 3: 1.24, 4: 1.37, 5: 1.50 (load 0.5); at load 0.85 three are slower than two
+    // (2.39 vs 2.27: longer probe runs, more requests in flight contend); C2 (k=19) 0.37 vs 0.35
+    static const int bpc_env = [] {  // KH_WALK_BPC: override (A/B runs)
+        const char* e = getenv("KH_WALK_BPC");
+        return e && atoi(e) > 0 ? atoi(e) : 0;
+    }();
+    const int bpc = bpc_env ? bpc_env : (grid_blocks < 0 ? -grid_blocks : 2);
     const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
-                                         (uint64_t)(grid_blocks > 0 ? grid_blocks : 2 * cu_count()));
+                                         (uint64_t)(grid_blocks > 0 ? grid_blocks : bpc * cu_count()));
     if (p.W == 1)
         with_kt<1>(p.K, [&](auto kt) { k_walk_q<1, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); });
     else

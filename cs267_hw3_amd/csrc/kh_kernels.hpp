@@ -103,6 +103,7 @@ bool rec_succ_fits(const KParams& p, uint32_t hcap);
 bool rec_succ_side(const KParams& p);
 hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uint32_t hcap, hipStream_t s,
                            unsigned blocks = 0);
+// grid_blocks > 0: that many blocks; <= 0: -grid_blocks blocks per CU (0: two)
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s);
 // the walkers' own head records (wb.start_rec), before the walk
