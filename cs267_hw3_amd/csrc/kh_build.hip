@@ -1980,7 +1980,8 @@ static void hot_fixup(const KParams& p, uint64_t cap, uint64_t n, uint32_t RC, b
 
 template <int W>
 static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bool table_empty, const PartBuffers& B,
-                               unsigned long long* ctr, unsigned long long* stats, hipStream_t s) {
+                               unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
+                               hipEvent_t after_hot = nullptr) {
     hipError_t e;
     const size_t lds = (size_t)build_lds(p, t.cap, B.headrec && B.hcap);
     if ((e = allow_lds(k_part_build<W>, lds)) != hipSuccess) return e;
@@ -2005,6 +2006,8 @@ static hipError_t build_launch(const KParams& p, uint64_t total, TableView t, bo
     if ((e = hipMemsetAsync(ctr + CT_OVF2, 0, 24, s)) != hipSuccess) return e;  // CT_OVF2, CT_HOT, CT_HOTNEW
     static_assert(CT_HOT == CT_OVF2 + 1 && CT_HOTNEW == CT_HOT + 1, "counter layout");
     hot_fixup<W>(p, t.cap, total, RC, table_empty, B, part_overflow_cap(total), ovf2_cap, ctr, stats, s);
+    // the remapped-region count (CT_HOT) is final here: the caller may read it beside the build
+    if (after_hot && (e = hipEventRecord(after_hot, s)) != hipSuccess) return e;
     KParams q = p;  // the build and the CAS inserts place keys of remapped regions by key hash
     q.hot = B.hot;
     // balanced bounds: an empty table's build sizes every region slice from its final count
@@ -2112,7 +2115,8 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
                               TableView t, bool table_empty, const PartBuffers& B, uint64_t* start_mask,
                               uint64_t* split_mask, unsigned long long* ctr, unsigned long long* stats, hipStream_t s,
                               hipEvent_t after_records = nullptr, uint64_t* wsplits = nullptr,
-                              uint64_t wsplits_cap = 0, hipEvent_t before_build = nullptr) {
+                              uint64_t wsplits_cap = 0, hipEvent_t before_build = nullptr,
+                              hipEvent_t after_hot = nullptr) {
     hipError_t e;
     const uint64_t ovf_cap = part_overflow_cap(n);
     const uint32_t CAP1 = part_win1_cap(n), RC = part_region_cap(p, n);
@@ -2166,7 +2170,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (after_records && (e = hipEventRecord(after_records, s)) != hipSuccess) return e;
     if ((e = win2_launch<W>(p, B, n, RC, rcnt, ovf_cap, ctr, stats, CAP1, wcnt, s)) != hipSuccess) return e;
     if (before_build && (e = hipEventRecord(before_build, s)) != hipSuccess) return e;
-    return build_launch<W>(p, n, t, table_empty, B, ctr, stats, s);
+    return build_launch<W>(p, n, t, table_empty, B, ctr, stats, s, after_hot);
 }
 
 // Staged build (sharded insert): words arrive in chunks (one per all-to-all chunk). Each chunk is
@@ -2281,13 +2285,14 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
                               TableView t, bool table_empty, const PartBuffers& b,
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
                               unsigned long long* stats, hipStream_t s, hipEvent_t after_records,
-                              uint64_t* wsplits, uint64_t wsplits_cap, hipEvent_t before_build) {
+                              uint64_t* wsplits, uint64_t wsplits_cap, hipEvent_t before_build,
+                              hipEvent_t after_hot) {
     if (n == 0) return hipSuccess;
     if (recs) {
         return p.W == 1 ? part_insert<1, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
-                                               stats, s, after_records, nullptr, 0, before_build)
+                                               stats, s, after_records, nullptr, 0, before_build, after_hot)
                         : part_insert<2, true>(p, recs, nullptr, n, t, table_empty, b, start_mask, split_mask, ctr,
-                                               stats, s, after_records, nullptr, 0, before_build);
+                                               stats, s, after_records, nullptr, 0, before_build, after_hot);
     }
     return p.W == 1 ? part_insert<1, false>(p, nullptr, words, n, t, table_empty, b, nullptr, nullptr, ctr, stats, s,
                                             nullptr, wsplits, wsplits_cap, before_build)

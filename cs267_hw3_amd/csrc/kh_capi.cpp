@@ -156,6 +156,12 @@ struct kh_table {
     hipStream_t side = nullptr;
     hipEvent_t ev_conv = nullptr, ev_side = nullptr;
     bool ins_timed = false, walk_timed = false, wk_timed = false;  // wk: ev_wk1 recorded by this walk
+    // counters copied to pinned host memory on the side stream once the last device insert's start
+    // compaction and hot-region mark are final (ev_hot / ev_ctr), so assemble reads them without
+    // waiting for the build: ctr_early says the copy belongs to the current table state
+    unsigned long long* hctr = nullptr;
+    hipEvent_t ev_hot = nullptr, ev_ctr = nullptr;
+    bool ctr_early = false;
 };
 
 namespace {
@@ -366,9 +372,11 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
                          &t->ev_b0, &t->ev_b1, &t->ev_wk1};
     for (auto* ev : evs)
         if (hipEventCreate(ev) != hipSuccess) return bail(fail(KH_ERR_HIP, "hipEventCreate failed"));
-    for (auto* ev : {&t->ev_conv, &t->ev_side})
+    for (auto* ev : {&t->ev_conv, &t->ev_side, &t->ev_hot, &t->ev_ctr})
         if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
             return bail(fail(KH_ERR_HIP, "hipEventCreate failed"));
+    if (hipHostMalloc((void**)&t->hctr, kh::CT_NUM * 8, hipHostMallocDefault) != hipSuccess)
+        return bail(fail(KH_ERR_NOMEM, "pinned host counters"));
     if ((rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8))) return bail(rc);
     if ((rc = t->hot.ensure(kh::HOT_WORDS * 4))) return bail(rc);
     t->kp.hot = t->hot.as<uint32_t>();
@@ -407,9 +415,10 @@ int kh_destroy(kh_table* t) {
     for (auto* b : bufs) b->release();
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_b0,
                         t->ev_b1, t->ev_wk1, t->ev_conv,
-                        t->ev_side};
+                        t->ev_side, t->ev_hot, t->ev_ctr};
     for (auto ev : evs)
         if (ev) (void)hipEventDestroy(ev);
+    if (t->hctr) (void)hipHostFree(t->hctr);
     if (t->side) (void)hipStreamDestroy(t->side);
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
     delete t;
@@ -421,6 +430,7 @@ int kh_destroy(kh_table* t) {
 
 int kh_reserve(kh_table* t, uint64_t n_kmers) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (n_kmers <= t->n_kmers) return KH_OK;
     if (t->n_inserted || t->staging)
         return fail(KH_ERR_STATE, "kh_reserve on a table holding %llu k-mers (clear it first)",
@@ -451,6 +461,7 @@ int kh_reserve(kh_table* t, uint64_t n_kmers) {
 
 int kh_clear(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (int rc = set_device(t)) return rc;
     if (int rc = join_succ(t)) return rc;
     t->slots_stale = true;
@@ -527,7 +538,8 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
                                       fresh, pb, t->mask.as<uint64_t>(), split_mask,
                                       t->ctr.as<unsigned long long>(),
                                       t->stats.as<unsigned long long>(), t->stream,
-                                      overlap ? t->ev_conv : nullptr, nullptr, 0, t->ev_b0));
+                                      overlap ? t->ev_conv : nullptr, nullptr, 0, t->ev_b0,
+                                      overlap ? t->ev_hot : nullptr));
         KH_HIP(hipEventRecord(t->ev_b1, t->stream));
     } else {
         if ((rc = cas_hot_prepass(t, dev_recs, nullptr, n))) return rc;
@@ -545,9 +557,18 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
                                          t->splits.as<uint64_t>(), t->ctr.as<unsigned long long>(), cs,
                                          kh::CT_N_SPLIT));
     KH_HIP(hipEventRecord(t->ev_ins1, t->stream));
+    t->ctr_early = false;
     if (overlap) {
         KH_HIP(hipEventRecord(t->ev_side, t->side));
         KH_HIP(hipStreamWaitEvent(t->stream, t->ev_side, 0));
+        // start / splitter counts (final after the compaction above) and the remapped-region count
+        // (final after the hot mark, ev_hot) to pinned memory beside the build
+        if (!kh::debug_flag("ctr_sync")) {
+            KH_HIP(hipStreamWaitEvent(t->side, t->ev_hot, 0));
+            KH_HIP(hipMemcpyAsync(t->hctr, t->ctr.p, kh::CT_NUM * 8, hipMemcpyDeviceToHost, t->side));
+            KH_HIP(hipEventRecord(t->ev_ctr, t->side));
+            t->ctr_early = true;
+        }
     }
     KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
     t->ins_timed = true;
@@ -634,6 +655,7 @@ static int insert_chunked_upload(kh_table* t, const uint8_t* host_recs, uint64_t
 
 int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (n == 0) return KH_OK;
     if (!host_recs) return fail(KH_ERR_ARG, "null records");
     if (int rc = set_device(t)) return rc;
@@ -680,6 +702,7 @@ int kh_find(kh_table* t, const uint8_t* keys, uint64_t n, uint8_t* out, uint8_t*
 
 int kh_set_starts(kh_table* t, const uint8_t* recs, uint64_t n) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (n && !recs) return fail(KH_ERR_ARG, "null records");
     if (int rc = set_device(t)) return rc;
     int rc;
@@ -705,8 +728,15 @@ int kh_assemble_dev(kh_table* t) {
     // The start count decides buffer sizes and the grid (the reference also knows
     // start_nodes.size() on the host before walking, kmer_hash.cpp:41).
     unsigned long long cv[kh::CT_NUM];
-    KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
-    KH_SYNC(t);
+    if (t->ctr_early) {  // copied beside the build (kh_insert_dev): wait for the copy, not the build
+        ++t->host_syncs;
+        KH_HIP(hipEventSynchronize(t->ev_ctr));
+        memcpy(cv, t->hctr, sizeof cv);
+        t->ctr_early = false;
+    } else {
+        KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
+        KH_SYNC(t);
+    }
     const uint64_t ns = cv[kh::CT_N_STARTS];
     uint64_t nsp = 0;
     const unsigned long long* nsp_dev = nullptr;
@@ -1031,6 +1061,7 @@ int ensure_route(kh_table* t, uint64_t n, int nranks) {
 
 int kh_collect_starts_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (n == 0) return KH_OK;
     if (!dev_recs) return fail(KH_ERR_ARG, "null records");
     if (int rc = set_device(t)) return rc;
@@ -1067,6 +1098,7 @@ int kh_pack_text_dev(kh_table* t, const void* dev_text, uint64_t len, void* dev_
 int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* words_out,
                  void* counts_out) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
     if (!counts_out || (n && (!dev_recs || !words_out))) return fail(KH_ERR_ARG, "null buffer");
     if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
@@ -1112,6 +1144,7 @@ static int collect_word_splits(kh_table* t, const void* words, uint64_t m, bool 
 int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* words_out,
                         void* counts_out) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
     if (!counts_out || (n && (!dev_recs || !words_out))) return fail(KH_ERR_ARG, "null buffer");
     if (!aligned16(dev_recs)) return fail(KH_ERR_ARG, "device records must be 16-byte aligned");
@@ -1143,6 +1176,7 @@ int kh_route_starts_dev(kh_table* t, const void* dev_recs, uint64_t n, int nrank
 int kh_route_starts_win_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void* words_out,
                             uint64_t win, void* counts_out) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (nranks < 1 || nranks > kh::MAX_RANKS) return fail(KH_ERR_ARG, "nranks %d outside [1,%d]", nranks, kh::MAX_RANKS);
     if (!counts_out || (n && (!dev_recs || !words_out))) return fail(KH_ERR_ARG, "null buffer");
     if (!aligned16(dev_recs) || !aligned16(words_out)) return fail(KH_ERR_ARG, "device buffers must be 16-byte aligned");
@@ -1192,6 +1226,7 @@ int kh_counters_dev(kh_table* t, void* dev_out) {
 
 int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (m == 0) return KH_OK;
     if (!words) return fail(KH_ERR_ARG, "null words");
     if (t->n_inserted + m > t->n_kmers)
@@ -1235,6 +1270,7 @@ int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
 
 int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64_t total_hint) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (m && !words) return fail(KH_ERR_ARG, "null words");
     if (int rc = set_device(t)) return rc;
     if (int rc = join_succ(t)) return rc;
@@ -1290,6 +1326,7 @@ int kh_insert_words_stage_dev(kh_table* t, const void* words, uint64_t m, uint64
 
 int kh_insert_words_finish(kh_table* t) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (!t->staging) return fail(KH_ERR_STATE, "no staged insert open");
     if (int rc = set_device(t)) return rc;
     t->build_timed = t->stage_part;
@@ -1333,6 +1370,7 @@ static unsigned long long* mw_word(kh_table* t, int i) { return t->mw_misc.as<un
 int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint64_t n_starts, uint64_t n_splitters,
                    uint64_t total_walkers, uint64_t* n_walkers) {
     if (!t) return fail(KH_ERR_ARG, "null table");
+    t->ctr_early = false;  // counters may change: assemble reads them on the stream
     if (nranks < 1 || nranks > kh::MAX_RANKS || rank < 0 || rank >= nranks)
         return fail(KH_ERR_ARG, "bad rank %d of %d", rank, nranks);
     if (int rc = set_device(t)) return rc;

@@ -368,7 +368,7 @@ hipError_t launch_part_insert(const KParams& p, const uint8_t* recs, const uint6
                               uint64_t* start_mask, uint64_t* split_mask, unsigned long long* ctr,
                               unsigned long long* stats, hipStream_t s, hipEvent_t after_records = nullptr,
                               uint64_t* word_splits = nullptr, uint64_t word_splits_cap = 0,
-                              hipEvent_t before_build = nullptr);
+                              hipEvent_t before_build = nullptr, hipEvent_t after_hot = nullptr);
 
 // Staged build of routed words (sharded insert): launch_part_stage per received chunk (first = the
 // first chunk of a build sized for `total` words), then launch_part_finish once. Requires
