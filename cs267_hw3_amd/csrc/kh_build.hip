@@ -1103,19 +1103,9 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t& total, 
     return pre + x - v;
 }
 
-#ifndef KH_STREAM_NT
-#define KH_STREAM_NT 0
-#endif
-// 16-B load of a streamed input (records, pass-1 / pass-2 windows), non-temporal under
-// KH_STREAM_NT: read once, it need not displace the windows' partly written lines in L2
-__device__ __forceinline__ ulonglong2 ld_stream16(const void* q) {
-    if (KH_STREAM_NT) {
-        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-        const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q));
-        return make_ulonglong2(v.x, v.y);
-    }
-    return *reinterpret_cast<const ulonglong2*>(q);
-}
+// 16-B load of a streamed input (records, pass-1 / pass-2 windows). Non-temporal loads here
+// measured slower (C3 9.79 -> 9.87 ms): the windows' partly written lines stay in L2 either way.
+__device__ __forceinline__ ulonglong2 ld_stream16(const void* q) { return *reinterpret_cast<const ulonglong2*>(q); }
 
 template <int W, int TB, int TILE>
 __device__ __forceinline__ void load_words_tb(const uint64_t* __restrict__ words, uint64_t base, uint64_t end,
@@ -1171,9 +1161,6 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
 #ifndef KH_SORT_SPLIT
 #define KH_SORT_SPLIT 1
 #endif
-#ifndef KH_DIRECT_SCATTER
-#define KH_DIRECT_SCATTER 0
-#endif
 // Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
 // with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
 // out[window(bin) + reserved + rank] (positions past cap -> overflow list).
@@ -1186,68 +1173,6 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
                                                    unsigned long long* ctr, unsigned long long* stats, NextF next) {
     constexpr int IPT = TILE / TB;
     static_assert(NB <= TB, "one bin per thread");
-    if constexpr (KH_DIRECT_SCATTER != 0 && !WRANK) {
-        // no LDS staging: every lane stores its word at its run position (L2 merges a run's
-        // stores; runs of one window come from blocks of one XCD)
-        __shared__ uint32_t spill_d;
-        if (threadIdx.x < NB) hist[threadIdx.x] = 0;
-        if (threadIdx.x == 0) spill_d = 0;
-        lds_barrier();
-        uint32_t rank[IPT];
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) rank[j] = (a[j] != EMPTY) ? atomicAdd(&hist[bin[j]], 1u) : 0u;
-        lds_barrier();
-        const uint32_t hv = threadIdx.x < NB ? hist[threadIdx.x] : 0u;
-        if (threadIdx.x < NB) {
-            const uint32_t g = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
-            gpos[threadIdx.x] = g;
-            if (hv && g + hv > cap) spill_d = 1;
-        }
-        lds_barrier();
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            if (a[j] == EMPTY) continue;
-            const uint32_t w = gpos[bin[j]] + rank[j];
-            if (w < cap) {
-                const uint64_t g = window(bin[j]) + w;
-                if (W == 2)
-                    *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(a[j], b[j]);
-                else
-                    out[g] = a[j];
-            }
-        }
-        if (spill_d) {  // as below: one overflow-list reservation per tile
-            __shared__ uint32_t keepd[NB];
-            __shared__ unsigned long long sbased;
-            uint32_t sp = 0;
-            if (threadIdx.x < NB) {
-                const uint32_t g = gpos[threadIdx.x];
-                const uint32_t keep = g >= cap ? 0u : min(hv, cap - g);
-                keepd[threadIdx.x] = keep;
-                sp = hv - keep;
-            }
-            uint32_t stot;
-            const uint32_t so = block_scan_u32<TB>(sp, stot, wsum);
-            if (threadIdx.x < NB) start[threadIdx.x] = so;
-            if (threadIdx.x == 0) sbased = atomicAdd(&ctr[CT_OVF], (unsigned long long)stot);
-            lds_barrier();
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                if (a[j] == EMPTY || rank[j] < keepd[bin[j]]) continue;
-                const uint64_t d = sbased + start[bin[j]] + (rank[j] - keepd[bin[j]]);
-                if (d < ovf_cap) {
-                    ovf[d * W] = a[j];
-                    if (W == 2) ovf[d * W + 1] = b[j];
-                } else {
-                    atomicAdd(&stats[ST_FULL], 1ull);
-                }
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        next();
-        lds_barrier();  // hist / gpos / start are rewritten by the next tile
-        return;
-    }
     __shared__ uint32_t spill;  // some bin's run passes its window's end (block-uniform after the barrier)
     if (threadIdx.x < NB) hist[threadIdx.x] = 0;
     if (threadIdx.x == 0) spill = 0;
