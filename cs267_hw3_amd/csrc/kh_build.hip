@@ -65,7 +65,11 @@ static uint64_t win_blocks1(uint64_t n) { return (n + (uint64_t)T1 * WIN_TILE - 
 // pass-2 blocks per bucket
 static uint64_t win_G(uint64_t n) {
     const uint64_t tiles_per_bucket = (n / NB1 + WIN_TILE - 1) / WIN_TILE + 1;
-    return (tiles_per_bucket + 1) / 2;
+    static const uint64_t tpb = [] {  // KH_WIN2_TPB: tiles per pass-2 block (A/B runs; default 2)
+        const char* e = getenv("KH_WIN2_TPB");
+        return (uint64_t)(e && atoi(e) > 0 ? atoi(e) : 2);
+    }();
+    return (tiles_per_bucket + tpb - 1) / tpb;
 }
 
 uint64_t part_count_words() { return (NW1 + 2 * NREG_MAX) / 2; }
