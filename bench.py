@@ -6,9 +6,11 @@ materialise the contig text (test_<rank>.dat bytes) in HBM. Inputs are generated
 copied to HBM before timing; the D2H of the contigs is outside the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2] [--n N]
-  N > 1: torch.distributed.run, one rank per GPU; the table is sharded by a hash of each
-         k-mer's minimizer, routed words and migrating walkers move with RCCL all-to-all
-         (cs267_hw3_amd.dist); weak scaling (n k-mers per GPU).
+  N > 1: one rank per GPU; the table is sharded by a hash of each k-mer's minimizer, routed
+         words and migrating walkers move with RCCL all-to-all (cs267_hw3_amd.dist); weak
+         scaling (n k-mers per GPU). Under an outer torch.distributed.run the ranks are its
+         processes; without one (no WORLD_SIZE) bench.py starts N ranks itself as a
+         torch.distributed.run child before any GPU call. A world size other than --gpus fails.
 """
 import argparse
 import json
@@ -196,6 +198,27 @@ def end_to_end(table, host, n, nl, truth, steps):
                     "(H2D + insert), kh_assemble, kh_contigs_text D2H into pinned host memory"}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without an outer torchrun: start N ranks (one process per GPU) as a
+    torch.distributed.run CHILD of this process and exit with its status. This parent has not
+    touched the GPU (nothing above imports torch or the library), and it never execs: the ranks
+    are children. Rank 0 prints the JSON line; its stdout is passed through unchanged."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, KH_BENCH_LAUNCHED="1")
+    log(f"bench: --gpus {n} without WORLD_SIZE: launching {n} ranks via torch.distributed.run")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,10 +242,16 @@ def main():
     w["name"] = args.workload
     if args.n:
         w["n"] = args.n
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if os.environ.get("KH_BENCH_LAUNCHED"):
+            raise SystemExit("bench: launched ranks see no WORLD_SIZE")
+        return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        # never report an N-GPU run measured on another number of ranks
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return 2
     if world > 1 or os.environ.get("KH_BENCH_FORCE_DIST") == "1":
         # sharded path (also forced at one rank to exercise it on a 1-GPU box)
         from cs267_hw3_amd import dist

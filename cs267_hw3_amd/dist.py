@@ -868,6 +868,9 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
 
     local = init_rank_process_group()
     comm = TorchComm()
+    if comm.world != world or comm.world != args.gpus:
+        raise SystemExit(f"bench: the communicator has {comm.world} ranks, --gpus {args.gpus}, "
+                         f"WORLD_SIZE {world}")
     k = w["k"]
     strong = bool(w.get("strong"))
     n_total = w["n"] if strong else w["n"] * world
@@ -950,7 +953,7 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
         achieved = units * b_alg / (build_ms / 1e3) / 1e9 if build_ms else 0.0
         out = {
             "metric": "k-mer inserts+lookups/sec (k=51)" if k == 51 else f"k-mer inserts+lookups/sec (k={k})",
-            "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+            "value": value, "unit": "ops/s", "n_gpus": comm.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": tmax * 1e3, "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": value / 72.6e6, "dtype": "u64",
             "data": "synthetic",

@@ -104,3 +104,33 @@ def test_bench_multiprocess(tmp_path):
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
     assert line["n_gpus"] == 2 and line["verified_vs_truth"] is True
     assert line["config"]["n_kmers_total"] == 4_000_000 and line["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_self_launch(tmp_path):
+    """`python bench.py --gpus 2` with no outer torchrun (the way the driver calls --gpus 1):
+    bench.py starts the 2 ranks itself as a torch.distributed.run child before any GPU call, and
+    the line reports the communicator's world size."""
+    import json
+    import sys
+    env = _shared_gpu_env()
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--kmers", "2000000",
+                        "--steps", "2", "--warmup", "1", "--no-cpu", "--e2e-steps", "0"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert line["n_gpus"] == 2 and line["verified_vs_truth"] is True
+    assert line["config"]["n_kmers_total"] == 4_000_000
+
+
+def test_bench_world_size_mismatch_fails(tmp_path):
+    """--gpus N under a launcher whose world size differs is an error, never a 1-GPU line
+    (checked before anything touches a GPU)."""
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
