@@ -127,6 +127,7 @@ struct kh_table {
     bool words_split = true;   // every routed word since the last clear went through splitter collection
     bool ms_on = false;        // the current migrating walk uses splitter segments
     uint64_t ms_ns = 0, ms_nsp = 0, ms_cap2 = 0, ms_nq = 0;
+    bool walk_bounded = false; // the last walk's text was sized before it ran (kh_assemble_dev)
     uint64_t mw_wg = 0;        // walkers of every rank (bound of a round's input / held-back messages)
     uint64_t mw_store_n = 0;   // text records in mw_store (valid when mw_store_known)
     uint64_t mw_store_bound = 0;  // upper bound of the store's records (its device count: mw_misc[2])
@@ -202,11 +203,8 @@ int read_ctr(kh_table* t, int idx, uint64_t* v) {
     return KH_OK;
 }
 
-// First device-side error, as a status code.
-int check_stats(kh_table* t) {
-    unsigned long long st[kh::ST_NUM];
-    KH_HIP(hipMemcpyAsync(st, t->stats.p, sizeof st, hipMemcpyDeviceToHost, t->stream));
-    KH_SYNC(t);
+// First device-side error of a copy of the stats, as a status code.
+static int stats_status(const unsigned long long* st) {
     if (st[kh::ST_FULL]) return fail(KH_ERR_FULL, "table full: %llu probes wrapped", st[kh::ST_FULL]);
     if (st[kh::ST_DUP]) return fail(KH_ERR_DUPLICATE, "%llu duplicate k-mers inserted", st[kh::ST_DUP]);
     if (st[kh::ST_BAD_EXT])
@@ -220,6 +218,14 @@ int check_stats(kh_table* t) {
     if (st[kh::ST_BAD_BASE])
         return fail(KH_ERR_BAD_BASE, "%llu k-mer lines with a base outside {A,C,G,T}", st[kh::ST_BAD_BASE]);
     return KH_OK;
+}
+
+// First device-side error, as a status code.
+int check_stats(kh_table* t) {
+    unsigned long long st[kh::ST_NUM];
+    KH_HIP(hipMemcpyAsync(st, t->stats.p, sizeof st, hipMemcpyDeviceToHost, t->stream));
+    KH_SYNC(t);
+    return stats_status(st);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -842,6 +848,7 @@ int kh_assemble_dev(kh_table* t) {
     // the pool the first attempt asked for.
     const bool bounded = !t->starts_explicit && !t->text_sync && !kh::debug_flag("text_sync");
     t->text_sync = false;
+    t->walk_bounded = bounded;
     if (bounded) {
         if ((rc = t->text.ensure(ns * (uint64_t)(t->kp.K + 1) + n + 64))) return rc;
         wb.text_cap = t->text.bytes;
@@ -922,14 +929,25 @@ int kh_assemble_dev(kh_table* t) {
 
 int kh_assemble(kh_table* t, uint64_t* n_contigs, uint64_t* out_bytes) {
     if (int rc = kh_assemble_dev(t)) return rc;
-    if (int rc = check_stats(t)) return rc;  // one wait (ordered after the queued work)
-    uint64_t ob = 0;
-    if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
-    if (t->last_contigs && ob > t->text.bytes) {  // past the bound (malformed input): sized walk
+    // the stats and the text's byte count in one wait (ordered after the queued work)
+    unsigned long long st[kh::ST_NUM], ob = 0;
+    KH_HIP(hipMemcpyAsync(st, t->stats.p, sizeof st, hipMemcpyDeviceToHost, t->stream));
+    KH_HIP(hipMemcpyAsync(&ob, t->ctr.as<unsigned long long>() + kh::CT_OUT_BYTES, 8, hipMemcpyDeviceToHost,
+                          t->stream));
+    KH_SYNC(t);
+    // a walk sized before it ran (kh_assemble_dev's bound) that passed its text bound or ran out of
+    // walker chunks (both only on malformed input, e.g. walks that overlap) is redone the slow way:
+    // the text sized from the scanned total, the chunk pool from what the first attempt asked for
+    if (t->walk_bounded && t->last_contigs && (st[kh::ST_CHUNK_OVF] || ob > t->text.bytes)) {
+        KH_HIP(hipMemsetAsync(t->stats.as<unsigned long long>() + kh::ST_CHUNK_OVF, 0, 8, t->stream));
         t->text_sync = true;
         if (int rc = kh_assemble_dev(t)) return rc;
         if (int rc = check_stats(t)) return rc;
-        if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &ob)) return rc;
+        uint64_t o2 = 0;
+        if (int rc = read_ctr(t, kh::CT_OUT_BYTES, &o2)) return rc;
+        ob = o2;
+    } else if (int rc = stats_status(st)) {
+        return rc;
     }
     if (n_contigs) *n_contigs = t->last_contigs;
     if (out_bytes) *out_bytes = ob;
@@ -1481,7 +1499,7 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
         nb = (uint64_t)P * in_cap;
         if (nb > t->mw_wg) nb = t->mw_wg;  // walkers never multiply
         if ((rc = t->mw_list.ensure((nb + 1) * kh::MSG_WORDS * 8))) return rc;
-        KH_HIP(kh::launch_slot_gather((const uint64_t*)in_slots, P, in_cap, t->mw_list.as<uint64_t>(), n_dev,
+        KH_HIP(kh::launch_slot_gather((const uint64_t*)in_slots, P, in_cap, t->mw_list.as<uint64_t>(), n_dev, nb,
                                       t->stream));
         src = t->mw_list.as<uint64_t>();
     } else {
@@ -1592,10 +1610,12 @@ int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
     KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
                                      t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
     if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
+    // the text is sized from a host bound (no device read): every writer stops at its end, so a
+    // corrupt length or an overflowed store fails at kh_sync instead of writing past it
     KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
-                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream, t->text.bytes));
     KH_HIP(kh::launch_mw_words(t->kp.K, (const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(),
-                               t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+                               t->contig_off.as<uint64_t>(), t->text.as<char>(), t->text.bytes, t->stream));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = nc;
@@ -1699,9 +1719,9 @@ int kh_mwalk_end_seg_dev(kh_table* t, const void* recs, uint64_t n, const void* 
                                      t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
     if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
     KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
-                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream, t->text.bytes));
     KH_HIP(kh::launch_mseg_words(t->kp.K, (const uint64_t*)recs, n, (const uint64_t*)seg_recs, m, nc, st,
-                                 t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream));
+                                 t->contig_off.as<uint64_t>(), t->text.as<char>(), t->text.bytes, t->stream));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = nc;

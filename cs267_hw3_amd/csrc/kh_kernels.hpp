@@ -211,15 +211,15 @@ hipError_t launch_mseg_retag(const uint64_t* recs, uint64_t n, uint64_t ns, uint
 hipError_t launch_mseg_lens(const uint64_t* in3, uint64_t m, uint64_t ns, const MSegState& st, uint32_t* contig_len,
                             hipStream_t s);
 hipError_t launch_mseg_words(int K, const uint64_t* recs, uint64_t n, const uint64_t* in3, uint64_t m, uint64_t ns,
-                             const MSegState& st, const uint64_t* off, char* out, hipStream_t s);
+                             const MSegState& st, const uint64_t* off, char* out, uint64_t cap, hipStream_t s);
 hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
                          hipStream_t s);
 // ---- fixed-size exchange slots (no host read per round) ----------------------------------------
 // A round's exchange buffer is P slots of slot_words(cap) words: [count, 0, cap messages].
 __host__ __device__ inline uint64_t slot_words(uint64_t cap) { return 2 + cap * MSG_WORDS; }
-// messages of P slots -> list (contiguous), *n = their number
+// messages of P slots -> list (contiguous, n_max at most), *n = their number
 hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
-                              unsigned long long* n, hipStream_t s);
+                              unsigned long long* n, uint64_t n_max, hipStream_t s);
 // this round's outgoing messages (walk outputs j < *n_dev with a destination, then the messages
 // held back last round) -> P slots of cap (overflow held back in carry_out / carry_dst_out,
 // *carry_n_out); live = [messages in flight, largest per-destination count].
@@ -261,8 +261,9 @@ hipError_t launch_fin_check(const unsigned long long* fin, uint64_t want, const 
                             uint64_t want_max, unsigned long long* stats, hipStream_t s);
 hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,
                           unsigned long long* fin, hipStream_t s);
+// cap: bytes of `out` (words past it are skipped: a bad length fails at kh_sync, never overruns)
 hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
-                           const uint64_t* off, char* out, hipStream_t s);
+                           const uint64_t* off, char* out, uint64_t cap, hipStream_t s);
 
 // read_kmers.hpp:62-76 on the device: n fixed-width "KMER BF\n" lines (K+4 bytes) -> kmer_pair
 // records; lines with a non-ACGT k-mer character count in stats[ST_BAD_BASE].

@@ -390,7 +390,8 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_lens_remote(const uint64_t* in3,
 
 // start segments' own words (bounded by the start segment's length, not the contig's)
 __global__ __launch_bounds__(BLOCK) void k_mseg_words_local(int K, const uint64_t* recs, uint64_t n, uint64_t ns,
-                                                            MSegState st, const uint64_t* off, char* out) {
+                                                            MSegState st, const uint64_t* off, char* out,
+                                                            uint64_t cap) {
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t t = recs[2 * i];
         if ((t >> 55) & 1) continue;
@@ -400,6 +401,7 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_words_local(int K, const uint64_
         const uint64_t app = st.len[c], j0 = wn * 32;
         if (j0 >= app) continue;
         const uint32_t cnt = (uint32_t)(app - j0 < 32 ? app - j0 : 32);
+        if (off[c] + K + j0 + cnt > cap) continue;  // a bad length: kh_sync reports it, never overrun
         const uint64_t word = recs[2 * i + 1];
         store_chars(out + off[c] + K + j0, cnt,
                     [&](uint32_t x) { return codes4_chars((uint32_t)(word >> (8 * x)) & 0xFFu); });
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_words_local(int K, const uint64_
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mseg_words_remote(int K, const uint64_t* in3, uint64_t m, uint64_t ns,
-                                                             const uint64_t* off, char* out) {
+                                                             const uint64_t* off, char* out, uint64_t cap) {
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t t = in3[3 * i];
         if (((t >> 48) & 0xFF) != 0) continue;
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_words_remote(int K, const uint64
         const uint64_t pc = in3[3 * i + 1];
         const uint64_t pos = pc & ((1ull << 48) - 1);
         const uint32_t cnt = (uint32_t)(pc >> 48);
-        if (!cnt) continue;
+        if (!cnt || off[c] + K + pos + cnt > cap) continue;  // bad position: never overrun
         const uint64_t word = in3[3 * i + 2];
         store_chars(out + off[c] + K + pos, cnt,
                     [&](uint32_t x) { return codes4_chars((uint32_t)(word >> (8 * x)) & 0xFFu); });
@@ -487,9 +489,9 @@ hipError_t launch_mseg_lens(const uint64_t* in3, uint64_t m, uint64_t ns, const 
 }
 
 hipError_t launch_mseg_words(int K, const uint64_t* recs, uint64_t n, const uint64_t* in3, uint64_t m, uint64_t ns,
-                             const MSegState& st, const uint64_t* off, char* out, hipStream_t s) {
-    if (n) k_mseg_words_local<<<grid_n(n, 8192), BLOCK, 0, s>>>(K, recs, n, ns, st, off, out);
-    if (m) k_mseg_words_remote<<<grid_n(m, 8192), BLOCK, 0, s>>>(K, in3, m, ns, off, out);
+                             const MSegState& st, const uint64_t* off, char* out, uint64_t cap, hipStream_t s) {
+    if (n) k_mseg_words_local<<<grid_n(n, 8192), BLOCK, 0, s>>>(K, recs, n, ns, st, off, out, cap);
+    if (m) k_mseg_words_remote<<<grid_n(m, 8192), BLOCK, 0, s>>>(K, in3, m, ns, off, out, cap);
     return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
     KParams p = specialize<KT>(p_in);
     if (mw.hot_on && *mw.hot_on == 0) p.hot = nullptr;  // no remapped region: skip the bitmap loads
     const bool chains = p.chain && mw.hcap != 0;
-    const uint64_t n_live = mw.n_dev ? (uint64_t)*mw.n_dev : mw.n_in;
+    const uint64_t n_live = mw.n_dev ? min((uint64_t)*mw.n_dev, mw.n_in) : mw.n_in;
     const uint32_t q4 = lane_id() & 3u, ql4 = lane_id() & ~3u;  // quad member, quad's first lane
     uint32_t reg = 0;  // region of the k-mer being probed (its head records live there)
     // append n bases (base i at bits 2i of piece, n <= room in the current word) to the walker's
@@ -371,7 +371,8 @@ __global__ __launch_bounds__(BLOCK) void k_mw_lens(const uint64_t* recs, uint64_
 
 // Origin side: word records -> characters.
 __global__ __launch_bounds__(BLOCK) void k_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc,
-                                                    const uint32_t* len, const uint64_t* off, char* out) {
+                                                    const uint32_t* len, const uint64_t* off, char* out,
+                                                    uint64_t cap) {
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t t = recs[2 * i];
         if ((t >> 55) & 1) continue;
@@ -382,6 +383,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_words(int K, const uint64_t* recs,
         const uint64_t j0 = wn * 32;
         if (j0 >= app) continue;
         const uint32_t cnt = (uint32_t)(app - j0 < 32 ? app - j0 : 32);
+        if (off[c] + K + j0 + cnt > cap) continue;  // a bad length: kh_sync reports it, never overrun
         const uint64_t word = recs[2 * i + 1];
         char* o = out + off[c] + K + j0;
         store_chars(o, cnt, [&](uint32_t x) { return codes4_chars((uint32_t)(word >> (8 * x)) & 0xFFu); });
@@ -473,9 +475,10 @@ __device__ __forceinline__ uint64_t slot_prefix(const uint64_t* slots, uint32_t 
 }
 
 __global__ __launch_bounds__(BLOCK) void k_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
-                                                       unsigned long long* n) {
+                                                       unsigned long long* n, uint64_t n_max) {
     __shared__ uint64_t pre[MAX_RANKS + 1];
-    const uint64_t tot = slot_prefix(slots, P, cap, pre);
+    // the list holds n_max messages (walkers never multiply; more would be a sender's bug)
+    const uint64_t tot = min(slot_prefix(slots, P, cap, pre), n_max);
     if (blockIdx.x == 0 && threadIdx.x == 0) *n = tot;
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * BLOCK) {
         uint32_t q = 0;
@@ -488,8 +491,8 @@ __global__ __launch_bounds__(BLOCK) void k_slot_gather(const uint64_t* slots, ui
 }
 
 hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
-                              unsigned long long* n, hipStream_t s) {
-    k_slot_gather<<<grid_for((uint64_t)P * cap, 4096), BLOCK, 0, s>>>(slots, P, cap, list, n);
+                              unsigned long long* n, uint64_t n_max, hipStream_t s) {
+    k_slot_gather<<<grid_for((uint64_t)P * cap, 4096), BLOCK, 0, s>>>(slots, P, cap, list, n, n_max);
     return hipGetLastError();
 }
 
@@ -504,7 +507,7 @@ struct SlotMsgOp {
     __device__ int owner(uint64_t i) const {
         if (i < r.cb) return i < *r.carry_n ? (int)r.carry_dst[i] : -1;
         const uint64_t j = i - r.cb;
-        return (j < *r.n_dev && r.dst[j] != MW_NONE) ? (int)r.dst[j] : -1;
+        return (j < *r.n_dev && j < r.nb && r.dst[j] != MW_NONE) ? (int)r.dst[j] : -1;
     }
     __device__ void emit(uint64_t i, int q, uint64_t d) const {
         if (q < 0) return;
@@ -597,9 +600,9 @@ hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_
 }
 
 hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
-                           const uint64_t* off, char* out, hipStream_t s) {
+                           const uint64_t* off, char* out, uint64_t cap, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_mw_words<<<grid_for(n, 8192), BLOCK, 0, s>>>(K, recs, n, nc, len, off, out);
+    k_mw_words<<<grid_for(n, 8192), BLOCK, 0, s>>>(K, recs, n, nc, len, off, out, cap);
     return hipGetLastError();
 }
 

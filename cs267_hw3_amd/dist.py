@@ -396,6 +396,8 @@ class DistributedKmerHashMap:
         self.checks = 0
         self.syncs = 0          # host reads of device data by this host since the last reset
         self._caps = []         # per-round slot capacities learnt from the last assemble
+        self._caps_walkers = 0  # ... whose walker count (another count: another input, not used)
+        self._cap_floor = 0     # this assemble: the demand of rounds that held messages back
         self._rounds_hint = 0   # its round count (the next assemble checks for the end there first)
 
     def close(self):
@@ -649,7 +651,7 @@ class DistributedKmerHashMap:
         else:
             P = self.P
             c = max(1024, (self._walkers + P * P - 1) // (P * P) * 5 // 4 + 1024) if P > 1 else self._walkers + 16
-        return max(1, min(c, self.SLOT_CAP_MAX))
+        return max(1, min(max(c, self._cap_floor), self.SLOT_CAP_MAX))
 
     SLOT_CAP_MAX = int(os.environ.get("KH_MW_SLOT_CAP", str(1 << 40)))  # tests: tiny slots (messages held back)
 
@@ -667,19 +669,29 @@ class DistributedKmerHashMap:
         if not failed:
             sh.mw_begin(P, self.comm.rank, total_kmers, self._ns, self._nsp, self._walkers)
         self.rounds = self.checks = 0
-        live = self._grow("_mw_live", 2 * 4096, torch.int64, dev, slack=1.0)
         inp, cap_in = None, 0
+        if self._caps_walkers != self._walkers:
+            # caps learnt from a walk of another walker count describe another input: start over
+            self._caps, self._rounds_hint = [], 0
+        self._cap_floor = 0
         check_at = self._rounds_hint or self.CHECK_EVERY
-        maxes = []
+        # rounds without splitter segments (KH_MW_SEGMENTS=0) grow with the longest chain; a
+        # walker advances every round it is not held back, so total_kmers bounds them
+        limit = self.MAX_ROUNDS if self._splitters else max(self.MAX_ROUNDS, total_kmers + self.MAX_ROUNDS)
+        # [in flight, largest per-destination count] of the rounds since the last check
+        live = self._grow("_mw_live", 2 * max(check_at, self.CHECK_EVERY) + 2, torch.int64, dev, slack=1.0)
+        maxes, used, base = [], [], 0
         while True:
             cap = self._cap(self.rounds)
+            used.append(cap)
             sw = _lib.slot_words(cap)
             out = self._grow("_mw_out_%d" % (self.rounds & 1), P * sw, torch.int64, dev)
+            lv = 2 * (self.rounds - base)
             if failed:
                 out.view(-1)[:P * sw].view(P, sw)[:, 0] = 0
-                live[2 * self.rounds:2 * self.rounds + 2] = 0
+                live[lv:lv + 2] = 0
             else:
-                sh.mw_round(inp, cap_in, out, cap, live[2 * self.rounds:])
+                sh.mw_round(inp, cap_in, out, cap, live[lv:])
             if local:
                 nxt = out      # one rank: slot 0 is the next round's input
             else:
@@ -687,29 +699,37 @@ class DistributedKmerHashMap:
                 self.comm.all_to_all(nxt[:P * sw], out[:P * sw], [sw] * P, [sw] * P)
             inp, cap_in = nxt, cap
             self.rounds += 1
-            if self.rounds >= check_at or self.rounds * 2 + 2 > live.numel():
-                # global max of every round's [in flight, largest per-destination] so far + errors
+            if self.rounds >= check_at or self.rounds >= limit:
+                # global max of the window's [in flight, largest per-destination] + errors
+                nw = 2 * (self.rounds - base)
                 if local:  # one rank: no reduction, the error is this rank's own
-                    h = self._host(live[:2 * self.rounds]).tolist() + [1 if self._err is not None else 0]
+                    h = self._host(live[:nw]).tolist() + [1 if self._err is not None else 0]
                     self.syncs -= 1  # counted below
                 else:
                     err = torch.tensor([1 if self._err is not None else 0], dtype=torch.int64, device=dev)
-                    h = self.comm.max_to_host(torch.cat([live[:2 * self.rounds], err]))
+                    h = self.comm.max_to_host(torch.cat([live[:nw], err])).tolist()
                 self.checks += 1
                 self.syncs += 1
                 if int(h[-1]):
                     if self._err is not None:
                         raise self._err
                     raise _lib.KmerHashError(_lib.KH_ERR_FULL, "another rank failed to size its shard")
-                maxes = [int(x) for x in h[1:2 * self.rounds:2]]
-                if int(h[2 * self.rounds - 2]) == 0:
+                maxes.extend(int(x) for x in h[1:nw:2])
+                if int(h[nw - 2]) == 0:
                     break
-                if self.rounds * 2 + 2 > live.numel():
-                    raise _lib.KmerHashError(_lib.KH_ERR_CYCLE, "migrating walk did not end in 4096 rounds")
+                # a round whose demand passed its slots held messages back: later rounds get slots
+                # for that demand, so the surplus drains in a few rounds, not thousands
+                for m, c in zip(maxes[base:], used[base:]):
+                    if m > c:
+                        self._cap_floor = max(self._cap_floor, m * 5 // 4 + 256)
+                if self.rounds >= limit:
+                    raise _lib.KmerHashError(_lib.KH_ERR_CYCLE, f"migrating walk did not end in {limit} rounds")
+                base = self.rounds
                 check_at = self.rounds + self.CHECK_EVERY
         # the next assemble: slots sized by what each round carried, and its first check here
         self._caps = [max(256, int(x) * 5 // 4 + 256) for x in maxes]
         self._rounds_hint = self.rounds
+        self._caps_walkers = self._walkers
         tb = sh.mw_text_bound()
         tout = self._grow("_mw_tout", max(tb, 1) * T, torch.int64, dev)
         counts = sh.mw_text(tout)
@@ -730,6 +750,7 @@ class DistributedKmerHashMap:
         return self.rounds
 
     CHECK_EVERY = int(os.environ.get("KH_MW_CHECK_EVERY", "4"))
+    MAX_ROUNDS = 4096  # with splitter segments (the default) C5's 10^6-k-mer chains take ~11
 
     def _segments_end(self, trecv, r, nseg):
         """Splitter segments: link each segment to its successor's owner, all-gather every rank's
@@ -785,7 +806,9 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
                  check=None, load_factor=0.5, steps=1):
     """P logical ranks on one GPU (threads): returns the per-rank contig texts. recs: a host
     record array, or a SyntheticKmers whose blocks each rank generates on the GPU (C4-size
-    inputs). Shards start at shard_kmers (default n / P) and grow to what they are routed.
+    inputs), or a list of host record arrays walked one after another on the same maps (clear
+    between them; returns a list of per-rank texts per input). Shards start at shard_kmers
+    (default n / P) and grow to what they are routed.
     check(rank, text) (optional) consumes each rank's text instead of returning it (large runs).
     `info` (a dict) receives the round count, per-rank table stats and, per rank, the blocking
     host reads of the last step (insert_all + assemble: this host's and the library's).
@@ -797,42 +820,46 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
     gc.collect()
     torch.cuda.empty_cache()
     comms = ThreadComm.group(nranks)
+    seq = isinstance(recs, (list, tuple))
+    inputs = list(recs) if seq else [recs]
     gen = recs if hasattr(recs, "records_dev") else None
-    n = gen.n if gen is not None else recs.shape[0]
-    split = (n + nranks - 1) // nranks
-    out = [None] * nranks
+    n0 = gen.n if gen is not None else inputs[0].shape[0]
+    out = [[None] * nranks for _ in inputs]
     errs = []
-    start = shard_kmers if shard_kmers else max(n // nranks, 1)
+    start = shard_kmers if shard_kmers else max(n0 // nranks, 1)
 
     def body(r):
         try:
             torch.cuda.set_device(device)
-            b = min(r * split, n)
-            e = min(b + split, n)
             shard = GpuShard(k, start, device=device, load_factor=load_factor)
             with torch.cuda.stream(shard.stream):
-                if gen is not None:
-                    mine = gen.records_dev(b, e, device=device, stream=shard.stream)
-                else:
-                    mine = torch.from_numpy(np.ascontiguousarray(recs[b:e])).to(shard.dev)
                 dm = DistributedKmerHashMap(comms[r], shard)
                 if insert_chunks:
                     dm.INSERT_CHUNKS = insert_chunks
                     dm.PIPELINE_MIN = 0
-                for step in range(steps):
-                    if step:
-                        shard.clear()
-                    s0 = dm.host_syncs()
-                    dm.insert_all(mine)
-                    comms[r].barrier()
-                    dm.assemble(n)
-                    syncs = dm.host_syncs() - s0
-                del mine
-                text = dm.contigs_text()
-                if check is not None:
-                    check(r, text)
-                else:
-                    out[r] = text
+                for i, inp in enumerate(inputs):
+                    n = gen.n if gen is not None else inp.shape[0]
+                    split = (n + nranks - 1) // nranks
+                    b = min(r * split, n)
+                    e = min(b + split, n)
+                    if gen is not None:
+                        mine = gen.records_dev(b, e, device=device, stream=shard.stream)
+                    else:
+                        mine = torch.from_numpy(np.ascontiguousarray(inp[b:e])).to(shard.dev)
+                    for step in range(steps):
+                        if step or i:
+                            shard.clear()
+                        s0 = dm.host_syncs()
+                        dm.insert_all(mine)
+                        comms[r].barrier()
+                        dm.assemble(n)
+                        syncs = dm.host_syncs() - s0
+                    del mine
+                    text = dm.contigs_text()
+                    if check is not None:
+                        check(r, text)
+                    else:
+                        out[i][r] = text
                 if info is not None:
                     info.setdefault("rounds", dm.rounds)
                     info.setdefault("stats", {})[r] = shard.stats()
@@ -850,7 +877,7 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
         t.join()
     if errs:
         raise errs[0]
-    return out
+    return out if seq else out[0]
 
 
 def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):

@@ -339,19 +339,32 @@ public:
         uint64_t n_in = 0;
         if (!failed) abi_check(kh_mwalk_begin(t_, P_, rank_, total_kmers, ns_, nsp_, walkers_, &n_in));
         rounds_ = checks_ = 0;
-        int64_t* live = live_.words(2 * kMaxRounds + 2);
         const int64_t* in = nullptr;
         uint64_t cap_in = 0;
+        // caps learnt from a walk of another walker count describe another input: start over
+        if (caps_walkers_ != walkers_) {
+            caps_.clear();
+            rounds_hint_ = 0;
+        }
+        cap_floor_ = 0;
         int check_at = rounds_hint_ ? rounds_hint_ : kCheckEvery;
-        std::vector<uint64_t> maxes;
+        // rounds without splitter segments (KH_MW_SEGMENTS=0) grow with the longest chain; a
+        // walker advances every round it is not held back, so total_kmers bounds them
+        const uint64_t limit = splitters_ ? (uint64_t)kMaxRounds : std::max<uint64_t>(kMaxRounds, total_kmers + kMaxRounds);
+        // [in flight, largest per-destination count] of the rounds since the last check
+        int64_t* live = live_.words(2 * (uint64_t)std::max(check_at, kCheckEvery) + 2);
+        std::vector<uint64_t> maxes, used;
+        int base = 0;
         for (;;) {
             const uint64_t cap = slot_cap(rounds_), sw = KH_SLOT_WORDS(cap);
+            used.push_back(cap);
             int64_t* out = slots_[rounds_ & 1].words(P * sw);
+            int64_t* lv = live + 2 * (rounds_ - base);
             if (failed) {
                 hip_check(hipMemset2DAsync(out, sw * 8, 0, 8, P, stream_), "hipMemset2DAsync");
-                hip_check(hipMemsetAsync(live + 2 * rounds_, 0, 16, stream_), "hipMemsetAsync");
+                hip_check(hipMemsetAsync(lv, 0, 16, stream_), "hipMemsetAsync");
             } else {
-                abi_check(kh_mwalk_round_dev(t_, in, cap_in, out, cap, live + 2 * rounds_));
+                abi_check(kh_mwalk_round_dev(t_, in, cap_in, out, cap, lv));
             }
             int64_t* nxt = out;  // one rank: slot 0 is the next round's input
             if (P > 1) {
@@ -363,11 +376,11 @@ public:
             in = nxt;
             cap_in = cap;
             ++rounds_;
-            if (rounds_ >= check_at || rounds_ >= kMaxRounds) {
-                // every rank's [in flight, largest per-destination] of every round so far + errors
-                const uint64_t w = 2 * (uint64_t)rounds_ + 1;
+            if (rounds_ >= check_at || (uint64_t)rounds_ >= limit) {
+                // every rank's window of [in flight, largest per-destination] + errors
+                const uint64_t nw = 2 * (uint64_t)(rounds_ - base), w = nw + 1;
                 int64_t* mine = pack_.words(w);
-                hip_check(hipMemcpyAsync(mine, live, (w - 1) * 8, hipMemcpyDeviceToDevice, stream_), "hipMemcpyAsync");
+                hip_check(hipMemcpyAsync(mine, live, nw * 8, hipMemcpyDeviceToDevice, stream_), "hipMemcpyAsync");
                 put_word(mine + w - 1, failed ? 1 : 0);
                 int64_t* allg = gather_.words(w * P);
                 comm_.allgather_dev(mine, w, allg, stream_);
@@ -378,10 +391,14 @@ public:
                 for (uint64_t q = 0; q < P; ++q)
                     for (uint64_t i = 0; i < w; ++i) mx[i] = std::max(mx[i], h[q * w + i]);
                 if (mx[w - 1]) throw std::runtime_error(failed ? err_ : "another rank failed to size its shard");
-                maxes.assign(rounds_, 0);
-                for (int r = 0; r < rounds_; ++r) maxes[r] = mx[2 * r + 1];
-                if (mx[2 * (uint64_t)rounds_ - 2] == 0) break;
-                if (rounds_ >= kMaxRounds) throw std::runtime_error("migrating walk did not end in kMaxRounds rounds");
+                for (uint64_t i = 1; i < nw; i += 2) maxes.push_back(mx[i]);
+                if (mx[nw - 2] == 0) break;
+                // a round whose demand passed its slots held messages back: later rounds get
+                // slots for that demand, so the surplus drains in a few rounds, not thousands
+                for (int r = base; r < rounds_; ++r)
+                    if (maxes[r] > used[r]) cap_floor_ = std::max<uint64_t>(cap_floor_, maxes[r] * 5 / 4 + 256);
+                if ((uint64_t)rounds_ >= limit) throw std::runtime_error("migrating walk did not end in its round limit");
+                base = rounds_;
                 check_at = rounds_ + kCheckEvery;
             }
         }
@@ -389,6 +406,7 @@ public:
         caps_.assign(maxes.size(), 0);
         for (size_t r = 0; r < maxes.size(); ++r) caps_[r] = std::max<uint64_t>(256, maxes[r] * 5 / 4 + 256);
         rounds_hint_ = rounds_;
+        caps_walkers_ = walkers_;
         uint64_t tb = 0;
         abi_check(kh_mwalk_text_bound(t_, &tb));
         int64_t* tout = tout_.words(std::max<uint64_t>(tb, 1) * T);
@@ -581,7 +599,7 @@ private:
             const uint64_t P = (uint64_t)P_;
             c = P > 1 ? std::max<uint64_t>(1024, (walkers_ + P * P - 1) / (P * P) * 5 / 4 + 1024) : walkers_ + 16;
         }
-        return std::max<uint64_t>(1, std::min<uint64_t>(c, slot_cap_max_));
+        return std::max<uint64_t>(1, std::min<uint64_t>(std::max(c, cap_floor_), slot_cap_max_));
     }
 
     // items of `width` words grouped by destination (ex.send) -> received (ex.recv); reverse:
@@ -673,6 +691,8 @@ private:
     uint64_t ns_ = 0, nsp_ = 0, walkers_ = 0, splitters_ = 0;  // of the last insert_all
     std::string err_;        // this shard could not be sized by the last insert_all
     std::vector<uint64_t> caps_;  // slot capacity per round, learnt from the last assemble
+    uint64_t caps_walkers_ = 0;   // ... whose walker count (another count: caps_ not used)
+    uint64_t cap_floor_ = 0;      // this assemble: the demand of rounds that held messages back
     uint64_t slot_cap_max_ = ~0ull;
     std::mutex m_;
     std::vector<hipEvent_t> events_;

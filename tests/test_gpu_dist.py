@@ -194,3 +194,19 @@ def test_sharded_tiny_slots_hold_messages_back(monkeypatch, P):
     monkeypatch.setattr(dist.DistributedKmerHashMap, "SLOT_CAP_MAX", 256)
     g = kh.SyntheticKmers(51, 60_000, 8, 200, 0, seed=7 + P)
     check_ranks(g, dist.run_threaded(51, g.records(), P, steps=2), P)
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_sharded_small_then_large_input(P):
+    """Slot capacities are learnt per input: a map that walked a small set, cleared and given a
+    C3-shape set 100x larger, sizes its first rounds from the new walker count (not the small
+    walk's slots of a few hundred), so the walk ends in a normal number of rounds with every
+    contig exact; then the small set again."""
+    from cs267_hw3_amd.dist import run_threaded
+    gs = kh.SyntheticKmers(51, 30_000, 8, 200, 0, seed=3)
+    gl = kh.SyntheticKmers(51, 3_000_000, 8, 200, 0, seed=4)
+    info = {}
+    texts = run_threaded(51, [gs.records(), gl.records(), gs.records()], P, info=info)
+    check_ranks(gs, texts[0], P)
+    check_ranks(gl, texts[1], P)
+    check_ranks(gs, texts[2], P)

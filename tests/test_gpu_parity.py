@@ -101,6 +101,42 @@ def test_explicit_start_list():
     assert t.contigs_text().splitlines() == want.splitlines()[::-1]
 
 
+def merging_walks(k, L, seed, every=1):
+    """Malformed input whose start walks overlap: one chain C_0..C_{L-1} plus, at every `every`-th
+    position j, three extra start k-mers x + C_{j-1}[1:] (bwd 'F') whose next_kmer is C_j. Every
+    start walks the shared tail again (kmer_hash.cpp:41-53 does not care), so the text is ~3L^2/2
+    bases, far past the table-start bound n + (K+1)·starts that kh_assemble_dev sizes first."""
+    rng = np.random.default_rng(seed)
+    B = "ACGT"
+    seq = "".join(B[x] for x in rng.integers(0, 4, L + k - 1))
+    lines = []
+    for i in range(L):
+        lines.append((seq[i:i + k], "F" if i == 0 else seq[i - 1], "F" if i == L - 1 else seq[i + k]))
+    seen = {x[0] for x in lines}
+    for j in range(1, L, every):
+        for x in B:
+            z = x + seq[j:j + k - 1]
+            if x == seq[j - 1] or z in seen:
+                continue
+            seen.add(z)
+            lines.append((z, "F", seq[j + k - 1]))
+    order = rng.permutation(len(lines))
+    text = "".join(f"{lines[i][0]} {lines[i][1]}{lines[i][2]}\n" for i in order).encode()
+    return kh.pack_text(k, text)
+
+
+@pytest.mark.parametrize("k,L,every", [(19, 3000, 1), (51, 2000, 3)])
+def test_overlapping_walks_redo(k, L, every):
+    """Walks that overlap (malformed input) pass the pre-walk text bound and exhaust the walker
+    chunk pool: kh_assemble redoes the walk sized from the scanned total with the pool the first
+    attempt asked for, and the text equals the oracle's (each start walked on its own)."""
+    recs = merging_walks(k, L, seed=7 + k, every=every)
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0 and len(want) > 4 * len(recs)
+    _, got, got_nc = run(k, recs)
+    assert got_nc == nc and got == want
+
+
 def test_empty_table():
     t = kh.KmerHashTable(19, 0)
     assert t.assemble() == (0, 0)
