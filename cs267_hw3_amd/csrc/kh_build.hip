@@ -65,10 +65,7 @@ static uint64_t win_blocks1(uint64_t n) { return (n + (uint64_t)T1 * WIN_TILE - 
 // pass-2 blocks per bucket
 static uint64_t win_G(uint64_t n) {
     const uint64_t tiles_per_bucket = (n / NB1 + WIN_TILE - 1) / WIN_TILE + 1;
-    static const uint64_t tpb = [] {  // KH_WIN2_TPB: tiles per pass-2 block (A/B runs; default 2)
-        const char* e = getenv("KH_WIN2_TPB");
-        return (uint64_t)(e && atoi(e) > 0 ? atoi(e) : 2);
-    }();
+    constexpr uint64_t tpb = 2;  // tiles per pass-2 block (1 / 2 / 3 measured the same, round 4)
     return (tiles_per_bucket + tpb - 1) / tpb;
 }
 
@@ -385,18 +382,6 @@ __device__ __forceinline__ int lds_insert_blk(const KParams& p, const Slice<W>& 
     }
     return LDS_OUT;
 }
-
-// KH_DEBUG=build_prof: per-phase shader-clock cycles of the prefetching build (thread 0 of every
-// block, summed), printed after each build. Off: one uniform branch per phase.
-__device__ unsigned long long g_build_prof[8];
-#define BPROF(i)                                                                       \
-    do {                                                                               \
-        if (prof && threadIdx.x == 0) {                                                \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
-            atomicAdd(&g_build_prof[i], t_ - pt_);                                     \
-            pt_ = t_;                                                                  \
-        }                                                                              \
-    } while (0)
 
 // ---- chains ------------------------------------------------------------------------------------
 // After a region's keys are in LDS (lt: S slots): link every k-mer x to its successor y =
@@ -754,18 +739,18 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                                                                  unsigned long long* stats, uint32_t RC,
                                                                  const uint32_t* __restrict__ rcnt,
                                                                  uint64_t* headrec, uint32_t hcap, uint32_t smax,
-                                                                 int prof, const uint64_t* __restrict__ rbt) {
+                                                                 const uint64_t* __restrict__ rbt) {
     const KParams p = specialize<KT>(p_in);
     extern __shared__ __attribute__((aligned(16))) unsigned long long lt_[];
     uint16_t* hlist = reinterpret_cast<uint16_t*>(lt_ + (uint64_t)smax * W);
     const Slice<W> lt{lt_, smax};
     __shared__ uint32_t hcnt;
-    unsigned long long pt_ = prof ? __builtin_amdgcn_s_memtime() : 0ull;
     uint64_t a[IPT], b[IPT];
     // window of region r (m = its fill, read one region ahead as a vector load: a scalar load
     // would be waited for at the next LDS barrier, which waits on lgkmcnt)
-    // z: a per-lane zero the compiler cannot fold (prof is 0 or 1) makes the address per-lane
-    const uint32_t z = threadIdx.x & (uint32_t)(prof >> 8);
+    // z: a per-lane zero the compiler cannot fold makes the address per-lane
+    uint32_t z = 0;
+    asm volatile("" : "+v"(z));
     auto fill = [&](uint32_t r) { return r < nreg(p) ? min(rcnt[r + z], RC) : 0u; };
     auto load = [&](uint32_t r, uint32_t m, uint64_t (&x)[IPT], uint64_t (&y)[IPT]) {
         const uint64_t base = (uint64_t)(r < nreg(p) ? r : 0) * RC;
@@ -818,7 +803,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 }
             }
             lds_barrier();
-            BPROF(0);
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {  // home | rank among the keys of that home << 16
                 pos[j] = LDS_DUP;
@@ -868,7 +852,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                     }
                 }
             }
-            BPROF(1);
         } else {
         if (W == 2) {
             const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(slots + lo * 2);
@@ -887,7 +870,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             lds_barrier();
         else
             __syncthreads();
-        BPROF(0);
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             pos[j] = LDS_DUP;
@@ -908,7 +890,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             }
         }
         lds_barrier();
-        BPROF(1);
         }  // probing insert
         // The next region's window goes into a/b as soon as this region's words are consumed
         // (after the inserts, or after the links that read them), so its loads are in flight
@@ -930,7 +911,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 }
             load(r + gridDim.x, m_next, a, b);
             lds_barrier();
-            BPROF(2);
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
                 if (pos[j] < 0) continue;
@@ -945,10 +925,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                     *lt.p0(sl) = slot_clean(lt.w0(sl), p);  // no record room: no index
             }
             lds_barrier();
-            BPROF(3);
             chain_heads<W, BUILD_THREADS>(p, lt, hlist, r, true, headrec, hcap, &hcnt);
             lds_barrier();
-            BPROF(4);
         } else {
             load(r + gridDim.x, m_next, a, b);
         }
@@ -990,7 +968,6 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             }
         }
         if (!(SORT && KH_FUSE_INIT)) lds_barrier();  // fused: the next region's first barrier orders it
-        BPROF(5);
         m_cur = m_next;
     }
 }
@@ -999,14 +976,8 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
 // per CU, ~170 regions each) measured slower, 3.71 -> 4.05 ms, and 2 generations of blocks 3.93:
 // region loads vary (sd ~7 %), so dynamic block dispatch balances better than a static split.
 // Same box, C3 build: 8192 blocks 3.73-3.79, 16384 3.69, 32768 3.72, 65536 3.75 ms.
-// KH_BUILD_GRID=<blocks> overrides it (A/B runs).
-static unsigned pf_grid() {
-    if (const char* e = getenv("KH_BUILD_GRID")) {
-        const int g = atoi(e);
-        if (g > 0) return (unsigned)g;
-    }
-    return 16384u;
-}
+// Round 4, final kernel: 8192 / 16384 / 24576 / 32768 blocks 2.79-2.81 ms.
+static unsigned pf_grid() { return 16384u; }
 
 template <int W, int IPT, int KT, class... A>
 static void pf_launch(bool fresh, bool sorted, size_t lds, hipStream_t s, A... a) {
@@ -1031,41 +1002,25 @@ static void launch_build_windows(const KParams& p, const PartBuffers& B, TableVi
     const int te = table_empty ? 1 : 0;
     const uint32_t smax = (uint32_t)region_max_slots(p, t.cap);
     const uint32_t hcap = B.headrec ? B.hcap : 0u;
-    const int prof = debug_flag("build_prof") ? 1 : 0;
-    // fresh slices: sorted slice insert instead of LDS CAS probing (KH_DEBUG=probe_build: off); the
-    // word-1 array of the split layout holds the home counts, so 16-B slots only. C3 build at load
-    // 0.5: 3.63 -> 2.96 ms; at 0.85 (balanced bounds): 12.5 -> 5.0 ms
-    const bool sorted = W == 2 && Slice<W>::SPLIT && !debug_flag("probe_build");
-    if (prof) {
-        static const unsigned long long zero[8] = {0};
-        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_build_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice, s);
-    }
+    // fresh slices: sorted slice insert instead of LDS CAS probing; the word-1 array of the split
+    // layout holds the home counts, so 16-B slots only. C3 build at load 0.5: 3.63 -> 2.96 ms; at
+    // 0.85 (balanced bounds): 12.5 -> 5.0 ms
+    const bool sorted = W == 2 && Slice<W>::SPLIT;
     if (debug_flag("plain_build"))  // tests: the large-window kernel at small sizes
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
                                                          stats, RC, rcnt, B.headrec, hcap, smax, B.rbt);
     else if (RC <= 4u * BUILD_THREADS)
         with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 4, decltype(kt)::value>(table_empty, sorted, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
-                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
+                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, B.rbt); });
     else if (RC <= 6u * BUILD_THREADS)
         with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 6, decltype(kt)::value>(table_empty, sorted, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
-                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
+                                                               ctr, stats, RC, rcnt, B.headrec, hcap, smax, B.rbt); });
     else if (RC <= 12u * BUILD_THREADS)
         with_kt<W>(p.K, [&](auto kt) { pf_launch<W, 12, decltype(kt)::value>(table_empty, sorted, lds, s, p, B.buf2, t.slots, t.cap, B.buf1, ovf_cap,
-                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, prof, B.rbt); });
+                                                                ctr, stats, RC, rcnt, B.headrec, hcap, smax, B.rbt); });
     else
         k_part_build<W><<<8192, BUILD_THREADS, lds, s>>>(p, B.buf2, t.slots, t.cap, te, B.buf1, ovf_cap, ctr,
                                                          stats, RC, rcnt, B.headrec, hcap, smax, B.rbt);
-    if (prof) {
-        unsigned long long v[8];
-        (void)hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_build_prof), sizeof v, 0, hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
-        unsigned long long novf = 0;
-        (void)hipMemcpyAsync(&novf, ctr + CT_OVF2, 8, hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
-        fprintf(stderr, "build_prof (s_memtime, summed over blocks): slice-init %llu insert %llu link %llu "
-                        "heads %llu walk+rec %llu write %llu | RC %u overflow %llu\n", v[0], v[1], v[2], v[3], v[4],
-                v[5], RC, novf);
-    }
 }
 
 template <int W>
@@ -1595,11 +1550,7 @@ static hipError_t win1_rec_launch(const KParams& p, const uint8_t* recs, uint64_
     constexpr int PK = W == 2 ? 13 : 5;
     // tiles of REC_TILE records: two blocks per CU (4 waves per SIMD) for the VALU-heavy parse and
     // minimizer scan (C3: 2.49 ms at 8192-record tiles and one block per CU, 2.30 at 3584; the
-    // words pass 2 keeps 8192: 1.60 vs 1.87 ms at 3584). KH_REC_TILE=8192 for A/B runs.
-    static const bool big = [] {
-        const char* e = getenv("KH_REC_TILE");
-        return e && atoi(e) == WIN_TILE;
-    }();
+    // words pass 2 keeps 8192: 1.60 vs 1.87 ms at 3584).
     auto go = [&](auto tile_c) -> hipError_t {
         constexpr int TILE = decltype(tile_c)::value;
         constexpr size_t lds = sort_lds(TILE);
@@ -1617,7 +1568,6 @@ static hipError_t win1_rec_launch(const KParams& p, const uint8_t* recs, uint64_
             return hipSuccess;
         });
     };
-    if (big) return go(std::integral_constant<int, WIN_TILE>{});
     return go(std::integral_constant<int, REC_TILE>{});
 }
 
@@ -2035,7 +1985,7 @@ static hipError_t sample_mark(const KParams& p, uint64_t cap, uint64_t n, uint32
 
 template <int W>
 static bool rec_pass_ok(const KParams& p) {
-    return ((p.P == 13 && W == 2) || (p.P == 5 && W == 1)) && !debug_flag("p1conv");
+    return (p.P == 13 && W == 2) || (p.P == 5 && W == 1);
 }
 
 // One batch: pass 1 (records or words), pass 2, build, overflow inserts.
@@ -2055,11 +2005,11 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
     // records of a compiled shape (k=51 / k=19 packed sizes): pass 1 reads them itself, no
-    // record -> word copy (KH_DEBUG=p1conv: the convert pass + pass 1 on its words)
+    // record -> word copy (other shapes: the convert pass + pass 1 on its words)
     const bool rec_pass = REC && rec_pass_ok<W>(p);
     // empty table: a 1-in-256 sample of the batch's minimizer regions marks the hot ones before
     // pass 1, so their keys are sorted straight into their key-hash regions (no spill storm)
-    const bool sample = table_empty && !debug_flag("no_hot_sample");
+    const bool sample = table_empty;
     uint32_t* samp = (REC && sample) ? rcnt : nullptr;
     if (rec_pass && sample) {
         if ((e = sample_records<W>(p, recs, n, rcnt, s)) != hipSuccess) return e;
@@ -2116,7 +2066,7 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
     }
     if (m == 0) return hipSuccess;
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(p, total);
-    if (sample && !debug_flag("no_hot_sample")) {  // the first chunk's sample marks the hot regions
+    if (sample) {  // the first chunk's sample marks the hot regions
         const uint64_t ns = (m + 255) >> 8;
         k_sample_regions<W><<<(unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024), 256, 0, s>>>(p, words, m,
                                                                                                           B.rcnt);
@@ -2155,7 +2105,7 @@ static hipError_t part_stage_recs(const KParams& p, const uint8_t* recs, uint64_
     }
     if (m == 0) return hipSuccess;
     const uint32_t CAP1 = part_win1_cap(m), RC = part_region_cap(p, total);
-    const bool samp_on = sample && !debug_flag("no_hot_sample");
+    const bool samp_on = sample;
     if (rec_pass_ok<W>(p)) {
         if (samp_on) {
             if ((e = sample_records<W>(p, recs, m, B.rcnt, s)) != hipSuccess) return e;

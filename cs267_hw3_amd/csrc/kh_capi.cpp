@@ -108,7 +108,6 @@ struct kh_table {
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
     DevBuf headrec;                           // chain head records (region build -> walker)
-    DevBuf start_rec;                         // each walker's own head record (k_start_rec)
     DevBuf hot;                               // remapped-region bitmap (KParams::hot), HOT_WORDS words
     DevBuf rbounds;                           // balanced region bounds (KParams::rb), 2^17 + 1 words
     uint32_t hcap = 0;                        // head records per region (0 = no chains)
@@ -128,6 +127,7 @@ struct kh_table {
     bool ms_on = false;        // the current migrating walk uses splitter segments
     uint64_t ms_ns = 0, ms_nsp = 0, ms_cap2 = 0, ms_nq = 0;
     bool walk_bounded = false; // the last walk's text was sized before it ran (kh_assemble_dev)
+    bool split_forced = false; // KH_SPLIT_BITS set: the walk uses every collected splitter
     uint64_t mw_wg = 0;        // walkers of every rank (bound of a round's input / held-back messages)
     uint64_t mw_store_n = 0;   // text records in mw_store (valid when mw_store_known)
     uint64_t mw_store_bound = 0;  // upper bound of the store's records (its device count: mw_misc[2])
@@ -274,7 +274,7 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     b.hot = t->hot.as<uint32_t>();
     b.rbt = t->rbounds.as<uint64_t>();
     // chain head records: sized by the table (regions x records per region), kept across builds
-    const uint32_t hcap = kh::debug_flag("no_chains") ? 0u : kh::part_head_cap(t->kp, t->cap);
+    const uint32_t hcap = kh::part_head_cap(t->kp, t->cap);
     if (hcap) {
         // + the per-region record counts the build writes after the records (k_rec_succ reads them)
         const uint64_t recb = (uint64_t)hcap * (1ull << t->kp.rbits) * 16, cntb = (1ull << t->kp.rbits) * 4;
@@ -288,17 +288,14 @@ int ensure_part(kh_table* t, uint64_t n, kh::PartBuffers& b) {
     return KH_OK;
 }
 
-// Balanced region bounds (kh_build.hip k_bounds) above load 0.6, where equal slices overflow:
-// KH_BALANCED=1/0 forces them on/off (A/B).
-bool balanced_bounds(const kh_table* t) {
-    if (const char* e = getenv("KH_BALANCED")) return strcmp(e, "0") != 0;
-    return t->load > 0.6;
-}
+// Balanced region bounds (kh_build.hip k_bounds) above load 0.6, where equal slices overflow
+// (at load 0.5 they measured slower: C3 8.84 -> 17.5 ms).
+bool balanced_bounds(const kh_table* t) { return t->load > 0.6; }
 
 // CAS-path insert into an empty table: remap the minimizer regions the batch would overfill
 // (kh_build.hip launch_hot_prepass); later batches place keys with the same bitmap.
 int cas_hot_prepass(kh_table* t, const void* recs, const void* words, uint64_t n, uint64_t total = 0) {
-    if (t->n_inserted != 0 || kh::debug_flag("no_hot")) return KH_OK;
+    if (t->n_inserted != 0) return KH_OK;
     if (int rc = t->pb_cnt.ensure(kh::part_count_words() * 8)) return rc;
     uint32_t* rcnt = t->pb_cnt.as<uint32_t>() + kh::PART_W1_COUNTERS;
     KH_HIP(hipMemsetAsync(t->hot.p, 0, kh::HOT_WORDS * 4, t->stream));
@@ -318,7 +315,11 @@ void size_table(kh_table* t, uint64_t n_kmers) {
     int bits = 1;
     while (bits < 12 && (n_kmers >> (20 + bits)) != 0) ++bits;
     bits = bits < 4 ? 4 : bits;
-    if (const char* e = getenv("KH_SPLIT_BITS")) bits = atoi(e);
+    t->split_forced = false;
+    if (const char* e = getenv("KH_SPLIT_BITS")) {  // tests: dense, sparse or no splitters
+        bits = atoi(e);
+        t->split_forced = true;
+    }
     t->kp.split_bits = bits < 0 ? 0 : (bits > 30 ? 30 : bits);
     const double c = (double)(n_kmers ? n_kmers : 1) / t->load;
     t->cap = (uint64_t)c;
@@ -416,7 +417,7 @@ int kh_destroy(kh_table* t) {
                       &t->mw_cnt, &t->mw_list, &t->mw_carry[0], &t->mw_carry[1], &t->mw_carry_dst[0],
                       &t->mw_carry_dst[1], &t->ms_res[0], &t->ms_res[1], &t->ms_res[2], &t->ms_res[3], &t->ms_res[4],
                       &t->ms_res[5], &t->ms_pend, &t->route_spl,
-                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot, &t->rbounds, &t->start_rec};
+                      &t->pb_buf1, &t->pb_buf2, &t->pb_cnt, &t->pb_ovf, &t->headrec, &t->hot, &t->rbounds};
     if (t->side) (void)hipStreamSynchronize(t->side);  // k_rec_succ may still read the table
     for (auto* b : bufs) b->release();
     hipEvent_t evs[] = {t->ev_ins0, t->ev_ins1, t->ev_ins2, t->ev_walk0, t->ev_walk1, t->ev_mat1, t->ev_b0,
@@ -536,7 +537,7 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
     KH_HIP(hipEventRecord(t->ev_ins0, t->stream));
     // partitioned build: the start / splitter bits exist once the record pass has run, so their
     // compaction runs on the side stream, overlapped with the partition passes and the build
-    const bool overlap = part && !kh::debug_flag("no_overlap");
+    const bool overlap = part;
     hipStream_t cs = overlap ? t->side : t->stream;
     t->build_timed = part;
     if (part) {
@@ -569,12 +570,10 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
         KH_HIP(hipStreamWaitEvent(t->stream, t->ev_side, 0));
         // start / splitter counts (final after the compaction above) and the remapped-region count
         // (final after the hot mark, ev_hot) to pinned memory beside the build
-        if (!kh::debug_flag("ctr_sync")) {
-            KH_HIP(hipStreamWaitEvent(t->side, t->ev_hot, 0));
-            KH_HIP(hipMemcpyAsync(t->hctr, t->ctr.p, kh::CT_NUM * 8, hipMemcpyDeviceToHost, t->side));
-            KH_HIP(hipEventRecord(t->ev_ctr, t->side));
-            t->ctr_early = true;
-        }
+        KH_HIP(hipStreamWaitEvent(t->side, t->ev_hot, 0));
+        KH_HIP(hipMemcpyAsync(t->hctr, t->ctr.p, kh::CT_NUM * 8, hipMemcpyDeviceToHost, t->side));
+        KH_HIP(hipEventRecord(t->ev_ctr, t->side));
+        t->ctr_early = true;
     }
     KH_HIP(hipEventRecord(t->ev_ins2, t->stream));
     t->ins_timed = true;
@@ -591,8 +590,7 @@ int kh_insert_dev(kh_table* t, const void* dev_recs, uint64_t n) {
 static int insert_chunked_upload(kh_table* t, const uint8_t* host_recs, uint64_t n) {
     const uint64_t R = (uint64_t)t->kp.R, W = (uint64_t)t->kp.W;
     // chunks of a multiple of 8192 records (the convert pass's tiles; start-mask words stay whole)
-    const char* ce = getenv("KH_UPLOAD_CHUNKS");
-    uint64_t nch = ce && atoi(ce) > 0 ? (uint64_t)atoi(ce) : 16;
+    uint64_t nch = 16;
     uint64_t chunk = ((n + nch - 1) / nch + 8191) & ~8191ull;
     nch = (n + chunk - 1) / chunk;
     int rc;
@@ -668,7 +666,7 @@ int kh_insert(kh_table* t, const uint8_t* host_recs, uint64_t n) {
     if (t->n_inserted + n > t->n_kmers)
         return fail(KH_ERR_FULL, "inserting %llu k-mers into a table created for %llu (%llu in)",
                     (unsigned long long)n, (unsigned long long)t->n_kmers, (unsigned long long)t->n_inserted);
-    if (t->n_inserted == 0 && n >= (1ull << 24) && use_part_build(t, n) && !kh::debug_flag("whole_upload"))
+    if (t->n_inserted == 0 && n >= (1ull << 24) && use_part_build(t, n))
         return insert_chunked_upload(t, host_recs, n);
     const uint64_t bytes = n * (uint64_t)t->kp.R;
     if (int rc = t->stage.ensure(bytes)) return rc;
@@ -757,7 +755,7 @@ int kh_assemble_dev(kh_table* t) {
     // longest segment bounds the walk: C5 with 10^6-k-mer chains took 64 ms at 1 per 4096, with
     // geometric segment lengths up to ~10x their mean; C3 pays +0.2 ms for the extra segments).
     const uint64_t* splits = t->splits.as<uint64_t>();
-    if (kp.split_bits && !getenv("KH_SPLIT_BITS")) {
+    if (kp.split_bits && !t->split_forced) {
         const uint64_t want = ns < (1ull << 20) ? (1ull << 20) - ns : 0;
         const uint64_t floor_cnt = t->n_inserted >> 8;
         const uint64_t d = want > floor_cnt ? want : floor_cnt;
@@ -798,14 +796,6 @@ int kh_assemble_dev(kh_table* t) {
     wb.max_steps = n;
     wb.headrec = t->headrec.as<uint64_t>();
     wb.hcap = t->headrec.p ? t->hcap : 0u;
-    // the walkers' own head records found before the walk (k_start_rec): opt-in, KH_DEBUG=start_rec.
-    // With successor records and three walker blocks per CU the walker's own first lookup is
-    // cheaper than the extra pass (C3 8.84 -> 8.81 ms, load 0.85 11.88 -> 11.72, C5 15.92 -> 15.15)
-    if (wb.hcap && kp.chain && kh::debug_flag("start_rec") &&
-        (uint64_t)wb.hcap * (1ull << kp.rbits) < 0xFFFFFFFFull) {
-        if ((rc = t->start_rec.ensure((nseg + 1) * 4))) return rc;
-        wb.start_rec = t->start_rec.as<uint32_t>();
-    }
     kh::SegBuffers sb{};
     if (kp.split_bits) {
         // walkers may stop before a splitter k-mer even when none was collected (then the link
@@ -846,7 +836,7 @@ int kh_assemble_dev(kh_table* t) {
     // starts on one contig, make the text longer than the k-mer count) the text is sized from the
     // scanned total, and if overlapping walks exhaust the chunk pool the walk is redone once with
     // the pool the first attempt asked for.
-    const bool bounded = !t->starts_explicit && !t->text_sync && !kh::debug_flag("text_sync");
+    const bool bounded = !t->starts_explicit && !t->text_sync;
     t->text_sync = false;
     t->walk_bounded = bounded;
     if (bounded) {
@@ -860,15 +850,14 @@ int kh_assemble_dev(kh_table* t) {
         // resolved still says 0 (the walker probes, as without), so the resolve runs on the side
         // stream beside the walk (request-bound beside a latency-bound walker); the table stream
         // waits for it after the walk (the next build rewrites the records).
-        if (attempt == 0 && wb.start_rec) KH_HIP(kh::launch_start_rec(kp, view(t), wb, t->stream));
         bool succ_side = false;
-        if (attempt == 0 && wb.hcap && !kh::debug_flag("no_rec_succ") && kh::rec_succ_fits(kp, wb.hcap)) {
-            const char* ce = getenv("KH_SUCC_CONC");  // 0: before the walk on the table stream
-            const char* be = getenv("KH_SUCC_BLOCKS");
-            const bool conc = (!ce || atoi(ce) != 0) && kh::rec_succ_side(kp);
-            // beside the walk: 1024 blocks (C3 walk + resolve 1.28 ms; the full 8192-block grid
-            // 1.32-1.34, 256 blocks 1.85: the resolve then lags the walkers; no resolve 1.46)
-            const unsigned blocks = be ? (unsigned)atoi(be) : (conc ? 1024u : 0u);
+        if (attempt == 0 && wb.hcap && kh::rec_succ_fits(kp, wb.hcap)) {
+            // beside the walk where a torn read is harmless (rec_succ_side: k > 40 at 16-B slots),
+            // else before it on the table stream; beside the walk 1024 blocks (C3 walk + resolve
+            // 1.28 ms; the full 8192-block grid 1.32-1.34, 256 blocks 1.85: the resolve then lags
+            // the walkers; no resolve 1.46)
+            const bool conc = kh::rec_succ_side(kp);
+            const unsigned blocks = conc ? 1024u : 0u;
             hipStream_t rs = t->stream;
             if (conc && t->side) {
                 KH_HIP(hipEventRecord(t->ev_side, t->stream));
@@ -1130,11 +1119,8 @@ int kh_route_dev(kh_table* t, const void* dev_recs, uint64_t n, int nranks, void
     return KH_OK;
 }
 
-// Splitter segments for the migrating walk (KH_MW_SEGMENTS=0 turns them off).
-static bool mseg_enabled(const kh_table* t) {
-    const char* e = getenv("KH_MW_SEGMENTS");
-    return t->kp.split_bits > 0 && !(e && !strcmp(e, "0"));
-}
+// Splitter segments for the migrating walk (on with the table's splitters, KH_SPLIT_BITS=0 off).
+static bool mseg_enabled(const kh_table* t) { return t->kp.split_bits > 0; }
 
 // Splitter density of the migrating walk: the table's (1 per 256 k-mers at C3 sizes). Measured
 // at one rank (C3 / C5 ms per step): segments off 15.4 / 2159, table density 17.8 / 36.5, 4x
@@ -1451,13 +1437,13 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     // chain records: every walker whose k-mer heads a record starts from it (k_mw_init), and the
     // records' successor runs are resolved beside the first round (k_rec_succ, as on one GPU)
     kh::KParams ikp = t->kp;
-    const uint32_t hcap = (t->headrec.p && t->kp.chain && !kh::debug_flag("no_start_rec") &&
+    const uint32_t hcap = (t->headrec.p && t->kp.chain &&
                            (uint64_t)t->hcap * (1ull << t->kp.rbits) < 0xFFFFFFFFull)
                               ? t->hcap
                               : 0u;
     KH_HIP(kh::launch_mw_init(ikp, view(t), hcap, t->starts.as<uint64_t>(), ns, (uint32_t)rank,
                               t->mw_init.as<uint64_t>(), t->stream));
-    if (t->headrec.p && t->hcap && !kh::debug_flag("no_rec_succ") && kh::rec_succ_fits(ikp, t->hcap)) {
+    if (t->headrec.p && t->hcap && kh::rec_succ_fits(ikp, t->hcap)) {
         hipStream_t rs = t->stream;
         if (kh::rec_succ_side(ikp) && t->side) {
             KH_HIP(hipEventRecord(t->ev_side, t->stream));

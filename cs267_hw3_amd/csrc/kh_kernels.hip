@@ -401,12 +401,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                         nrec = 0;
                         active = true;
                         entry = chains;
-                        const uint32_t sr = chains && wb.start_rec ? wb.start_rec[cc] : 0u;
-                        if (sr) {  // its own record, found before the walk (k_start_rec)
-                            s = WQ_REC | (uint64_t)(sr - 1);
-                            resolved = false;
-                            entry = false;
-                        } else if (chains) {
+                        if (chains) {
                             lookup();  // its own slot tells whether a record covers its run
                         } else {
                             resolved = true;
@@ -579,49 +574,6 @@ __global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t
     }
 }
 
-// Each walker's own head record (the walker would look its k-mer up first): index + 1 when the
-// k-mer's slot carries one and the record's run begins with the walker's own extension (the
-// walker's rule for a start, kmer_hash.cpp:42-44), else 0.
-template <int W, int KT>
-__global__ __launch_bounds__(BLOCK) void k_start_rec(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
-                                                     WalkBuffers wb) {
-    const KParams p = specialize<KT>(p_in);
-    const uint64_t n = wb.n_starts + walk_splits(wb);
-    for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < n; c += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t* src = c < wb.n_starts ? wb.starts + c * W : wb.splits + (c - wb.n_starts) * W;
-        const uint64_t x0 = src[0], x1 = (W == 2) ? src[1] : 0;
-        const Key k = slot_key(x0, x1, p);
-        const Place pl = place(k, p);
-        uint64_t sl = home_of(pl, cap, p);
-        const uint64_t want0 = (W == 1) ? k.lo : k.hi;
-        uint32_t out = 0;
-        for (uint64_t probes = 0; probes < cap; ++probes) {
-            uint64_t w0, w1;
-            load_slot<W>(slots, sl, w0, w1);
-            if (w0 == EMPTY) break;
-            if (slot_keybits(w0, p) == want0 && (W == 1 || w1 == k.lo)) {
-                const uint32_t hidx = slot_hidx(w0, p);
-                if (hidx && ext_fwd(slot_ext(w0)) == ext_fwd(slot_ext(x0)))
-                    out = (uint32_t)((uint64_t)pl.r * wb.hcap + hidx);
-                break;
-            }
-            sl = (sl + 1 == cap) ? 0 : sl + 1;
-        }
-        wb.start_rec[c] = out;
-    }
-}
-
-hipError_t launch_start_rec(const KParams& p, TableView t, const WalkBuffers& wb, hipStream_t s) {
-    const uint64_t nw = wb.n_starts + wb.n_splits;
-    if (!nw || !wb.start_rec || !wb.hcap) return hipSuccess;
-    const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK, 8192);
-    if (p.W == 1)
-        with_kt<1>(p.K, [&](auto kt) { k_start_rec<1, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb); });
-    else
-        with_kt<2>(p.K, [&](auto kt) { k_start_rec<2, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb); });
-    return hipGetLastError();
-}
-
 bool rec_succ_fits(const KParams& p, uint32_t hcap) {
     return p.chain && hcap && rec_succ_shift(p) < 64 && (uint64_t)hcap + 1 < (1ull << (64 - rec_succ_shift(p)));
 }
@@ -652,11 +604,7 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     // grid_blocks <= 0: -grid_blocks blocks per CU (0: two). Walker blocks per CU, C3 walk ms:
     // 1: 1.78, 2: 1.32, 3: 1.24, 4: 1.37, 5: 1.50 (load 0.5); at load 0.85 three are slower than two
     // (2.39 vs 2.27: longer probe runs, more requests in flight contend); C2 (k=19) 0.37 vs 0.35
-    static const int bpc_env = [] {  // KH_WALK_BPC: override (A/B runs)
-        const char* e = getenv("KH_WALK_BPC");
-        return e && atoi(e) > 0 ? atoi(e) : 0;
-    }();
-    const int bpc = bpc_env ? bpc_env : (grid_blocks < 0 ? -grid_blocks : 2);
+    const int bpc = grid_blocks < 0 ? -grid_blocks : 2;
     const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
                                          (uint64_t)(grid_blocks > 0 ? grid_blocks : bpc * cu_count()));
     if (p.W == 1)

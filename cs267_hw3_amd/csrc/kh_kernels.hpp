@@ -88,9 +88,6 @@ struct WalkBuffers {
     // chain head records of the last region build (kh_build.hip region_chains); hcap 0 = none
     const uint64_t* headrec = nullptr;
     uint32_t hcap = 0;
-    // per walker (start, then walked splitter): its own head record's global index + 1, 0 = look
-    // the k-mer up (k_start_rec; null = every walker looks its k-mer up)
-    uint32_t* start_rec = nullptr;
     // bytes of the text buffer the materialisation writes into (0: sized from the scanned total);
     // a contig that would pass it is not written (the caller compares the total with it)
     uint64_t text_cap = 0;
@@ -106,8 +103,6 @@ hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uin
 // grid_blocks > 0: that many blocks; <= 0: -grid_blocks blocks per CU (0: two)
 hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, unsigned long long* ctr,
                        unsigned long long* stats, int grid_blocks, hipStream_t s);
-// the walkers' own head records (wb.start_rec), before the walk
-hipError_t launch_start_rec(const KParams& p, TableView t, const WalkBuffers& wb, hipStream_t s);
 
 static constexpr uint32_t SEG_NONE = 0xFFFFFFFFu, SEG_AT_SPLIT = 0xFFFFFFFEu;
 

@@ -415,11 +415,7 @@ hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, un
                          hipStream_t s) {
     if (mw.n_in == 0) return hipSuccess;
     // ~4 inputs per lane keeps lanes busy through the run-length tail without a work queue
-    // (KH_MW_IPL: inputs per lane, A/B runs)
-    static const uint64_t ipl = [] {
-        const char* e = getenv("KH_MW_IPL");
-        return (uint64_t)(e && atoi(e) > 0 ? atoi(e) : 4);
-    }();
+    constexpr uint64_t ipl = 4;
     const unsigned g = grid_for((mw.n_in + ipl - 1) / ipl, 4096);
     if (p.W == 1)
         with_kt<1>(p.K, [&](auto kt) { k_mw_run<1, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats); });

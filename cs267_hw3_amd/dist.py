@@ -420,10 +420,11 @@ class DistributedKmerHashMap:
     # >= 2 GiB - 8 B (tools/rccl_big_msg.cpp and .py; profiles/r04/rccl_big_msg: RCCL 2.27.7 and
     # torch's 2.26.6, equal and split all_to_all and grouped send/recv alike; exact at 1 GiB), so
     # no single call moves more than A2A_CHUNK_BYTES per peer.
-    A2A_CHUNK_BYTES = int(os.environ.get("KH_A2A_CHUNK_MB", "512")) << 20
-    # one rank: exchanges are skipped (KH_DIST_SELF_EXCHANGE=1 runs them anyway, for tests), and the
-    # records go straight into the records pass (KH_DIST_ROUTE_ONE_RANK=1 routes them anyway)
-    SELF_EXCHANGE = os.environ.get("KH_DIST_SELF_EXCHANGE") == "1"
+    A2A_CHUNK_BYTES = 512 << 20
+    # one rank: exchanges are skipped (KH_DIST_SELF_EXCHANGE=1 runs them anyway, for tests;
+    # =pipelined also in chunks at any size), and the records go straight into the records pass
+    # (KH_DIST_ROUTE_ONE_RANK=1 routes them anyway)
+    SELF_EXCHANGE = os.environ.get("KH_DIST_SELF_EXCHANGE", "0") in ("1", "pipelined")
     ROUTE_ONE_RANK = os.environ.get("KH_DIST_ROUTE_ONE_RANK") == "1"
 
     def _exchange_counts(self, counts, extra=None):
@@ -496,10 +497,11 @@ class DistributedKmerHashMap:
                     pos += rc[q]
 
     # pipelined insert: chunk c-1, received, is partitioned while chunk c is on the wire
-    # (KH_INSERT_CHUNKS=1: one transfer)
-    INSERT_CHUNKS = int(os.environ.get("KH_INSERT_CHUNKS", "4"))
-    ROUTE_WINDOW_BYTES = int(os.environ.get("KH_ROUTE_WINDOW_GB", "64")) << 30
-    PIPELINE_MIN = int(os.environ.get("KH_PIPELINE_MIN", 1 << 22))  # records per rank below which one chunk
+    # (tests set INSERT_CHUNKS / PIPELINE_MIN on the instance)
+    INSERT_CHUNKS = 4
+    ROUTE_WINDOW_BYTES = 64 << 30
+    # records per rank below which one chunk
+    PIPELINE_MIN = 0 if os.environ.get("KH_DIST_SELF_EXCHANGE") == "pipelined" else 1 << 22
 
     def _exchange_count_matrix(self, counts, spl, mine):
         """counts: list over chunks of [P+1] int64 device tensors (per-destination, total); spl:
@@ -653,7 +655,7 @@ class DistributedKmerHashMap:
             c = max(1024, (self._walkers + P * P - 1) // (P * P) * 5 // 4 + 1024) if P > 1 else self._walkers + 16
         return max(1, min(max(c, self._cap_floor), self.SLOT_CAP_MAX))
 
-    SLOT_CAP_MAX = int(os.environ.get("KH_MW_SLOT_CAP", str(1 << 40)))  # tests: tiny slots (messages held back)
+    SLOT_CAP_MAX = 1 << 40  # tests: tiny slots (messages held back), set on the class
 
     def _assemble_migrate(self, total_kmers):
         """Walkers move to the rank owning their next k-mer (minimizer sharding keeps runs of
@@ -749,7 +751,7 @@ class DistributedKmerHashMap:
         sh.sync()  # the library counts this one (kh_sync)
         return self.rounds
 
-    CHECK_EVERY = int(os.environ.get("KH_MW_CHECK_EVERY", "4"))
+    CHECK_EVERY = 4
     MAX_ROUNDS = 4096  # with splitter segments (the default) C5's 10^6-k-mer chains take ~11
 
     def _segments_end(self, trecv, r, nseg):
@@ -914,22 +916,11 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
     dm = DistributedKmerHashMap(comm, shard)
     R = record_size(k)
 
-    phase_log = os.environ.get("KH_BENCH_PHASES") == "1"
-
     def step():
         with torch.cuda.stream(shard.stream):
             shard.clear()
-            t0 = time.perf_counter()
             dm.insert_all(recs)
-            if phase_log:
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
             dm.assemble(n_total)
-            if phase_log:
-                torch.cuda.synchronize()
-                print(f"[rank {rank}] insert {1e3 * (t1 - t0):.2f} ms, assemble "
-                      f"{1e3 * (time.perf_counter() - t1):.2f} ms, rounds {dm.rounds}", file=sys.stderr,
-                      flush=True)
 
     for _ in range(args.warmup):
         step()

@@ -191,7 +191,7 @@ int kh_mwalk_text_bound(kh_table* t, uint64_t* n_records); /* text_dev writes at
 int kh_mwalk_text_dev(kh_table* t, void* dev_out, void* dev_counts_out);
 int kh_mwalk_end_dev(kh_table* t, const void* dev_recs, uint64_t n);
 /* Splitter segments of the migrating walk (kh_mseg.hip; on when the shard collects splitters,
- * KH_MW_SEGMENTS=0 turns them off). kh_mwalk_begin then also seeds a walker at every splitter
+ * KH_SPLIT_BITS=0 turns them off). kh_mwalk_begin then also seeds a walker at every splitter
  * k-mer this shard owns (n_walkers includes them) and walkers stop before splitters. When
  * kh_mwalk_segments reports > 0 on any rank, after the text records have come home the end of the
  * walk is, instead of kh_mwalk_end_dev:

@@ -175,7 +175,8 @@ int ko_assemble(int K, const uint8_t* recs, size_t n, char** out, size_t* out_le
         if (recs[i * (size_t)R + P] == 'F') starts[ns++] = i; /* kmer_hash.cpp:27-31 */
     }
     double t1 = now_s();
-    /* upper bound of the output: every k-mer contributes <= 1 char, every contig K + '\n' */
+    /* the output when walks are disjoint (every k-mer contributes <= 1 char, every contig K +
+       '\n'); walks that overlap (malformed input) grow it */
     size_t cap = n + ns * ((size_t)K + 1) + 1;
     char* o = (char*)malloc(cap);
     if (!o) {
@@ -187,11 +188,23 @@ int ko_assemble(int K, const uint8_t* recs, size_t n, char** out, size_t* out_le
     uint8_t cur[32], nxt[32];
     int rc = 0;
     for (size_t s = 0; s < ns && rc == 0; ++s) {
+        if (pos + (size_t)K + 2 >= cap) {
+            char* g = (char*)realloc(o, 2 * cap + (size_t)K + 2);
+            if (!g) { rc = -4; break; }
+            o = g;
+            cap = 2 * cap + (size_t)K + 2;
+        }
         memcpy(cur, recs + starts[s] * (size_t)R, (size_t)R);
         ko_unpack(K, cur, o + pos); /* extract_contig: front().kmer_str() */
         pos += (size_t)K;
         size_t steps = 0;
         while (cur[P + 1] != 'F') { /* kmer_hash.cpp:44 */
+            if (pos + 2 >= cap) { /* overlapping walks: grow */
+                char* g = (char*)realloc(o, 2 * cap);
+                if (!g) { rc = -4; break; }
+                o = g;
+                cap *= 2;
+            }
             o[pos++] = (char)cur[P + 1]; /* extract_contig: every non-F forward ext */
             ko_next_kmer(K, cur, nxt);
             if (!ko_table_find(t, nxt, cur)) { rc = -1; break; } /* kmer_hash.cpp:47-49 */

@@ -51,9 +51,7 @@ def test_dist_launcher_one_rank(tmp_path, mode):
     import sys
     env = dict(os.environ, PYTHONPATH=ROOT)
     if mode != "plain":
-        env["KH_DIST_SELF_EXCHANGE"] = "1"
-    if mode == "self_exchange_pipelined":
-        env["KH_PIPELINE_MIN"] = "0"
+        env["KH_DIST_SELF_EXCHANGE"] = "pipelined" if mode == "self_exchange_pipelined" else "1"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
                         "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port",
                         "29533", "-m", "cs267_hw3_amd.kmer_hash_dist",
