@@ -49,6 +49,12 @@ WORKLOADS = {
                 gen=dict(hot_permille=300, n_motifs=8),
                 desc="C5 hot-bucket: k=51, 200M synthetic k-mers per GPU, contigs U[8,200], 30% of "
                      "them built around one of 8 shared minimizer motifs"),
+    # the hot-bucket half's worst case for the remap: a fixed flank before every motif (the
+    # families share the minimizer's neighbour window too: a 32-base repeat)
+    "c5f": dict(k=51, n=200_000_000, len_min=8, len_max=200, single=0, seed=5197,
+                gen=dict(hot_permille=300, n_motifs=8, hot_flank=True),
+                desc="C5 hot-bucket, flank: as c5h, every motif preceded by a fixed 16-mer (families "
+                     "share the minimizer and its neighbour window)"),
 }
 RANDOM_REQ_CEILING = 49e9
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
@@ -363,7 +369,8 @@ def main():
         "vs_baseline": value / BEST_PUBLISHED_OPS, "dtype": "u64", "data": "synthetic",
         "config": {"workload": w["desc"], "k": k, "n_kmers_per_gpu": n, "contigs": nc,
                    "lookups": nl, "parallelism": "1 GPU", "load_factor": args.load,
-                   "hot_regions": s["n_hot_regions"], "overflow_cas_keys": s["n_overflow"],
+                   "hot_regions": s["n_hot_regions"], "spread_regions": s["n_spread_regions"],
+                   "overflow_cas_keys": s["n_overflow"],
                    "vs_baseline_ref": "72.6e6 ops/s: reference best, k=51 human-chr14, "
                                       "4 nodes x 128 CPU ranks (BASELINE.md)"},
         "inserts_per_s": n / (ms / 1e3), "lookups_per_s": nl / (ms / 1e3),

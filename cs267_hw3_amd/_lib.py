@@ -34,7 +34,7 @@ class KhStats(ctypes.Structure):
         (name, ctypes.c_double) for name in (
             "ms_insert", "ms_insert_kernel", "ms_walk", "ms_materialize")] + [("n_bad_base", c_u64)] + \
             [(f, ctypes.c_double) for f in ("ms_build", "ms_walk_kernel")] + \
-            [(f, c_u64) for f in ("n_hot_regions", "n_overflow")]
+            [(f, c_u64) for f in ("n_hot_regions", "n_overflow", "n_spread_regions")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -122,6 +122,10 @@ _SIGS = {
                                          ctypes.c_uint32, ctypes.c_uint32, c_u64, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                          ctypes.c_uint32, ctypes.c_uint32]),
+    "kh_gen_create_hot_ex": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_int, c_u64, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, c_u64, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "kh_gen_destroy": (ctypes.c_int, [c_vp]),
     "kh_gen_num_contigs": (c_u64, [c_vp]),
     "kh_gen_records": (ctypes.c_int, [c_vp, c_u64, c_u64, c_vp]),

@@ -140,7 +140,7 @@ bool part_usable(const KParams& p, uint64_t cap, uint64_t n) {
 // that one is remapped (hot_on: the table has remapped regions; one uniform test per block).
 __device__ __forceinline__ uint32_t part_region(uint32_t win, Key k, const KParams& p, bool hot_on, int js = -1) {
     const uint32_t r = mini_region(win, p);
-    return (hot_on && region_is_hot(p.hot, r)) ? hot_region(k, win, p, js) : r;
+    return (hot_on && region_is_hot(p.hot, r)) ? remap_region(k, win, p, js) : r;
 }
 
 // ---- record -> word conversion (k other than 51 / 19) ---------------------------------------------
@@ -1727,7 +1727,8 @@ static uint32_t balanced_T(const KParams& p, uint64_t cap, uint64_t n) {
 template <int Unused = 0>
 __global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint32_t RC, int slack16, int sample_shift,
                                                   const uint32_t* counts, uint32_t* hot, uint32_t* hot_list,
-                                                  unsigned long long* ctr, int allow_new, int list_new, uint32_t Tfix) {
+                                                  unsigned long long* ctr, int allow_new, int list_new, uint32_t Tfix,
+                                                  int ct = CT_HOT) {
     const uint32_t NR = nreg(p);
     const uint32_t r = blockIdx.x * 256u + threadIdx.x;
     bool h = false, hn = false;
@@ -1747,7 +1748,7 @@ __global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint3
     const uint32_t lane = lane_id();
     const uint32_t r0 = r - lane;  // the wave's 64 regions: two bitmap words
     if (r0 < NR && (lane == 0 || lane == 32)) hot[(r0 >> 5) + (lane >> 5)] = (uint32_t)(m >> lane);
-    if (lane == 0 && m) atomicAdd(&ctr[CT_HOT], (unsigned long long)__popcll(m));
+    if (lane == 0 && m) atomicAdd(&ctr[ct], (unsigned long long)__popcll(m));
     const unsigned long long i = wave_reserve(&ctr[CT_HOTNEW], list_new && hn);
     if (list_new && hn) hot_list[i] = r;
 }
@@ -1942,10 +1943,12 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
     q.hot = hot;
     int shift = 0;
     while (n && total > n && ((uint64_t)n << (shift + 1)) <= total) ++shift;
+    const uint32_t Tb = balanced_T(p, cap, total > n ? total : n);
     k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, 0xFFFFFFFFu, shift ? 0 : 1, shift, rcnt, hot, hot_list,
-                                                     ctr, 1, 0, balanced_T(p, cap, total > n ? total : n));
-    if (p.rb) {  // balanced bounds from the counts after the remap (a second, hot-aware count)
-        if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
+                                                     ctr, 1, 0, Tb);
+    auto count_placed = [&]() -> hipError_t {  // the region each key goes to under the bitmap so far
+        hipError_t x;
+        if ((x = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return x;
         if (n) {
             const unsigned grid = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
             if (p.W == 2) {
@@ -1956,6 +1959,15 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
                 else k_region_count<1, false><<<grid, 256, 0, s>>>(q, nullptr, words, n, rcnt, 1);
             }
         }
+        return hipGetLastError();
+    };
+    // level 2: target regions the remap overfills (kh_codec.hpp remap_region)
+    if ((e = count_placed()) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(ctr + CT_HOT2, 0, 8, s)) != hipSuccess) return e;
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, 0xFFFFFFFFu, shift ? 0 : 1, shift, rcnt, hot + HOT_WORDS,
+                                                     hot_list, ctr, 1, 0, Tb, CT_HOT2);
+    if (p.rb) {  // balanced bounds from the counts after the remap (a hot-aware count)
+        if ((e = count_placed()) != hipSuccess) return e;
         launch_bounds(p, cap, rcnt, 0xFFFFFFFFu, const_cast<uint64_t*>(p.rb), s);
     }
     return hipGetLastError();
@@ -1980,6 +1992,60 @@ static hipError_t sample_mark(const KParams& p, uint64_t cap, uint64_t n, uint32
     if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 16, s)) != hipSuccess) return e;  // CT_HOT, CT_HOTNEW
     k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot, B.hot_list, ctr, 1, 0,
                                                      balanced_T(p, cap, n));
+    return hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s);
+}
+
+// Level 2 of the bitmap (kh_codec.hpp remap_region): a 1-in-256 sample of the batch counted by its
+// placement under level 1 marks the target regions the remap overfills (a family whose copies also
+// share the neighbour window lands in one), so their remapped keys spread by key hash before pass 1
+// instead of piling into one window and the global CAS list (quadratic probe runs in the worst
+// case). Same sampled threshold as level 1. Returns at once when level 1 marked nothing.
+template <int W, bool REC, int KT>
+__global__ __launch_bounds__(256) void k_sample_placed(KParams p_in, const uint8_t* __restrict__ recs,
+                                                       const uint64_t* __restrict__ words, uint64_t n, uint32_t* counts,
+                                                       const unsigned long long* ctr) {
+    if (!ctr[CT_HOT]) return;
+    const KParams p = specialize<KT>(p_in);
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) << 8; i < n; i += ((uint64_t)gridDim.x * 256) << 8) {
+        uint32_t r;
+        if (REC) {
+            uint64_t x0, x1;
+            load_record_regs(recs, i, (uint32_t)p.R, x0, x1);
+            Key k;
+            uint32_t ext;
+            parse_record_regs(x0, x1, p, k, ext);
+            const uint32_t mn = mini_scan(k, p);
+            r = place_w(mini_window(k, mn, p), k, p, (int)(mn & 63u)).r;
+        } else {
+            r = word_place(words[i * W], W == 2 ? words[i * W + 1] : 0ull, p).r;
+        }
+        (void)wave_count_add(counts, r, true);
+    }
+}
+
+// recs (records) or words (partition words carrying j*) of a batch of n, scaled to a build of
+// RC-word windows; counts: zeroed region counters (left zeroed)
+template <int W>
+static hipError_t sample_level2(const KParams& p, const uint8_t* recs, const uint64_t* words, uint64_t n,
+                                uint64_t cap, uint32_t RC, uint64_t total, const PartBuffers& B,
+                                unsigned long long* ctr, hipStream_t s) {
+    KParams q = p;
+    q.hot = B.hot;
+    const uint64_t ns = (n + 255) >> 8;
+    const unsigned nb = (unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024);
+    hipError_t e;
+    if ((e = with_kt<W>(p.K, [&](auto kt) {
+             constexpr int KT = decltype(kt)::value;
+             if (recs)
+                 k_sample_placed<W, true, KT><<<nb, 256, 0, s>>>(q, recs, nullptr, n, B.rcnt, ctr);
+             else
+                 k_sample_placed<W, false, KT><<<nb, 256, 0, s>>>(q, nullptr, words, n, B.rcnt, ctr);
+             return hipGetLastError();
+         })) != hipSuccess)
+        return e;
+    if ((e = hipMemsetAsync(ctr + CT_HOT2, 0, 8, s)) != hipSuccess) return e;
+    k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot + HOT_WORDS, B.hot_list, ctr, 1, 0,
+                                                     balanced_T(p, cap, total), CT_HOT2);
     return hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s);
 }
 
@@ -2014,6 +2080,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     if (rec_pass && sample) {
         if ((e = sample_records<W>(p, recs, n, rcnt, s)) != hipSuccess) return e;
         if ((e = sample_mark(p, t.cap, n, RC, B, ctr, s)) != hipSuccess) return e;
+        if ((e = sample_level2<W>(p, recs, nullptr, n, t.cap, RC, n, B, ctr, s)) != hipSuccess) return e;
     }
     if (!REC && sample) {
         const uint64_t ns = (n + 255) >> 8;
@@ -2040,6 +2107,7 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
             words = B.buf2;
         }
         if (sample && (e = sample_mark(p, t.cap, n, RC, B, ctr, s)) != hipSuccess) return e;
+        if (sample && (e = sample_level2<W>(p, nullptr, words, n, t.cap, RC, n, B, ctr, s)) != hipSuccess) return e;
         // converted records and routed words (k_route_scatter) both carry j* and the order bits
         if ((e = win1_launch<W>(p, words, n, CAP1, wcnt, B, ovf_cap, ctr, stats, s, REC ? nullptr : wsplits,
                                 wsplits_cap, true)) != hipSuccess)
@@ -2071,7 +2139,9 @@ static hipError_t part_stage(const KParams& p, const uint64_t* words, uint64_t m
         k_sample_regions<W><<<(unsigned)((ns + 255) / 256 < 1024 ? (ns + 255) / 256 : 1024), 256, 0, s>>>(p, words, m,
                                                                                                           B.rcnt);
         // the sample covers this chunk: scale it to the whole build (chunks are alike)
-        if ((e = sample_mark(p, cap, m, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess) return e;
+        const uint32_t RCm = (uint32_t)((uint64_t)RC * m / total);
+        if ((e = sample_mark(p, cap, m, RCm, B, ctr, s)) != hipSuccess) return e;
+        if ((e = sample_level2<W>(p, nullptr, words, m, cap, RCm, m, B, ctr, s)) != hipSuccess) return e;
     }
     if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = win1_launch<W>(p, words, m, CAP1, B.wcnt, B, part_overflow_cap(total), ctr, stats, s, wsplits,
@@ -2108,8 +2178,10 @@ static hipError_t part_stage_recs(const KParams& p, const uint8_t* recs, uint64_
     const bool samp_on = sample;
     if (rec_pass_ok<W>(p)) {
         if (samp_on) {
+            const uint32_t RCm = (uint32_t)((uint64_t)RC * m / total);
             if ((e = sample_records<W>(p, recs, m, B.rcnt, s)) != hipSuccess) return e;
-            if ((e = sample_mark(p, cap, m, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess) return e;
+            if ((e = sample_mark(p, cap, m, RCm, B, ctr, s)) != hipSuccess) return e;
+            if ((e = sample_level2<W>(p, recs, nullptr, m, cap, RCm, m, B, ctr, s)) != hipSuccess) return e;
         }
         if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
         if ((e = win1_rec_launch<W>(p, recs, m, CAP1, B.wcnt, B, start_mask, split_mask, part_overflow_cap(total), ctr,
@@ -2132,8 +2204,11 @@ static hipError_t part_stage_recs(const KParams& p, const uint8_t* recs, uint64_
         k_part1_convert<W, 5><<<nb, PB, 0, s>>>(p, recs, m, words_tmp, start_mask, split_mask, samp);
     else
         k_part1_convert<W><<<nb, PB, 0, s>>>(p, recs, m, words_tmp, start_mask, split_mask, samp);
-    if (samp_on && (e = sample_mark(p, cap, m, (uint32_t)((uint64_t)RC * m / total), B, ctr, s)) != hipSuccess)
-        return e;
+    if (samp_on) {
+        const uint32_t RCm = (uint32_t)((uint64_t)RC * m / total);
+        if ((e = sample_mark(p, cap, m, RCm, B, ctr, s)) != hipSuccess) return e;
+        if ((e = sample_level2<W>(p, nullptr, words_tmp, m, cap, RCm, m, B, ctr, s)) != hipSuccess) return e;
+    }
     if ((e = hipMemsetAsync(B.wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
     if ((e = win1_launch<W>(p, words_tmp, m, CAP1, B.wcnt, B, part_overflow_cap(total), ctr, stats, s, nullptr, 0,
                             true)) != hipSuccess)

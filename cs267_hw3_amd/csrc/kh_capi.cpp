@@ -108,7 +108,7 @@ struct kh_table {
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
     DevBuf headrec;                           // chain head records (region build -> walker)
-    DevBuf hot;                               // remapped-region bitmap (KParams::hot), HOT_WORDS words
+    DevBuf hot;                               // remapped-region bitmap (KParams::hot), 2 levels of HOT_WORDS
     DevBuf rbounds;                           // balanced region bounds (KParams::rb), 2^17 + 1 words
     uint32_t hcap = 0;                        // head records per region (0 = no chains)
     bool last_insert_part = false;
@@ -214,7 +214,9 @@ static int stats_status(const unsigned long long* st) {
                     st[kh::ST_MISSING]);
     if (st[kh::ST_CYCLE]) return fail(KH_ERR_CYCLE, "%llu walks exceeded the table size", st[kh::ST_CYCLE]);
     if (st[kh::ST_SPIN]) return fail(KH_ERR_HIP, "%llu inserts timed out on a slot", st[kh::ST_SPIN]);
-    if (st[kh::ST_CHUNK_OVF]) return fail(KH_ERR_NOMEM, "walker chunk pool overflow");
+    if (st[kh::ST_CHUNK_OVF])
+        return fail(KH_ERR_NOMEM, "walker output overflow or overlapping walks (malformed input; kh_assemble redoes "
+                                  "such a walk unsegmented)");
     if (st[kh::ST_BAD_BASE])
         return fail(KH_ERR_BAD_BASE, "%llu k-mer lines with a base outside {A,C,G,T}", st[kh::ST_BAD_BASE]);
     return KH_OK;
@@ -298,7 +300,7 @@ int cas_hot_prepass(kh_table* t, const void* recs, const void* words, uint64_t n
     if (t->n_inserted != 0) return KH_OK;
     if (int rc = t->pb_cnt.ensure(kh::part_count_words() * 8)) return rc;
     uint32_t* rcnt = t->pb_cnt.as<uint32_t>() + kh::PART_W1_COUNTERS;
-    KH_HIP(hipMemsetAsync(t->hot.p, 0, kh::HOT_WORDS * 4, t->stream));
+    KH_HIP(hipMemsetAsync(t->hot.p, 0, 2 * kh::HOT_WORDS * 4, t->stream));
     KH_HIP(kh::launch_hot_prepass(t->kp, (const uint8_t*)recs, (const uint64_t*)words, n, t->cap, rcnt,
                                   t->hot.as<uint32_t>(), rcnt + kh::HOT_WORDS * 32, t->ctr.as<unsigned long long>(),
                                   t->stream, total));
@@ -385,7 +387,8 @@ int kh_create(kh_table** out, int k, uint64_t n_kmers, double load_factor, int d
     if (hipHostMalloc((void**)&t->hctr, kh::CT_NUM * 8, hipHostMallocDefault) != hipSuccess)
         return bail(fail(KH_ERR_NOMEM, "pinned host counters"));
     if ((rc = t->slots.ensure(t->cap * (uint64_t)t->kp.W * 8))) return bail(rc);
-    if ((rc = t->hot.ensure(kh::HOT_WORDS * 4))) return bail(rc);
+    if ((rc = t->hot.ensure(2 * kh::HOT_WORDS * 4))) return bail(rc);
+    if (hipMemset(t->hot.p, 0, 2 * kh::HOT_WORDS * 4) != hipSuccess) return bail(fail(KH_ERR_HIP, "hipMemset failed"));
     t->kp.hot = t->hot.as<uint32_t>();
     // region slot ranges: equal until a balanced table's first build (lookups read them only when
     // balanced; the build always does)
@@ -474,7 +477,7 @@ int kh_clear(kh_table* t) {
     t->slots_stale = true;
     KH_HIP(hipMemsetAsync(t->ctr.p, 0, kh::CT_NUM * 8, t->stream));
     KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
-    KH_HIP(hipMemsetAsync(t->hot.p, 0, kh::HOT_WORDS * 4, t->stream));  // placement by minimizer again
+    KH_HIP(hipMemsetAsync(t->hot.p, 0, 2 * kh::HOT_WORDS * 4, t->stream));  // placement by minimizer again
     KH_HIP(hipMemsetAsync(t->route_spl.p, 0, kh::MAX_RANKS * 8, t->stream));
     t->n_inserted = 0;
     t->assembled = false;
@@ -746,7 +749,10 @@ int kh_assemble_dev(kh_table* t) {
     const unsigned long long* nsp_dev = nullptr;
     kh::KParams kp = t->kp;
     if (!cv[kh::CT_HOT]) kp.hot = nullptr;  // no remapped region: the walker skips the bitmap load
-    if (kp.split_bits && t->split_ok)
+    // splitter segments only where walks are known disjoint (table-collected starts): a segment
+    // is written once, so walks that overlap (explicit starts, malformed input) walk unsegmented
+    const bool disjoint = !t->starts_explicit && !t->text_sync;
+    if (kp.split_bits && t->split_ok && disjoint)
         nsp = cv[kh::CT_N_SPLIT];
     else
         kp.split_bits = 0;
@@ -1018,6 +1024,7 @@ int kh_get_stats(kh_table* t, kh_stats* s) {
     }
     if (t->build_timed && hipEventElapsedTime(&ms, t->ev_b0, t->ev_b1) == hipSuccess) s->ms_build = ms;
     s->n_hot_regions = ct[kh::CT_HOT];
+    s->n_spread_regions = ct[kh::CT_HOT2];
     s->n_overflow = t->last_insert_part ? ct[kh::CT_OVF2] : 0;
     (void)hipGetLastError();  // a failed elapsed-time query is not the caller's error
     return KH_OK;

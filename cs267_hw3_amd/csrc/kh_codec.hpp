@@ -209,14 +209,7 @@ KH_HD uint64_t fmix64(uint64_t h) {
 // Placement hash (NOT the reference's djb2: djb2 over 5 bytes spans < 2^38 at K=19 and would put
 // every key of a high-bit shard split on one GPU; SURVEY §7 hard part 1). Placement never changes
 // the output, only where a key lives.
-KH_HD uint64_t key_hash(Key k) {
-#ifdef KH_CHEAP_HASH  // experiment only
-    uint64_t h = (k.lo ^ (k.hi << 17)) * 0xff51afd7ed558ccdull;
-    return h ^ (h >> 31);
-#else
-    return fmix64(k.lo ^ fmix64(k.hi ^ 0x9e3779b97f4a7c15ull));
-#endif
-}
+KH_HD uint64_t key_hash(Key k) { return fmix64(k.lo ^ fmix64(k.hi ^ 0x9e3779b97f4a7c15ull)); }
 
 KH_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -363,10 +356,22 @@ KH_HD uint32_t hot_region(Key k, uint32_t win, const KParams& p, int js = -1) {
     return mix32((win * 0x9E3779B1u) ^ second_window(k, win, p, js) ^ 0x2545F491u) >> (32 - p.rbits);
 }
 KH_HD bool region_is_hot(const uint32_t* hot, uint32_t r) { return hot && ((hot[r >> 5] >> (r & 31u)) & 1u); }
+// The bitmap has two levels of 2^17 bits (KParams::hot): level 1 marks minimizer regions whose keys
+// are remapped (hot_region); level 2 marks target regions that the remap itself overfills — a family
+// whose copies also share the neighbour window (a shared stretch of 2M bases: a repeat) lands in one
+// target region — and the remapped keys headed there go to a region of their whole key's hash
+// (evenly spread; their runs lose their chains, so the walker looks each such k-mer up). Level 2 is
+// read only for keys level 1 remapped.
+static constexpr uint32_t HOT_LEVEL_WORDS = (1u << REGION_BITS_MAX) / 32;
+KH_HD uint32_t spread_region(Key k, const KParams& p) { return (uint32_t)(key_hash(k) >> 32) >> (32 - p.rbits); }
+KH_HD uint32_t remap_region(Key k, uint32_t win, const KParams& p, int js = -1) {
+    const uint32_t t = hot_region(k, win, p, js);
+    return region_is_hot(p.hot + HOT_LEVEL_WORDS, t) ? spread_region(k, p) : t;
+}
 KH_HD Place place_w(uint32_t win, Key k, const KParams& p, int js = -1) {
     uint32_t r = mini_region(win, p);
     const uint32_t h = key_hash32(k);
-    if (region_is_hot(p.hot, r)) r = hot_region(k, win, p, js);
+    if (region_is_hot(p.hot, r)) r = remap_region(k, win, p, js);
     return Place{r, h};
 }
 KH_HD Place place(Key k, const KParams& p) {

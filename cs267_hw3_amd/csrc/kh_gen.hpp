@@ -97,8 +97,13 @@ struct GenView {
     // The motifs are the M-mers of smallest minimizer order among 2^16 seeded draws,
     // so the occurrence is (almost always) the k-mer's minimizer: all k-mers of the hot contigs
     // of motif h share one minimizer window, one placement region and one shard owner.
-    uint32_t hot_pm = 0, n_motifs = 0, period = 0, M = 0;
+    // flank mode (the worst case of the table's hot remap): a fixed per-motif M-mer
+    // flank[h] is planted right before every occurrence (pattern = flank then motif, plen = 2M, one
+    // per K bases), so the k-mers holding the whole pattern share the minimizer AND its neighbour
+    // window (kh_codec.hpp second_window): the remap alone would pile them into one region.
+    uint32_t hot_pm = 0, n_motifs = 0, period = 0, M = 0, plen = 0;
     uint32_t motif[GEN_MAX_MOTIFS] = {};
+    uint32_t flank[GEN_MAX_MOTIFS] = {};
 
     KH_HD uint64_t hot_hash(uint64_t i) const { return splitmix(seed ^ 0x3f84d5b5b5470917ull ^ (i * 0xd1b54a32d192ed03ull)); }
     // motif index of contig i, or -1 when the contig is not hot
@@ -113,11 +118,12 @@ struct GenView {
                               ((uint64_t)salt[i] << 40) ^ b);
         const int h = hot_motif(i);
         if (h < 0) return r;
-        const uint32_t mo = motif[h];
+        // pattern bases, first base in the top bits: flank (flank mode) then motif
+        const uint64_t pat = plen > M ? ((uint64_t)flank[h] << (2 * M)) | motif[h] : (uint64_t)motif[h];
         uint32_t q = (uint32_t)((b * 32) % period);
         for (int x = 0; x < 32; ++x) {
-            if (q < M) {
-                const uint64_t base = (mo >> (2 * (M - 1 - q))) & 3u;
+            if (q < plen) {
+                const uint64_t base = (pat >> (2 * (plen - 1 - q))) & 3u;
                 r = (r & ~(3ull << (2 * x))) | (base << (2 * x));
             }
             if (++q == period) q = 0;

@@ -187,7 +187,16 @@ int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint
 int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
                       uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
                       uint32_t long_len, int front_starts, uint32_t hot_permille, uint32_t n_motifs) {
+    return kh_gen_create_hot_ex(out, k, n, len_min, len_max, single_permille, seed, shuffle, threads, n_long, long_len,
+                                front_starts, hot_permille, n_motifs, 0u);
+}
+
+int kh_gen_create_hot_ex(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
+                         uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
+                         uint32_t long_len, int front_starts, uint32_t hot_permille, uint32_t n_motifs,
+                         uint32_t flags) {
     if (!out) return hfail(KH_ERR_ARG, "out is NULL");
+    const bool flank = (flags & KH_GEN_HOT_FLANK) != 0;
     *out = nullptr;
     if (k < 1 || k > KH_K_MAX || len_min < 1 || len_max < len_min || single_permille > 1000)
         return hfail(KH_ERR_ARG, "bad generator parameters");
@@ -207,12 +216,23 @@ int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_
         v.hot_pm = hot_permille;
         v.n_motifs = n_motifs;
         v.M = (uint32_t)v.kp.M;
+        v.plen = v.M;
         // every k-mer holds a full occurrence when the period is K - M + 1, which needs
         // K >= 2M + 7 to leave 8 free bases between occurrences (k=51: 20); shorter k (19, 31)
         // plant one motif per K bases: every k-mer keeps K - M free bases (4^7 at k=19) and
         // K - M + 1 of the K phases hold a full occurrence
         const uint32_t full = (uint32_t)(k - v.kp.M + 1);
         v.period = full >= v.M + 8 ? full : (uint32_t)k;
+        if (flank) {
+            // flank + motif (2M bases) once per K bases: K - 2M + 1 of the K phases (k=51: 20)
+            // hold the whole pattern, the others keep >= K - 2M free bases
+            if ((uint32_t)k < 2 * v.M + 8) {
+                delete g;
+                return hfail(KH_ERR_ARG, "hot flank mode needs k >= 2M + 8 (k=51 at M=16)");
+            }
+            v.plen = 2 * v.M;
+            v.period = (uint32_t)k;
+        }
         const uint32_t mmask = (uint32_t)((1ull << (2 * v.M)) - 1);
         for (uint32_t h = 0; h < n_motifs; ++h) {
             uint32_t best = 0, bo = 0xFFFFFFFFu;
@@ -225,6 +245,14 @@ int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_
                 }
             }
             v.motif[h] = best;
+            // flank: any M-mer ordered above the motif (the motif stays the minimizer)
+            for (uint32_t t = 0; flank; ++t) {
+                const uint32_t c = (uint32_t)kh::splitmix(seed ^ 0x1f83d9abfb41bd6bull ^ ((uint64_t)h << 20) ^ t) & mmask;
+                if (kh::win_order(c) > bo) {
+                    v.flank[h] = c;
+                    break;
+                }
+            }
         }
     }
     // 1) contig lengths until n k-mers (last one truncated); the first n_long contigs have
@@ -267,7 +295,7 @@ int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_
         int free_min = k;
         for (uint32_t t = 0; t < v.period; ++t) {
             int fixed = 0;
-            for (int q = 0; q < k; ++q) fixed += (t + (uint32_t)q) % v.period < v.M;
+            for (int q = 0; q < k; ++q) fixed += (t + (uint32_t)q) % v.period < v.plen;
             free_min = k - fixed < free_min ? k - fixed : free_min;
         }
         const double nh = (double)n * v.hot_pm / 1000.0;

@@ -545,9 +545,13 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
 // Successor of every head record of the last build: the run after the tail starts at
 // y = next_kmer(tail); when y's slot carries a head-record index (y heads a run with a record),
 // that index goes into the record (rec_succ), so the walker reads y's record straight after this
-// one instead of probing y's slot first (one dependent request per run instead of two). One wave
-// per region over its records (count after the records, written by the build). Splitters need no
-// test here: the walker checks the next k-mer for one before it follows a successor.
+// one instead of probing y's slot first (one dependent request per run instead of two). Splitters
+// need no test here: the walker checks the next k-mer for one before it follows a successor.
+// Each wave owns a contiguous range of regions and keeps its 64 lanes busy with a queue over the
+// range's records (the per-region counts follow the records, written by the build): a lane reads
+// its record, then probes y's 4-slot blocks quad-transposed as the walker does (lane q of a quad
+// loads slot q of each member's 64-B block; one request per block instead of one per slot: ~1.3
+// requests per lookup slot by slot). Records of consecutive lanes are consecutive 16-B lines.
 template <int W, int KT>
 __global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
                                                     uint64_t* headrec, uint32_t hcap) {
@@ -555,21 +559,110 @@ __global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t
     const uint32_t NR = nreg(p);
     const uint32_t* hn = reinterpret_cast<const uint32_t*>(headrec + (uint64_t)NR * hcap * 2);
     const int sh = rec_succ_shift(p);
-    const uint32_t lane = lane_id(), waves = gridDim.x * (BLOCK / 64);
-    for (uint32_t r = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; r < NR; r += waves) {
-        const uint32_t n = min(hn[r], hcap);
-        for (uint32_t id = lane; id < n; id += 64) {
-            uint64_t* rec = headrec + ((uint64_t)r * hcap + id) * 2;
-            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(rec);
-            const uint32_t f = ext_fwd(slot_ext(v.x));
+    const uint32_t lane = lane_id(), q = lane & 3u, ql = lane & ~3u;
+    const uint32_t waves = gridDim.x * (BLOCK / 64), wv = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64;
+    const uint32_t rpw = (NR + waves - 1) / waves;
+    uint32_t r = wv * rpw;                       // wave-uniform queue cursor: region r, record id
+    const uint32_t r_end = min(r + rpw, NR);
+    uint32_t id = 0;
+    // lane state: its record (index + 1, 0 = idle), y, the probe position (WQ_IDLE: record load)
+    uint64_t rec = 0, s = WQ_IDLE, x0 = 0;
+    Key y{0, 0};
+    bool fetch = false;
+    while (true) {
+        // refill idle lanes from the queue (uniform loop: one region per sub-step)
+        uint64_t idle = __ballot(rec == 0);
+        while (idle && r < r_end) {
+            const uint32_t nr = min(hn[r], hcap);
+            if (id >= nr) {
+                ++r;
+                id = 0;
+                continue;
+            }
+            const uint32_t take = min(nr - id, (uint32_t)__popcll(idle));
+            const uint32_t rk = mbcnt64(idle);
+            if (rec == 0 && rk < take) {
+                rec = (uint64_t)r * hcap + id + rk + 1;
+                fetch = true;
+            }
+            id += take;
+            idle = __ballot(rec == 0);
+        }
+        if (!__any(rec != 0)) break;
+        // loads: a fetching lane reads its record; a probing lane's quad reads its block
+        const uint64_t sp = (rec && !fetch) ? s : WQ_IDLE;
+        uint64_t sj[4], w0[4], w1[4];
+        sj[0] = qbcast64<0>(sp);
+        sj[1] = qbcast64<1>(sp);
+        sj[2] = qbcast64<2>(sp);
+        sj[3] = qbcast64<3>(sp);
+        ulonglong2 rv = make_ulonglong2(0, 0);
+        if (fetch) rv = *reinterpret_cast<const ulonglong2*>(headrec + (rec - 1) * 2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            w0[j] = EMPTY;
+            w1[j] = 0;
+            const uint64_t my = (sj[j] & ~3ull) + q;
+            if (sj[j] != WQ_IDLE && my < cap) load_slot_nt<W>(slots, my, w0[j], w1[j]);
+        }
+        uint64_t kh_[4], kl_[4];
+        kh_[0] = qbcast64<0>(y.hi);
+        kh_[1] = qbcast64<1>(y.hi);
+        kh_[2] = qbcast64<2>(y.hi);
+        kh_[3] = qbcast64<3>(y.hi);
+        kl_[0] = qbcast64<0>(y.lo);
+        kl_[1] = qbcast64<1>(y.lo);
+        kl_[2] = qbcast64<2>(y.lo);
+        kl_[3] = qbcast64<3>(y.lo);
+        uint32_t myfh = 4, myfe = 4, myidx = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t my = (sj[j] & ~3ull) + q;
+            const bool valid = sj[j] != WQ_IDLE && my >= sj[j] && my < cap;
+            const bool empty = w0[j] == EMPTY;
+            const bool hit = !empty & (slot_keybits(w0[j], p) == ((W == 1) ? kl_[j] : kh_[j])) &
+                             ((W == 1) | (w1[j] == kl_[j]));
+            const uint32_t bh = (uint32_t)(__ballot(valid && hit) >> ql) & 0xFu;
+            const uint32_t be = (uint32_t)(__ballot(valid && empty) >> ql) & 0xFu;
+            const uint32_t fh = bh ? (uint32_t)__builtin_ctz(bh) : 4u;
+            const uint32_t fe = be ? (uint32_t)__builtin_ctz(be) : 4u;
+            const uint32_t hx = qor32(q == fh ? slot_hidx(w0[j], p) : 0u);
+            if (q == (uint32_t)j) {
+                myfh = fh;
+                myfe = fe;
+                myidx = hx;
+            }
+        }
+        if (rec) {
+            bool done = false;
             uint32_t succ = 0;
-            uint64_t w0 = 0;
-            if (f <= 3u && probe<W>(key_next(slot_key(v.x, v.y, p), f, p), p, slots, cap, w0))
-                succ = slot_hidx(w0, p);
-            // one 64-bit store; walkers may read the record concurrently (side stream), which
-            // is only allowed when the successor field lies in the upper dword (rec_succ_side)
-            __hip_atomic_store(rec, (v.x & ((1ull << sh) - 1)) | ((uint64_t)succ << sh), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            if (fetch) {
+                x0 = rv.x;
+                const uint32_t f = ext_fwd(slot_ext(rv.x));
+                if (f <= 3u) {
+                    y = key_next(slot_key(rv.x, rv.y, p), f, p);
+                    s = home_of(place(y, p), cap, p);
+                } else {
+                    done = true;  // the run ends its contig: no successor
+                }
+                fetch = false;
+            } else if (myfh < myfe) {
+                succ = myidx;
+                done = true;
+            } else if (myfe < 4u) {
+                done = true;      // y is not in the table (the walker reports it)
+            } else {
+                const uint64_t nx = (s & ~3ull) + 4;
+                s = nx >= cap ? 0 : nx;
+            }
+            if (done) {
+                // one 64-bit store; walkers may read the record concurrently (side stream), which
+                // is only allowed when the successor field lies in the upper dword (rec_succ_side)
+                __hip_atomic_store(headrec + (rec - 1) * 2, (x0 & ((1ull << sh) - 1)) | ((uint64_t)succ << sh),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rec = 0;
+                s = WQ_IDLE;
+            }
         }
     }
 }
@@ -587,7 +680,8 @@ bool rec_succ_side(const KParams& p) { return rec_succ_shift(p) >= 32; }
 hipError_t launch_rec_succ(const KParams& p, TableView t, uint64_t* headrec, uint32_t hcap, hipStream_t s,
                            unsigned blocks) {
     if (!rec_succ_fits(p, hcap)) return hipSuccess;
-    const unsigned grid = blocks ? blocks : (unsigned)hmin((nreg(p) + BLOCK / 64 - 1) / (BLOCK / 64), 8192);
+    // a wave per ~16 regions keeps its lanes' record queue full (the waves' ranges are contiguous)
+    const unsigned grid = blocks ? blocks : (unsigned)hmin((nreg(p) + BLOCK / 64 - 1) / (BLOCK / 64), 8u * cu_count());
     if (p.W == 1)
         with_kt<1>(p.K, [&](auto kt) { k_rec_succ<1, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, headrec, hcap); });
     else
@@ -857,7 +951,9 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers 
         uint64_t off = 0, hops = 0;
         uint32_t pend = SEG_NONE;
         while (true) {
-            sb.seg_contig[g] = (uint32_t)c;
+            // a segment another contig reached first: two walks overlap (malformed input); the
+            // segment text would be written once, so kh_assemble redoes the walk unsegmented
+            if (atomicExch(&sb.seg_contig[g], (uint32_t)c) != SEG_NONE) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
             sb.seg_off[g] = (uint32_t)off;
             off += wb.contig_len[g] - 1;
             g = wb.seg_next[g];
@@ -900,7 +996,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain_jump(WalkBuffers wb, SegBuf
         if (g == SEG_NONE) continue;
         uint64_t off = sb.clen[c] - 1, hops = 0;
         while (true) {
-            sb.seg_contig[g] = (uint32_t)c;
+            if (atomicExch(&sb.seg_contig[g], (uint32_t)c) != SEG_NONE) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
             sb.seg_off[g] = (uint32_t)off;
             sb.anchor[g] = 1;
             off += sb.jsum[g];
@@ -915,7 +1011,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain_jump(WalkBuffers wb, SegBuf
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_seg_fill(WalkBuffers wb, SegBuffers sb) {
+__global__ __launch_bounds__(BLOCK) void k_seg_fill(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     if (!*sb.long_flag) return;
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg; i += (uint64_t)gridDim.x * BLOCK) {
@@ -927,7 +1023,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_fill(WalkBuffers wb, SegBuffers s
             off += wb.contig_len[g] - 1;
             g = wb.seg_next[g];
             if (g == SEG_NONE) break;
-            sb.seg_contig[g] = c;
+            if (atomicExch(&sb.seg_contig[g], c) != SEG_NONE) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
             sb.seg_off[g] = (uint32_t)off;
         }
     }
@@ -979,7 +1075,7 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
         k_seg_chain<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
         k_seg_jump<<<gs, BLOCK, 0, s>>>(wb, sb);
         k_seg_chain_jump<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
-        k_seg_fill<<<gs, BLOCK, 0, s>>>(wb, sb);
+        k_seg_fill<<<gs, BLOCK, 0, s>>>(wb, sb, stats);
     }
     return hipGetLastError();
 }

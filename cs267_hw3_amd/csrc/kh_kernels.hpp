@@ -37,7 +37,8 @@ enum CtrIdx : int {
                        // runs that left their slice) after the hot-region fixup
     CT_HOT = 9,        // remapped ("hot") placement regions of the table (kh_build.hip k_hot_mark)
     CT_HOTNEW = 10,    // regions the last exact mark remapped (their window words move: k_hot_gather)
-    CT_NUM = 11
+    CT_HOT2 = 11,      // level-2 marks: target regions whose remapped keys spread by key hash
+    CT_NUM = 12
 };
 
 // Chunk of appended bases: 8 words x 32 bases (2 bits each) = 256 bases.
@@ -339,7 +340,7 @@ struct PartBuffers {
     uint32_t hcap = 0;
 };
 // Bitmap words of the remapped-region set (one bit per region, 2^17 regions at most).
-static constexpr uint32_t HOT_WORDS = (1u << 17) / 32;
+static constexpr uint32_t HOT_WORDS = HOT_LEVEL_WORDS;  // one level of the hot bitmap (two levels)
 
 // Balanced region bounds (KParams::rb) from region counts (nullptr: equal ranges).
 // rb: the table's bounds (2^rbits + 1 words); counts nullptr: equal ranges (the build kernels read

@@ -204,7 +204,9 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_pred(const uint64_t* msgs, uint6
             continue;
         }
         const uint64_t g = ns + id[s];
-        st.jump[g] = msgs[4 * i + 2];
+        // a second predecessor: two walks run into one segment (malformed input, walks overlap)
+        if (atomicExch((unsigned long long*)&st.jump[g], (unsigned long long)msgs[4 * i + 2]) != GID_NONE)
+            atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
         st.acc[g] = msgs[4 * i + 3];
     }
 }

@@ -877,7 +877,8 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
         t.start()
     for t in th:
         t.join()
-    if errs:
+    if errs:  # the failure itself, not the barrier aborts it caused on the other ranks
+        errs.sort(key=lambda e: isinstance(e, threading.BrokenBarrierError))
         raise errs[0]
     return out if seq else out[0]
 

@@ -210,16 +210,19 @@ class SyntheticKmers:
     """Seeded synthetic dataset (kh_gen_*): records at any position range + ground truth."""
 
     def __init__(self, k, n, len_min=8, len_max=200, single_permille=0, seed=1, shuffle=True,
-                 threads=0, n_long=0, long_len=0, front_starts=False, hot_permille=0, n_motifs=0):
+                 threads=0, n_long=0, long_len=0, front_starts=False, hot_permille=0, n_motifs=0,
+                 hot_flank=False):
         """n_long / long_len / front_starts: the C5 walker skew; hot_permille / n_motifs: the C5
-        hot-bucket half (contigs sharing a few minimizer motifs, kh_gen_create_hot)."""
+        hot-bucket half (contigs sharing a few minimizer motifs, kh_gen_create_hot); hot_flank: a
+        fixed flank before every motif too (the shared stretch is 2M bases: the remap's worst case)."""
         self.k, self.n = k, int(n)
         self.R = record_size(k)
         self._L = _lib.lib()
         h = ctypes.c_void_p()
-        check(self._L.kh_gen_create_hot(ctypes.byref(h), k, self.n, len_min, len_max,
-                                        single_permille, seed, 1 if shuffle else 0, threads,
-                                        n_long, long_len, 1 if front_starts else 0, hot_permille, n_motifs))
+        check(self._L.kh_gen_create_hot_ex(ctypes.byref(h), k, self.n, len_min, len_max,
+                                           single_permille, seed, 1 if shuffle else 0, threads,
+                                           n_long, long_len, 1 if front_starts else 0, hot_permille, n_motifs,
+                                           1 if hot_flank else 0))
         self._h = h
 
     def close(self):

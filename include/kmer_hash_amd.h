@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KH_ABI_VERSION 2
+#define KH_ABI_VERSION 3
 #define KH_K_MAX 60
 
 enum {
@@ -69,6 +69,8 @@ typedef struct kh_stats {
     uint64_t n_hot_regions;  /* placement regions remapped (shared minimizers overfilled them): keys by (minimizer, neighbour window) */
     uint64_t n_overflow;     /* keys of the last partitioned build inserted by global CAS (full windows,
                                 probe runs that left their region slice) */
+    uint64_t n_spread_regions; /* remap targets the remap itself overfilled (a family sharing its
+                                  neighbour window too): their remapped keys placed by key hash */
 } kh_stats;
 
 /* ---- sizes / info --------------------------------------------------------------------------*/
@@ -254,6 +256,15 @@ int kh_gen_create_skewed(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint
 int kh_gen_create_hot(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
                       uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
                       uint32_t long_len, int front_starts, uint32_t hot_permille, uint32_t n_motifs);
+/* flags: KH_GEN_HOT_FLANK plants a fixed per-motif M-mer right before every motif occurrence (one
+ * flank + motif pattern per K bases, k >= 2M + 8): the k-mers holding the whole pattern (20 of 51
+ * phases at k=51) share the minimizer and its neighbour window, the worst case of the table's hot
+ * remap (a long exact repeat shared by a family). */
+#define KH_GEN_HOT_FLANK 1u
+int kh_gen_create_hot_ex(kh_gen** out, int k, uint64_t n, uint32_t len_min, uint32_t len_max,
+                         uint32_t single_permille, uint64_t seed, int shuffle, int threads, uint32_t n_long,
+                         uint32_t long_len, int front_starts, uint32_t hot_permille, uint32_t n_motifs,
+                         uint32_t flags);
 int kh_gen_destroy(kh_gen* g);
 uint64_t kh_gen_num_contigs(const kh_gen* g);
 /* records at output positions [pos_begin, pos_end) in kmer_pair layout (block split of

@@ -28,6 +28,9 @@ C5 = dict(k=51, len_min=2, len_max=16, single=0, seed=5199, n_long=8, long_len=1
 # C5's hot-bucket half: 30 % of the contigs carry one of 8 shared minimizer motifs (60M k-mers in
 # 8 minimizer windows: each window alone is ~2,500 region slices' worth of keys)
 C5H = dict(k=51, len_min=8, len_max=200, single=0, seed=5198, hot_permille=300, n_motifs=8)
+# its worst case for the remap: a fixed flank before every motif, so ~40 % of each family shares the
+# neighbour window too (one remap target region per family before the level-2 spread)
+C5F = dict(C5H, seed=5197, hot_flank=True)
 
 
 def _gen(cfg, n):
@@ -141,6 +144,36 @@ def test_c5_hot_bucket_200m_one_gpu(load):
     text, st = _single_gpu(g, n, load)
     assert st["n_contigs"] == g.num_contigs and st["n_hot_regions"] >= 8
     assert text == g.truth()
+
+
+@pytest.mark.parametrize("load", [0.5, 0.85])
+def test_c5_hot_flank_200m_one_gpu(load):
+    """Hot families that also share the neighbour window (a 32-base repeat): the remap's target
+    regions overfill, the sampled level-2 mark spreads their remapped keys by key hash before pass
+    1, so the global CAS list (list B) stays under 1 % of n and the text equals the truth."""
+    n = 200_000_000
+    g = _gen(C5F, n)
+    text, st = _single_gpu(g, n, load)
+    assert st["n_contigs"] == g.num_contigs and st["n_hot_regions"] >= 8
+    assert st["n_spread_regions"] >= 8, st
+    assert st["n_overflow"] < n // 100, st
+    assert text == g.truth()
+
+
+def test_c5_hot_flank_20m_vs_oracle_and_8_ranks():
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_bind as ob
+    n = 20_000_000
+    g = _gen(C5F, n)
+    rc, want, nc, _, _, _ = ob.assemble(51, g.records())
+    assert rc == 0 and want == g.truth()
+    text, st = _single_gpu(g, n)
+    assert st["n_contigs"] == nc and text == want
+    assert st["n_spread_regions"] > 0 and st["n_overflow"] < n // 100, st
+    # the owners of the shared minimizers receive whole families; their shards spread them too
+    info = _sharded(g, 8)
+    assert sum(s["n_inserted"] for s in info["stats"].values()) == n
+    assert max(s["n_overflow"] for s in info["stats"].values()) < n // 100
 
 
 def test_c5_hot_bucket_20m_vs_oracle():

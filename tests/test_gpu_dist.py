@@ -210,3 +210,15 @@ def test_sharded_small_then_large_input(P):
     check_ranks(gs, texts[0], P)
     check_ranks(gl, texts[1], P)
     check_ranks(gs, texts[2], P)
+
+
+def test_sharded_overlapping_walks_fail_loudly():
+    """Walks that run into each other (malformed input: a k-mer with two predecessors) make a
+    splitter segment two walks' successor; the sharded walk cannot write one segment into two
+    contigs, so it fails with an error on every rank instead of returning wrong text (the
+    single-GPU kh_assemble redoes such a walk unsegmented: test_overlapping_walks_redo)."""
+    from cs267_hw3_amd.dist import run_threaded
+    from test_gpu_parity import merging_walks
+    recs = merging_walks(19, 3000, seed=26)
+    with pytest.raises(kh.KmerHashError):
+        run_threaded(19, recs, 2)

@@ -424,6 +424,31 @@ def test_gpu_hot_minimizers_vs_oracle(monkeypatch, mode, k, n, lmax, hot, motifs
     assert found.all() and np.array_equal(out, sel)
 
 
+@pytest.mark.parametrize("mode", ["part", "cas"])
+@pytest.mark.parametrize("batches", [1, 3])
+def test_gpu_hot_flank_vs_oracle(monkeypatch, mode, batches):
+    """Families sharing the minimizer and its neighbour window (generator flank mode): level 2 of
+    the remap spreads them; both insert paths and multi-batch inserts agree with the oracle, and
+    find returns the exact records."""
+    monkeypatch.setenv("KH_INSERT", mode)
+    k, n = 51, 2_000_000
+    g = kh.SyntheticKmers(k, n, 8, 200, 10, seed=77 + batches, hot_permille=300, n_motifs=4, hot_flank=True)
+    recs = g.records()
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0 and want == g.truth()
+    t, got, gnc = run(k, recs, batches=batches)
+    assert gnc == nc and got == want
+    s = t.stats()
+    assert s["n_full"] == s["n_dup"] == s["n_missing"] == 0
+    assert s["n_hot_regions"] > 0 and s["n_spread_regions"] > 0, s
+    if mode == "part" and batches == 1:
+        assert s["n_overflow"] < n // 100, s
+    P = (k + 3) // 4
+    sel = recs[np.random.default_rng(3).choice(len(recs), 2000, replace=False)]
+    out, found = t.find(sel[:, :P])
+    assert found.all() and np.array_equal(out, sel)
+
+
 def test_gpu_hot_remap_off_is_not_needed_for_random_sets():
     """Random (non-repetitive) C3-shape input: no region is remapped; only probe runs that leave
     their slice near its end take the CAS path (a few per 10^4 keys at this table size)."""

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # every declared symbol is also bound with a signature in the Python stub
     assert sorted(_lib._SIGS) == declared
-    assert L.kh_abi_version() == 2
+    assert L.kh_abi_version() == 3
     hdr = open(os.path.join(os.path.dirname(GOLDEN), "..", "include", "kmer_hash_amd.h")).read()
     for name in ("MSG_WORDS", "TEXT_REC_WORDS", "LINK_WORDS", "PRED_WORDS", "SEG_REC_WORDS"):
         assert f"#define KH_{name} {getattr(_lib, name)}" in hdr

@@ -1,55 +1,64 @@
-// Spread of a hot minimizer family (the C5 hot-bucket set) over the remap target regions: the
-// secondary-window rule of kh_codec.hpp (second_window: the M-mer next to the minimizer occurrence)
-// against the rule it replaced (the lowest-order other window, which often overlaps the shared
-// motif and so takes few distinct values). Host only: ./tools/hot_spread [n]
+// Spread of hot minimizer families over the placement regions (host only, kh_codec.hpp rules):
+// level 1 remaps a region whose minimizer family overfills it to hot_region(minimizer window,
+// neighbour window); level 2 sends the remapped keys of a target region that the remap itself
+// overfills (a family sharing its neighbour window too: the generator's flank mode) to a region of
+// their key hash. Prints the largest region counts after each level.
+//   ./tools/hot_spread [n] [flank 0|1]
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-#include <algorithm>
-#include "kmer_hash_amd.h"
+
 #include "kh_codec.hpp"
+#include "kmer_hash_amd.h"
 using namespace kh;
-static uint32_t old_second(Key k, uint32_t win, const KParams& p) {
-    uint32_t best = 0xFFFFFFFFu, bw = win;
-    for (int j = 0; j <= p.K - p.M; ++j) {
-        const uint32_t w = win_bits(k, j, p);
-        const uint32_t o = (win_order(w) << 6) | (uint32_t)j;
-        if (w != win && o < best) { best = o; bw = w; }
-    }
-    return bw;
+
+static void top(const char* what, std::vector<uint32_t> c) {
+    std::sort(c.rbegin(), c.rend());
+    printf("%s: largest region counts %u %u %u, 10th %u\n", what, c[0], c[1], c[2], c[10]);
 }
+
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 20000000ull;
+    const uint32_t flags = argc > 2 && atoi(argv[2]) ? KH_GEN_HOT_FLANK : 0u;
     kh_gen* g;
-    if (kh_gen_create_hot(&g, 51, n, 8, 200, 0, 5198, 1, 8, 0, 0, 0, 300, 8)) return 1;
+    if (kh_gen_create_hot_ex(&g, 51, n, 8, 200, 0, 5198, 1, 8, 0, 0, 0, 300, 8, flags)) {
+        fprintf(stderr, "%s\n", kh_last_error());
+        return 1;
+    }
     KParams p = make_params(51);
-    uint64_t cap = (uint64_t)(n / 0.5);
-    int rb = 9; while (rb < 17 && (cap >> (rb + 1)) >= REGION_SLOTS) ++rb;
-    p.rbits = rb;
-    const uint32_t NR = 1u << rb;
+    const uint64_t cap = (uint64_t)(n / 0.5);
+    set_region_bits(p, cap);
+    const uint32_t NR = 1u << p.rbits;
     std::vector<uint8_t> recs(n * p.R);
     kh_gen_records(g, 0, n, recs.data());
-    std::vector<uint32_t> cnt(NR, 0), wins(n);
+    std::vector<uint32_t> l0(NR, 0), wins(n);
+    std::vector<int> js(n);
     std::vector<Key> keys(n);
     for (uint64_t i = 0; i < n; ++i) {
-        uint32_t ext; parse_record(&recs[i * p.R], p, keys[i], ext);
-        wins[i] = mini_window(keys[i], mini_scan(keys[i], p), p);
-        ++cnt[mini_region(wins[i], p)];
+        uint32_t ext;
+        parse_record(&recs[i * p.R], p, keys[i], ext);
+        const uint32_t mn = mini_scan(keys[i], p);
+        wins[i] = mini_window(keys[i], mn, p);
+        js[i] = (int)(mn & 63u);
+        ++l0[mini_region(wins[i], p)];
     }
-    const double mean = (double)n / NR;
-    std::vector<uint32_t> tn(NR, 0), to(NR, 0);
-    uint64_t nhot = 0, hotr = 0;
-    for (uint32_t r = 0; r < NR; ++r) hotr += cnt[r] > 4 * mean;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t r = mini_region(wins[i], p);
-        if (cnt[r] <= 4 * mean) continue;
-        ++nhot;
-        ++tn[mix32((wins[i] * 0x9E3779B1u) ^ second_window(keys[i], wins[i], p) ^ 0x2545F491u) >> (32 - rb)];
-        ++to[mix32((wins[i] * 0x9E3779B1u) ^ old_second(keys[i], wins[i], p) ^ 0x2545F491u) >> (32 - rb)];
-    }
-    std::sort(tn.rbegin(), tn.rend()); std::sort(to.rbegin(), to.rend());
-    printf("n=%llu regions=%u mean=%.0f slots/region=%.0f hot regions=%llu hot keys=%llu\n",
-           (unsigned long long)n, NR, mean, (double)cap / NR, (unsigned long long)hotr, (unsigned long long)nhot);
-    printf("new: top target counts %u %u %u %u ; old: %u %u %u %u\n", tn[0], tn[1], tn[2], tn[10], to[0], to[1], to[2], to[10]);
+    const double mean = (double)n / NR, thr = 2.0 * mean;  // the marks' threshold, roughly
+    std::vector<uint32_t> hot(2 * HOT_LEVEL_WORDS, 0);
+    uint64_t h1 = 0, h2 = 0;
+    for (uint32_t r = 0; r < NR; ++r)
+        if (l0[r] > thr) hot[r >> 5] |= 1u << (r & 31), ++h1;
+    p.hot = hot.data();
+    std::vector<uint32_t> l1(NR, 0);
+    for (uint64_t i = 0; i < n; ++i) ++l1[place_w(wins[i], keys[i], p, js[i]).r];
+    for (uint32_t r = 0; r < NR; ++r)
+        if (l1[r] > thr) hot[HOT_LEVEL_WORDS + (r >> 5)] |= 1u << (r & 31), ++h2;
+    std::vector<uint32_t> l2(NR, 0);
+    for (uint64_t i = 0; i < n; ++i) ++l2[place_w(wins[i], keys[i], p, js[i]).r];
+    printf("n=%llu flank=%u regions=%u mean=%.0f level-1 marks %llu level-2 marks %llu\n", (unsigned long long)n,
+           flags, NR, mean, (unsigned long long)h1, (unsigned long long)h2);
+    top("minimizer regions", l0);
+    top("after level 1", l1);
+    top("after level 2", l2);
     kh_gen_destroy(g);
 }
