@@ -340,17 +340,18 @@ struct Place {
 // family and piles it into a few regions again. The home inside the region is home_in(.., key_hash32).
 // js: the occurrence's window index j* (mini_scan's low 6 bits: the first window of the smallest
 // order, so the first with the minimizer's content), or -1 to find it from win
+// window index of the minimizer occurrence (js < 0: found from its content win)
+KH_HD int occurrence(Key k, uint32_t win, const KParams& p, int js) {
+    if (js >= 0) return js;
+    for (int j = 0; j <= p.K - p.M; ++j)
+        if (win_bits(k, j, p) == win) return j;
+    return 0;
+}
+KH_HD int second_index(int js, const KParams& p) {
+    return js + 2 * p.M <= p.K ? js + p.M : (js >= p.M ? js - p.M : (2 * js < p.K - p.M ? p.K - p.M : 0));
+}
 KH_HD uint32_t second_window(Key k, uint32_t win, const KParams& p, int js = -1) {
-    if (js < 0) {
-        js = 0;
-        for (int j = 0; j <= p.K - p.M; ++j)
-            if (win_bits(k, j, p) == win) {
-                js = j;
-                break;
-            }
-    }
-    const int j2 = js + 2 * p.M <= p.K ? js + p.M : (js >= p.M ? js - p.M : (2 * js < p.K - p.M ? p.K - p.M : 0));
-    return win_bits(k, j2, p);
+    return win_bits(k, second_index(occurrence(k, win, p, js), p), p);
 }
 KH_HD uint32_t hot_region(Key k, uint32_t win, const KParams& p, int js = -1) {
     return mix32((win * 0x9E3779B1u) ^ second_window(k, win, p, js) ^ 0x2545F491u) >> (32 - p.rbits);
@@ -359,14 +360,29 @@ KH_HD bool region_is_hot(const uint32_t* hot, uint32_t r) { return hot && ((hot[
 // The bitmap has two levels of 2^17 bits (KParams::hot): level 1 marks minimizer regions whose keys
 // are remapped (hot_region); level 2 marks target regions that the remap itself overfills — a family
 // whose copies also share the neighbour window (a shared stretch of 2M bases: a repeat) lands in one
-// target region — and the remapped keys headed there go to a region of their whole key's hash
-// (evenly spread; their runs lose their chains, so the walker looks each such k-mer up). Level 2 is
-// read only for keys level 1 remapped.
+// target region — and the remapped keys headed there spread by the bases next to that stretch
+// (spread_region). Level 2 is read only for keys level 1 remapped.
 static constexpr uint32_t HOT_LEVEL_WORDS = (1u << REGION_BITS_MAX) / 32;
-KH_HD uint32_t spread_region(Key k, const KParams& p) { return (uint32_t)(key_hash(k) >> 32) >> (32 - p.rbits); }
+// Level-2 placement of a remapped key whose target region t overfilled: t mixed with the SPREAD_B
+// bases right next to the shared stretch (the minimizer and neighbour windows) on the right when
+// they fit in the k-mer, else on the left. Those bases are fixed positions of the contig, so along
+// a run (the stretch moves one window index per k-mer) they stay the same until the side switches:
+// a run changes region at most once more and keeps its chains, while the family spreads over up to
+// 4^SPREAD_B regions. Short k (K < 2M + 2 SPREAD_B - 1, no room on either side): whole-key hash.
+static constexpr int SPREAD_B = 8;
+KH_HD uint32_t spread_region(Key k, uint32_t t, uint32_t win, const KParams& p, int js) {
+    if (p.K >= 2 * p.M + 2 * SPREAD_B - 1) {
+        const int j = occurrence(k, win, p, js), j2 = second_index(j, p);
+        const int lo = j < j2 ? j : j2, hi = (j < j2 ? j2 : j) + p.M;
+        const int at = lo >= SPREAD_B ? lo - SPREAD_B : hi;  // K - hi >= SPREAD_B when lo < SPREAD_B
+        const uint32_t b = win_bits(k, at, p) & ((1u << (2 * SPREAD_B)) - 1u);
+        return mix32((t * 0x85EBCA6Bu) ^ (b * 0x9E3779B1u) ^ 0x68E31DA4u) >> (32 - p.rbits);
+    }
+    return (uint32_t)(key_hash(k) >> 32) >> (32 - p.rbits);
+}
 KH_HD uint32_t remap_region(Key k, uint32_t win, const KParams& p, int js = -1) {
     const uint32_t t = hot_region(k, win, p, js);
-    return region_is_hot(p.hot + HOT_LEVEL_WORDS, t) ? spread_region(k, p) : t;
+    return region_is_hot(p.hot + HOT_LEVEL_WORDS, t) ? spread_region(k, t, win, p, js) : t;
 }
 KH_HD Place place_w(uint32_t win, Key k, const KParams& p, int js = -1) {
     uint32_t r = mini_region(win, p);

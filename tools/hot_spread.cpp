@@ -32,12 +32,13 @@ int main(int argc, char** argv) {
     const uint32_t NR = 1u << p.rbits;
     std::vector<uint8_t> recs(n * p.R);
     kh_gen_records(g, 0, n, recs.data());
-    std::vector<uint32_t> l0(NR, 0), wins(n);
+    std::vector<uint32_t> l0(NR, 0), wins(n), fwd(n);
     std::vector<int> js(n);
     std::vector<Key> keys(n);
     for (uint64_t i = 0; i < n; ++i) {
         uint32_t ext;
         parse_record(&recs[i * p.R], p, keys[i], ext);
+        fwd[i] = ext_fwd(ext);
         const uint32_t mn = mini_scan(keys[i], p);
         wins[i] = mini_window(keys[i], mn, p);
         js[i] = (int)(mn & 63u);
@@ -55,6 +56,17 @@ int main(int argc, char** argv) {
         if (l1[r] > thr) hot[HOT_LEVEL_WORDS + (r >> 5)] |= 1u << (r & 31), ++h2;
     std::vector<uint32_t> l2(NR, 0);
     for (uint64_t i = 0; i < n; ++i) ++l2[place_w(wins[i], keys[i], p, js[i]).r];
+    // runs: k-mers whose successor lands in another region (each costs the walker a lookup)
+    auto breaks = [&]() {
+        uint64_t b = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (fwd[i] > 3) continue;
+            const Key y = key_next(keys[i], fwd[i], p);
+            b += place(y, p).r != place_w(wins[i], keys[i], p, js[i]).r;
+        }
+        return (unsigned long long)b;
+    };
+    printf("region changes along contigs (walker lookups): %llu of %llu k-mers\n", breaks(), (unsigned long long)n);
     printf("n=%llu flank=%u regions=%u mean=%.0f level-1 marks %llu level-2 marks %llu\n", (unsigned long long)n,
            flags, NR, mean, (unsigned long long)h1, (unsigned long long)h2);
     top("minimizer regions", l0);
