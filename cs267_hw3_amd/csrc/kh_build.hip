@@ -1643,34 +1643,86 @@ static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n
 // bounds come from the first build after a clear and stay until the next clear; lookups read
 // them from rb (two adjacent words per region). When a slice would exceed the LDS slice
 // (region_max_slots), equal ranges are written instead.
+// A region whose proportional slice would pass the LDS slice (a clump of remapped runs at load
+// 0.85) gets its count clamped so that its slice fits (a few fixed-point rounds: clamping frees
+// capacity, which grows the others' slices); the keys past its slice take the global CAS insert.
+// Only if the clamped bounds still do not fit are equal ranges written (round 4 fell back to equal
+// ranges whenever one region did not fit: at load 0.85 that overflowed a tenth of the regions).
 template <int Unused = 0>
 __global__ __launch_bounds__(1024) void k_bounds(KParams p, uint64_t cap, const uint32_t* counts, uint32_t RC,
                                                  uint64_t smax, uint64_t* rb) {
     __shared__ unsigned long long wsum[16];
+    __shared__ unsigned long long wmax[16];
     __shared__ int bad;
     const uint32_t NR = nreg(p);
     const uint32_t per = (NR + 1023) / 1024;
     const uint32_t r0 = threadIdx.x * per;
-    uint64_t loc = 0;
-    for (uint32_t r = r0; r < r0 + per && r < NR; ++r) loc += counts ? min(counts[r], RC) : 0u;
-    // exclusive scan of loc over the block (16 waves)
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t cmax = ~0ull;  // clamp of the region counts
+    auto cnt = [&](uint32_t r) -> uint64_t {
+        const uint64_t c = counts ? min(counts[r], RC) : 0u;
+        return c < cmax ? c : cmax;
+    };
+    // block sum (and max) of this thread's clamped counts
+    auto reduce = [&](uint64_t v, uint64_t m, uint64_t& tot, uint64_t& mx) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            v += __shfl_xor(v, o, 64);
+            const uint64_t y = __shfl_xor(m, o, 64);
+            m = y > m ? y : m;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            wsum[w] = v;
+            wmax[w] = m;
+        }
+        __syncthreads();
+        tot = 0;
+        mx = 0;
+        for (uint32_t i = 0; i < 16; ++i) {
+            tot += wsum[i];
+            mx = wmax[i] > mx ? wmax[i] : mx;
+        }
+    };
+    uint64_t N0 = 0, mx = 0;
+    {
+        uint64_t v = 0, m = 0;
+        for (uint32_t r = r0; r < r0 + per && r < NR; ++r) {
+            v += cnt(r);
+            m = cnt(r) > m ? cnt(r) : m;
+        }
+        reduce(v, m, N0, mx);
+    }
+    const double beta = (double)N0 / NR / 8.0 + 1.0;  // prior: no region gets an empty slice
+    uint64_t N = N0;
+    for (int it = 0; it < 6; ++it) {
+        const double sc = (double)cap / ((double)N + beta * NR);
+        const double lim = 0.97 * (double)smax / sc - beta;
+        if ((double)mx <= lim) break;  // every slice fits
+        cmax = lim < 1.0 ? 1ull : (uint64_t)lim;
+        uint64_t v = 0, m = 0;
+        for (uint32_t r = r0; r < r0 + per && r < NR; ++r) {
+            v += cnt(r);
+            m = cnt(r) > m ? cnt(r) : m;
+        }
+        reduce(v, m, N, mx);
+    }
+    uint64_t loc = 0;
+    for (uint32_t r = r0; r < r0 + per && r < NR; ++r) loc += cnt(r);
+    // exclusive scan of loc over the block (16 waves)
     uint64_t x = loc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint64_t y = __shfl_up(x, o, 64);
         if ((int)lane >= o) x += y;
     }
+    __syncthreads();
     if (threadIdx.x == 0) bad = 0;
     if (lane == 63) wsum[w] = x;
     __syncthreads();
-    uint64_t pre = 0, N = 0;
-    for (uint32_t i = 0; i < 16; ++i) {
-        pre += i < w ? wsum[i] : 0ull;
-        N += wsum[i];
-    }
+    uint64_t pre = 0;
+    for (uint32_t i = 0; i < 16; ++i) pre += i < w ? wsum[i] : 0ull;
     pre += x - loc;
-    const double beta = (double)N / NR / 8.0 + 1.0;  // prior: no region gets an empty slice
     const double scale = (double)cap / ((double)N + beta * NR);
     auto bound = [&](uint32_t r, uint64_t P) -> uint64_t {
         const uint64_t b = (uint64_t)(((double)P + beta * r) * scale);
@@ -1678,7 +1730,7 @@ __global__ __launch_bounds__(1024) void k_bounds(KParams p, uint64_t cap, const 
     };
     uint64_t P = pre, prev = bound(r0, pre);
     for (uint32_t r = r0; r < r0 + per && r < NR; ++r) {
-        P += counts ? min(counts[r], RC) : 0u;
+        P += cnt(r);
         const uint64_t nx = bound(r + 1, P);
         if (nx - prev > smax) bad = 1;
         prev = nx;
@@ -1688,7 +1740,7 @@ __global__ __launch_bounds__(1024) void k_bounds(KParams p, uint64_t cap, const 
     P = pre;
     for (uint32_t r = r0; r < r0 + per && r < NR; ++r) {
         rb[r] = eq ? (r ? mulhi64((uint64_t)r << (64 - p.rbits), cap) : 0ull) : bound(r, P);
-        P += counts ? min(counts[r], RC) : 0u;
+        P += cnt(r);
     }
     if (threadIdx.x == 0) rb[NR] = cap;
 }

@@ -13,6 +13,9 @@ B="--no-cpu --e2e-steps 0 --steps 7 --warmup 2"
 for w in c3 c5h c5f c5; do
   timeout -k 10 300 python bench.py --workload $w $B > gpurun_out/bench_$w.log 2>&1
 done
+for w in c3 c5h c5f; do
+  timeout -k 10 300 python bench.py --workload $w --load 0.85 $B > gpurun_out/bench_${w}_85.log 2>&1
+done
 KH_BENCH_FORCE_DIST=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
   --master-addr 127.0.0.1 --master-port 29544 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu --e2e-steps 0 \
   > gpurun_out/b_dist.log 2>&1
