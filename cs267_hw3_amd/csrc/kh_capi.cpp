@@ -116,7 +116,7 @@ struct kh_table {
     uint64_t stage_total = 0, stage_n = 0;
     uint64_t collected_n = 0;  // records passed to kh_route_starts_dev since the last clear
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
-    DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_misc, mw_store;  // migrating walk
+    DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
     // splitter segments of the migrating walk (kh_mseg.hip)
     DevBuf ms_len, ms_hi, ms_lo, ms_has, ms_done, ms_jump, ms_acc, ms_stab, ms_stab_id, ms_qsrc, ms_misc;
     DevBuf mw_cnt, mw_list, mw_carry[2], mw_carry_dst[2];  // fixed-slot rounds
@@ -414,7 +414,7 @@ int kh_destroy(kh_table* t) {
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->splits, &t->splits_w, &t->seg_next,
                       &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id,
                       &t->seg_jump, &t->seg_jsum, &t->seg_anchor, &t->seg_pend,
-                      &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage,
+                      &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
                       &t->mw_cnt, &t->mw_list, &t->mw_carry[0], &t->mw_carry[1], &t->mw_carry_dst[0],
@@ -1499,10 +1499,9 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
         KH_HIP(kh::launch_add_count(n_dev, t->rw_n, nullptr, 0, t->stream));
     }
     const uint64_t cb = t->mw_wg;  // held-back messages: at most every walker
-    // text records stage per lane of the walk's grid (not per input: it does not grow with the
-    // walkers this rank holds, C5's 111M on one rank at 1B)
     if ((rc = t->mw_tmp.ensure((nb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_dst.ensure(nb + 1)) ||
-        (rc = t->mw_stage.ensure(kh::mw_run_lanes(nb) * kh::MW_REC_SLOTS * 16)) ||
+        (rc = t->mw_stage.ensure((nb + 1) * kh::MW_REC_SLOTS * 16)) || (rc = t->mw_nrec.ensure(nb + 1)) ||
+        (rc = t->mw_off.ensure((nb + 1) * 8)) || (rc = t->scratch.ensure(kh::scan_scratch_words(nb) * 8 + 64)) ||
         (rc = t->mw_cnt.ensure((2 * P + 2) * 8)) ||
         (rc = t->mw_carry[0].ensure((cb + 1) * kh::MSG_WORDS * 8)) ||
         (rc = t->mw_carry[1].ensure((cb + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_carry_dst[0].ensure(cb + 1)) ||
@@ -1522,12 +1521,14 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
     mw.tmp = t->mw_tmp.as<uint64_t>();
     mw.dst = t->mw_dst.as<uint8_t>();
     mw.stage = t->mw_stage.as<uint64_t>();
-    // text records of this round -> the rank-local store, appended at its device-side count (sized
-    // at begin; a walk that would pass it fails instead of overrunning it)
-    mw.store = t->mw_store.as<uint64_t>();
-    mw.store_cap = t->mw_store_bound;
-    mw.store_n = mw_word(t, 2);
+    mw.nrec = t->mw_nrec.as<uint8_t>();
     KH_HIP(kh::launch_mw_run(t->kp, view(t), mw, t->stats.as<unsigned long long>(), t->stream));
+    // text records of this round -> the rank-local store at offsets continuing its device-side
+    // count (sized at begin; a walk that would pass it fails instead of overrunning it)
+    unsigned long long* store_n = mw_word(t, 2);
+    KH_HIP(kh::launch_mw_text_offsets(mw, t->mw_off.as<uint64_t>(), t->scratch.as<uint64_t>(), store_n, t->stream));
+    KH_HIP(kh::launch_mw_compact(mw, t->mw_off.as<uint64_t>(), t->mw_store.as<uint64_t>(), t->mw_store_bound,
+                                 t->stats.as<unsigned long long>(), t->stream));
     // outgoing walkers (+ the ones held back last round) -> P slots of out_cap; overflow held back
     const int cur = t->mw_cur, nxt = 1 - cur;
     kh::SlotRound r;

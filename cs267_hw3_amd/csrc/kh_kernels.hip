@@ -327,8 +327,8 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
     const uint64_t n = wb.n_starts + walk_splits(wb);
     const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
     const bool chains = p.chain && wb.hcap != 0;
-    uint64_t bbase = 0;
-    uint32_t bused = WALK_GRAB;
+    uint64_t bbase = 0, rbase = 0;
+    uint32_t bused = WALK_GRAB, rleft = 0;  // rleft: walkers left in the wave's reservation
     bool bdry = false;
     uint64_t bw0 = 0, bw1 = 0;
 
@@ -361,9 +361,16 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                 uint64_t n0 = 0, n1 = 0, nc = ~0ull;
                 if (cnt > avail) {
                     if (!bdry) {
-                        unsigned long long g = 0;
-                        if (lane == 0) g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB);
-                        bbase = __shfl(g, 0, 64);
+                        if (rleft == 0) {  // reserve WALK_BATCHES batches with one atomic
+                            unsigned long long g = 0;
+                            if (lane == 0)
+                                g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB * WALK_BATCHES);
+                            rbase = __shfl(g, 0, 64);
+                            rleft = WALK_GRAB * WALK_BATCHES;
+                        }
+                        bbase = rbase;
+                        rbase += WALK_GRAB;
+                        rleft -= WALK_GRAB;
                         if (bbase >= n) bdry = true;
                         const uint64_t mi = bbase + lane;
                         if (mi < n) {
@@ -751,82 +758,6 @@ __global__ __launch_bounds__(BLOCK) void k_write_heads(KParams p, const uint64_t
     }
 }
 
-// Whole lines of single-chunk contigs, heads of the others. 16 lanes per contig write its line
-// [off, off + K + len) as aligned dwords (lane l: dwords l, l + 16, ...): the K head characters
-// from the start k-mer, then — when the contig's bases all sit in its own first chunk (one
-// segment of <= CHUNK_BASES appended bases: every C3 contig without a splitter, every C5 short
-// one) — the appended bases from that chunk (chunk c belongs to segment c = contig c), then '\n'.
-// A store instruction covers four contigs' lines in 64-B runs, and a contig costs one level of
-// independent metadata loads (start key, offset, length, successor) instead of the chunk writer's
-// chunk -> segment -> contig -> offset chain. Bytes of the first / last dword that belong to a
-// neighbouring line are not written; the appended bases of longer contigs are left to the chunk
-// writer (which skips single-chunk contigs).
-__device__ __forceinline__ bool single_chunk(uint64_t c, const uint32_t* len, const uint32_t* seg_next) {
-    return (uint64_t)len[c] - 1 <= (uint64_t)CHUNK_BASES && (!seg_next || seg_next[c] == SEG_NONE);
-}
-
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_write_text(KParams p, const uint64_t* starts, uint64_t nc,
-                                                      const uint32_t* clen, const uint32_t* slen,
-                                                      const uint32_t* seg_next, const uint64_t* chunk_data,
-                                                      const uint64_t* off, char* out, uint64_t cap) {
-    constexpr uint32_t G = 16;
-    const uint32_t l = threadIdx.x & (G - 1);
-    const uint64_t groups = (uint64_t)gridDim.x * (BLOCK / G);
-    const int64_t K = p.K;
-    for (uint64_t c = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / G; c < nc; c += groups) {
-        const uint64_t w0 = starts[c * W];
-        const uint64_t w1 = (W == 2) ? starts[c * W + 1] : 0;
-        const Key k = slot_key(w0, w1, p);
-        const uint64_t o = off[c];
-        const int64_t total = K + (int64_t)clen[c];  // head + appended bases + '\n'
-        if (o + (uint64_t)total > cap) continue;  // past the buffer: not written
-        const int64_t app = total - K - 1;
-        const bool single = single_chunk(c, slen, seg_next);
-        const uint64_t* cw = chunk_data + c * CHUNK_WORDS;
-        const uint64_t first = o & ~3ull;
-        const uint32_t ndw = (uint32_t)((o + (uint64_t)total - first + 3) >> 2);
-        for (uint32_t d = l; d < ndw; d += G) {
-            const int64_t p0 = (int64_t)(first + 4ull * d) - (int64_t)o;  // line position of byte 0
-            // the (at most two) chunk words holding this dword's appended bases
-            const int64_t ia = p0 - K < 0 ? 0 : p0 - K, ib = p0 + 3 - K < app - 1 ? p0 + 3 - K : app - 1;
-            uint64_t wa = 0, wb = 0;
-            if (single && ia <= ib) {
-                wa = cw[ia >> 5];
-                wb = (ib >> 5) != (ia >> 5) ? cw[ib >> 5] : wa;
-            }
-            uint32_t dw = 0, own = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int64_t pos = p0 + b;
-                uint32_t ch = 0;
-                bool mine = pos >= 0 && pos < total;
-                if (mine) {
-                    if (pos < K) {
-                        ch = (0x54474341u >> (8 * key_base(k, (int)pos, p))) & 0xFFu;
-                    } else if (pos - K < app) {
-                        const int64_t i = pos - K;
-                        const uint64_t w = (i >> 5) == (ia >> 5) ? wa : wb;
-                        ch = (0x54474341u >> (8 * (uint32_t)((w >> (2 * (i & 31))) & 3u))) & 0xFFu;
-                        mine = single;
-                    } else {
-                        ch = '\n';
-                    }
-                }
-                dw |= ch << (8 * b);
-                own |= (mine ? 1u : 0u) << b;
-            }
-            char* dst = out + first + 4ull * d;
-            if (own == 0xFu) {
-                *reinterpret_cast<uint32_t*>(dst) = dw;
-            } else {
-                for (int b = 0; b < 4; ++b)
-                    if ((own >> b) & 1u) dst[b] = (char)(dw >> (8 * b));
-            }
-        }
-    }
-}
-
 __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* chunk_data,
                                                         const uint32_t* owner, const uint32_t* seq,
                                                         const unsigned long long* ctr,
@@ -845,7 +776,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* c
         const uint32_t c = ch < n_first ? (uint32_t)ch : owner[ch];
         const uint64_t j0 = (ch < n_first ? 0ull : (uint64_t)seq[ch] * CHUNK_BASES) + (uint64_t)w * 32;
         const uint64_t app = (uint64_t)len[c] - 1;
-        if (j0 >= app || app <= (uint64_t)CHUNK_BASES) continue;  // single-chunk contigs: k_write_text
+        if (j0 >= app) continue;
         const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
         if (off[c] + K + j0 + cntb > cap) continue;
         const uint64_t word = chunk_data[t];
@@ -952,11 +883,9 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
     const uint64_t cap = wb.text_cap ? wb.text_cap : ~0ull;
     const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
     if (p.W == 1)
-        k_write_text<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, wb.contig_len, nullptr, wb.chunk_data,
-                                             offsets, out, cap);
+        k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
     else
-        k_write_text<2><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, wb.contig_len, nullptr, wb.chunk_data,
-                                             offsets, out, cap);
+        k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
     const unsigned gc =
         (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr,
@@ -1162,14 +1091,17 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
 // Four threads per chunk (words q and q + 4 of it): C3 segments (~100 bases) use ~4 of a chunk's
 // 8 words and C5's ~21M contigs of 2-16 k-mers one, so eight threads per chunk (one per word)
 // mostly load the segment metadata only to find their word unused.
-static constexpr uint32_t WC_TPC = 4;
+#ifndef KH_WC_TPC
+#define KH_WC_TPC 4
+#endif
+static constexpr uint32_t WC_TPC = KH_WC_TPC;
 __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_t* chunk_data, const uint32_t* owner,
                                                             const uint32_t* seq, const unsigned long long* ctr,
                                                             uint64_t chunk_cap, uint64_t n_starts,
                                                             const unsigned long long* nsp_dev, uint64_t nsp,
                                                             const uint32_t* seg_len, const uint32_t* seg_contig,
-                                                            const uint32_t* seg_off, const uint32_t* seg_next,
-                                                            const uint64_t* off, char* out, uint64_t cap) {
+                                                            const uint32_t* seg_off, const uint64_t* off,
+                                                            char* out, uint64_t cap) {
     const uint64_t nseg = n_starts + (nsp_dev ? (uint64_t)*nsp_dev : nsp);
     const uint64_t nchunks = min(nseg + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
     const uint64_t nt = nchunks * WC_TPC;
@@ -1177,7 +1109,6 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
         const uint64_t ch = t / WC_TPC;
         const uint32_t q = (uint32_t)(t % WC_TPC);
         const uint32_t g = ch < nseg ? (uint32_t)ch : owner[ch];
-        if (g < n_starts && single_chunk(g, seg_len, seg_next)) continue;  // written by k_write_text
         const uint32_t c = seg_contig[g];
         if (c == SEG_NONE) continue;  // a segment no contig reached
         const uint64_t cb = ch < nseg ? 0ull : (uint64_t)seq[ch] * CHUNK_BASES;
@@ -1207,17 +1138,11 @@ hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const
     }
     if (!(phases & MAT_WRITE)) return hipSuccess;
     const uint64_t cap = wb.text_cap ? wb.text_cap : ~0ull;
-    const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
-    if (p.W == 1)
-        k_write_text<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, sb.clen, wb.contig_len, wb.seg_next, wb.chunk_data,
-                                             offsets, out, cap);
-    else
-        k_write_text<2><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, sb.clen, wb.contig_len, wb.seg_next, wb.chunk_data,
-                                             offsets, out, cap);
+    if ((e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s, cap)) != hipSuccess) return e;
     const unsigned gc = (unsigned)hmin((wb.chunk_cap * WC_TPC + BLOCK - 1) / BLOCK, 8192);
     k_write_chunks_seg<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr, wb.chunk_cap,
                                             nc, wb.n_splits_dev, wb.n_splits, wb.contig_len, sb.seg_contig,
-                                            sb.seg_off, wb.seg_next, offsets, out, cap);
+                                            sb.seg_off, offsets, out, cap);
     return hipGetLastError();
 }
 

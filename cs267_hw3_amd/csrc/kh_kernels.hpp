@@ -157,10 +157,8 @@ struct MWalkRound {
     const unsigned long long* hot_on = nullptr;  // ctr[CT_HOT]: remapped regions exist (null: use p.hot)
     uint64_t* tmp;        // n_in * MSG_WORDS: outgoing message of input j
     uint8_t* dst;         // n_in: its destination rank (0xFF = finished)
-    uint64_t* stage;      // grid lanes * MW_REC_SLOTS * 2: text records of the lane's current input
-    uint64_t* store;      // the rank-local text store (store_cap records) ...
-    uint64_t store_cap;
-    unsigned long long* store_n;  // ... and its fill (device counter, continued across rounds)
+    uint64_t* stage;      // n_in * MW_REC_SLOTS * 2: text records of input j
+    uint8_t* nrec;        // n_in
     const uint64_t* headrec = nullptr;  // chain head records of this shard's build (hcap 0 = none)
     uint32_t hcap = 0;
 };
@@ -243,8 +241,12 @@ hipError_t launch_slot_round(const SlotRound& r, uint64_t* hist, uint64_t* off, 
 // *out = a + min(*b, bmax) (the first round's live walkers: starts + collected splitters)
 hipError_t launch_add_count(unsigned long long* out, uint64_t a, const unsigned long long* b, uint64_t bmax,
                             hipStream_t s);
-// lanes of k_mw_run's grid for n_in inputs (its per-lane stage holds MW_REC_SLOTS records each)
-uint64_t mw_run_lanes(uint64_t n_in);
+// text records of this round: absolute store offsets continuing *store_n (device counter, updated)
+hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
+                                  unsigned long long* store_n, hipStream_t s);
+// store_cap: the store's records; a round that would pass it fails the walk (ST_CHUNK_OVF)
+hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, uint64_t store_cap,
+                             unsigned long long* stats, hipStream_t s);
 hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, uint64_t* scratch,
                            uint64_t* out, uint64_t* counts, hipStream_t s);
 hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,

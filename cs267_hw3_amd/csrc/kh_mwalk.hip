@@ -28,10 +28,6 @@ __device__ __forceinline__ uint64_t rec_tag(uint32_t origin, bool fin, uint64_t 
 // One lane per input message (static stride, no work-queue atomics), one load per lane per loop
 // iteration, like k_walk_q. A lane's run ends when the walker finishes, migrates, or has flushed
 // MW_RUN_WORDS words this round (it then re-sends itself, bounding the per-input text region).
-// The text records of a run collect in the lane's own stage slot (MW_REC_SLOTS records) and go to
-// the rank's text store when the run ends: the lanes that ended in a loop iteration reserve their
-// records with one atomicAdd per wave (a wave prefix sum of their counts), so no per-input stage,
-// record counts or scan scale with the walkers a rank holds.
 // Chains (kh_build.hip): a probed k-mer whose slot names a head record is crossed in one step —
 // the record's tail key carries the run's bases. A chain shares one minimizer, hence one owner,
 // so it never crosses ranks. As on one GPU (k_walk_q), a walker starts from its own record when
@@ -67,8 +63,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
     uint64_t s = 0, buf = 0;
     uint32_t steps = 0, idx = 0, origin = 0, st = 0, nrec = 0, nwords = 0;
     uint32_t nsucc = 0;  // the last record's successor run (head-record index + 1 in its region)
-    uint64_t* const rec = mw.stage + ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * (MW_REC_SLOTS * 2);
-    bool flush = false;  // the lane's run ended: its nrec records go to the store
+    uint64_t* rec = nullptr;
     auto finish = [&](uint64_t jj) {
         if (steps & 31) {
             rec[2 * nrec] = rec_tag(origin, false, steps >> 5, idx);
@@ -81,31 +76,6 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
         mw.dst[jj] = MW_NONE;
     };
     while (true) {
-        if (__any(flush)) {
-            const uint32_t lane = lane_id();
-            const uint32_t c = flush ? nrec : 0u;
-            uint32_t x = c;  // inclusive wave scan of the ending lanes' record counts
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o, 64);
-                if (lane >= (uint32_t)o) x += y;
-            }
-            const uint32_t tot = __shfl(x, 63, 64);
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(mw.store_n, (unsigned long long)tot);
-            base = __shfl(base, 0, 64);
-            if (flush) {
-                const uint64_t o = base + x - c;
-                if (o + c > mw.store_cap) {  // the store's bound was wrong (a cycle?): fail, never overrun
-                    atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
-                } else {
-                    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(rec);
-                    ulonglong2* dst = reinterpret_cast<ulonglong2*>(mw.store) + o;
-                    for (uint32_t r = 0; r < c; ++r) dst[r] = src[r];
-                }
-            }
-            flush = false;
-        }
         if (!active && j < n_live) {
             const uint64_t* m = mw.in + j * MSG_WORDS;
             k.hi = m[0];
@@ -116,6 +86,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             const uint64_t m4 = m[4];
             origin = (uint32_t)m4 & 0xFFu;
             st = (uint32_t)(m4 >> 8) & 0xFFu;
+            rec = mw.stage + j * (MW_REC_SLOTS * 2);
             nrec = 0;
             nwords = 0;
             nsucc = 0;
@@ -187,7 +158,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             }
             if (fin) finish(j);
             if (fin || ovf) {
-                flush = true;
+                mw.nrec[j] = (uint8_t)nrec;
                 active = false;
                 j += stride;
             }
@@ -279,7 +250,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             } else if (myfe < 4u) {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
                 atomicAdd(&stats[ST_MISSING], 1ull);
                 finish(j);
-                flush = true;
+                mw.nrec[j] = (uint8_t)nrec;
                 active = false;
                 j += stride;
             } else {
@@ -328,6 +299,29 @@ __global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p_in, const uint64_t*
         m[3] = (idx0 + i) << 32;
         m[4] = rix ? rank | ((uint64_t)MW_READREC << 8) | (rix << 32)
                    : rank | ((uint64_t)(f > 4 ? EXT_BAD : f) << 8);
+    }
+}
+
+struct NrecF {
+    const uint8_t* n;
+    const unsigned long long* n_dev;  // inputs past the live count wrote nothing
+    __device__ uint64_t operator()(uint64_t i) const { return (!n_dev || i < *n_dev) ? n[i] : 0u; }
+};
+
+__global__ __launch_bounds__(BLOCK) void k_mw_compact(const uint64_t* stage, const uint8_t* nrec,
+                                                      const uint64_t* off, uint64_t nb, uint64_t* store,
+                                                      const unsigned long long* n_dev, uint64_t store_cap,
+                                                      unsigned long long* stats) {
+    const uint64_t n = n_dev ? min((uint64_t)*n_dev, nb) : nb;
+    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
+        const uint32_t c = nrec[j];
+        if (off[j] + c > store_cap) {  // the store's bound was wrong (a cycle?): fail, never overrun
+            atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+            continue;
+        }
+        const ulonglong2* src = reinterpret_cast<const ulonglong2*>(stage + j * (MW_REC_SLOTS * 2));
+        ulonglong2* dst = reinterpret_cast<ulonglong2*>(store + off[j] * 2);
+        for (uint32_t r = 0; r < c; ++r) dst[r] = src[r];
     }
 }
 
@@ -417,17 +411,31 @@ hipError_t launch_mw_init(const KParams& p, TableView t, uint32_t hcap, const ui
     return hipGetLastError();
 }
 
-// ~4 inputs per lane keeps lanes busy through the run-length tail without a work queue
-uint64_t mw_run_lanes(uint64_t n_in) { return (uint64_t)grid_for((n_in + 3) / 4, 4096) * BLOCK; }
-
 hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
                          hipStream_t s) {
     if (mw.n_in == 0) return hipSuccess;
-    const unsigned g = (unsigned)(mw_run_lanes(mw.n_in) / BLOCK);
+    // ~4 inputs per lane keeps lanes busy through the run-length tail without a work queue
+    constexpr uint64_t ipl = 4;
+    const unsigned g = grid_for((mw.n_in + ipl - 1) / ipl, 4096);
     if (p.W == 1)
         with_kt<1>(p.K, [&](auto kt) { k_mw_run<1, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats); });
     else
         with_kt<2>(p.K, [&](auto kt) { k_mw_run<2, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, mw, stats); });
+    return hipGetLastError();
+}
+
+hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t* scratch,
+                                  unsigned long long* store_n, hipStream_t s) {
+    if (mw.n_in == 0) return hipSuccess;
+    // offsets continue the store's running count (store_n, on the device: no host round trip)
+    return scan_exclusive(NrecF{mw.nrec, mw.n_dev}, mw.n_in, off, scratch, store_n, (unsigned long long*)nullptr, s);
+}
+
+hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, uint64_t store_cap,
+                             unsigned long long* stats, hipStream_t s) {
+    if (mw.n_in == 0) return hipSuccess;
+    k_mw_compact<<<grid_for(mw.n_in, 8192), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store, mw.n_dev, store_cap,
+                                                           stats);
     return hipGetLastError();
 }
 

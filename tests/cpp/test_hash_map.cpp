@@ -12,6 +12,9 @@
 //   test_hash_map_<K> gen     <n> <P> <len_min> <len_max> kh::ShardedTable at P ranks (threads, one
 //        GPU) on n generated k-mers (records made in HBM by kh_gen_records_dev); large enough per
 //        rank for the chunked, overlapped insert; each rank's text == its block's ground truth
+//   test_hash_map_<K> gen2    <n_small> <n> <P>           one kh::ShardedTable per rank walks a small
+//        generated set, is cleared, and walks a set of n (slot capacities learnt per input), then
+//        the small one again; every text == its block's truth
 // Exit status 0 = pass; a failed check prints it and exits 1.
 #include <algorithm>
 #include <cstdio>
@@ -227,6 +230,59 @@ int gen(uint64_t n, int P, uint32_t lmin, uint32_t lmax) {
     return 0;
 }
 
+// small input, clear, large input, clear, small again on the same maps (slot
+// capacities learnt from one input must not size another's rounds)
+int gen2(uint64_t n_small, uint64_t n, int P) {
+    kh_gen* gs = nullptr;
+    kh_gen* gl = nullptr;
+    kh::abi_check(kh_gen_create(&gs, KMER_LEN, n_small, 8, 200, 0, 3, 1, 0));
+    kh::abi_check(kh_gen_create(&gl, KMER_LEN, n, 8, 200, 0, 4, 1, 0));
+    kh::ThreadComm::Group group(P);
+    std::vector<std::thread> th;
+    std::vector<int> ok(P, 0);
+    std::vector<int> rounds(P, 0);
+    for (int r = 0; r < P; ++r)
+        th.emplace_back([&, r] {
+            try {
+                kh::hip_check(hipSetDevice(0), "hipSetDevice");
+                kh::ShardedTable st(KMER_LEN, n_small / P + 1, *group.comm(r), 0, &group);
+                kh::DevBuf recs;
+                int good = 1;
+                for (kh_gen* g : {gs, gl, gs}) {
+                    const uint64_t m = g == gs ? n_small : n;
+                    uint64_t b, e;
+                    block(m, P, r, b, e);
+                    void* d = recs.ensure((e - b) * kh_record_size(KMER_LEN) + 16);
+                    st.clear();
+                    kh::abi_check(kh_gen_records_dev(g, b, e, d, st.stream()));
+                    st.insert_all_dev(d, e - b);
+                    rounds[r] = std::max(rounds[r], st.assemble(m));
+                    const std::string text = st.contigs_text();
+                    uint64_t bytes = 0;
+                    kh::abi_check(kh_gen_truth(g, b, e, nullptr, 0, &bytes));
+                    std::string want(bytes, '\0');
+                    kh::abi_check(kh_gen_truth(g, b, e, &want[0], bytes, &bytes));
+                    good &= text == want;
+                }
+                ok[r] = good;
+            } catch (const std::exception& ex) {
+                fprintf(stderr, "rank %d: %s\n", r, ex.what());
+                group.abort();
+            }
+        });
+    for (auto& t : th) t.join();
+    kh_gen_destroy(gs);
+    kh_gen_destroy(gl);
+    for (int r = 0; r < P; ++r)
+        if (!ok[r]) {
+            fprintf(stderr, "rank %d differs from the truth of its block\n", r);
+            return 1;
+        }
+    printf("gen2 ok: n_small=%llu n=%llu P=%d max rounds=%d\n", (unsigned long long)n_small, (unsigned long long)n, P,
+           rounds[0]);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -238,6 +294,8 @@ int main(int argc, char** argv) {
     try {
         if (mode == "gen" && argc >= 6)
             return gen(strtoull(argv[2], nullptr, 10), atoi(argv[3]), (uint32_t)atoi(argv[4]), (uint32_t)atoi(argv[5]));
+        if (mode == "gen2" && argc >= 5)
+            return gen2(strtoull(argv[2], nullptr, 10), strtoull(argv[3], nullptr, 10), atoi(argv[4]));
         if (mode == "stock") return stock(fname);
         if (mode == "refloop" && argc >= 5) return refloop(fname, atoi(argv[3]), argv[4], false);
         if (mode == "refloopc" && argc >= 5) return refloop(fname, atoi(argv[3]), argv[4], true);

@@ -129,6 +129,18 @@ def test_sharded_table_generated(k, n, P, lmin, lmax):
     assert "gen ok" in r.stdout
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 4])
+def test_cpp_sharded_small_then_large(P):
+    """kh::ShardedTable walks a small set, is cleared, walks one 100x larger, then the small one
+    again on the same maps: slot capacities are learnt per input (walker count), every text
+    equals its block's truth."""
+    r = subprocess.run([_exe("test", 51), "gen2", "30000", "3000000", str(P)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gen2 ok" in r.stdout
+
+
 @pytest.mark.parametrize("P", [1, 8])
 def test_cpp_host_sharded_step_syncs(P):
     """The C++ host's sharded step (tools/kh_bench_cpp: clear + insert_all_dev + assemble) over P

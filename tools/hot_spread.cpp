@@ -5,6 +5,7 @@
 // their key hash. Prints the largest region counts after each level.
 //   ./tools/hot_spread [n] [flank 0|1]
 #include <algorithm>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -67,6 +68,45 @@ int main(int argc, char** argv) {
         return (unsigned long long)b;
     };
     printf("region changes along contigs (walker lookups): %llu of %llu k-mers\n", breaks(), (unsigned long long)n);
+    // per contig (ground-truth lines): lookups along it = 1 + region changes; the longest contigs
+    // of lookups bound the walk (one dependent request each)
+    {
+        uint64_t bytes = 0;
+        kh_gen_truth(g, 0, n, nullptr, 0, &bytes);
+        std::string text(bytes, '\0');
+        kh_gen_truth(g, 0, n, &text[0], bytes, &bytes);
+        std::vector<uint32_t> per;
+        size_t a = 0;
+        while (a < text.size()) {
+            size_t b = text.find('\n', a);
+            const int L = (int)(b - a);
+            uint32_t look = 1;
+            uint32_t prev = ~0u;
+            for (int t = 0; t + p.K <= L; ++t) {
+                uint8_t pk[32] = {0};
+                for (int q = 0; q < p.K; ++q) {
+                    const char c = text[a + t + q];
+                    const uint32_t code = c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : 3;
+                    pk[q / 4] |= (uint8_t)(code << (6 - 2 * (q % 4)));
+                }
+                pk[p.P] = 'A';
+                pk[p.P + 1] = 'A';
+                Key k;
+                uint32_t ext;
+                parse_record(pk, p, k, ext);
+                const uint32_t r = place(k, p).r;
+                if (t && r != prev) ++look;
+                prev = r;
+            }
+            per.push_back(look);
+            a = b + 1;
+        }
+        std::sort(per.rbegin(), per.rend());
+        double mean = 0;
+        for (auto x : per) mean += x;
+        printf("lookups per contig: mean %.2f, top %u %u %u, 100th %u, 1000th %u (of %zu contigs)\n",
+               mean / per.size(), per[0], per[1], per[2], per[99], per[999], per.size());
+    }
     printf("n=%llu flank=%u regions=%u mean=%.0f level-1 marks %llu level-2 marks %llu\n", (unsigned long long)n,
            flags, NR, mean, (unsigned long long)h1, (unsigned long long)h2);
     top("minimizer regions", l0);
