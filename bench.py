@@ -242,6 +242,8 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=3,
                     help="steps of the reference-boundary (host records -> host contigs) figure")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-routed", action="store_true",
+                    help="forced one-rank sharded line: skip the routed-step measurement")
     args = ap.parse_args()
 
     w = dict(WORKLOADS[args.workload])

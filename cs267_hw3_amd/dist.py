@@ -943,13 +943,36 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
     dist.all_reduce(tot)
     nc, nl = tot.tolist()
     ok = None
-    if not args.no_verify:
-        ok_local = int(dm.contigs_text() == g.truth(b, e))
+    truth = None if args.no_verify else g.truth(b, e)
+
+    def verify():
+        ok_local = int(dm.contigs_text() == truth)
         okt = torch.tensor([ok_local], dtype=torch.int64, device="cuda")
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
-        if not ok and rank == 0:
+        if not okt.item() and rank == 0:
             print("bench: contig text differs from the generator ground truth", file=sys.stderr)
+        return bool(okt.item())
+
+    if truth is not None:
+        ok = verify()
+    routed = None
+    if world == 1 and not dm.ROUTE_ONE_RANK and not getattr(args, "no_routed", False):
+        # The step P > 1 runs, at one rank: records through the one-pass route and the receiver's
+        # k_win1 + k_win2 (KH_DIST_ROUTE_ONE_RANK=1) instead of the single-GPU records pass.
+        # Timed after the headline steps, same bracket; not part of `value`.
+        dm.ROUTE_ONE_RANK = True
+        step()
+        rt = []
+        for _ in range(args.steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            rt.append(time.perf_counter() - t0)
+        routed = {"ms_per_step": 1e3 * sum(rt) / len(rt),
+                  "insert_pipeline_ms": shard.stats()["ms_insert_kernel"],
+                  "verified_vs_truth": verify() if truth is not None else None}
+        dm.ROUTE_ONE_RANK = False
     cpu = None
     if rank == 0 and cpu_baseline is not None and not args.no_cpu:
         # the CPU restatement of the reference on a bounded sample of the same generator/config
@@ -986,6 +1009,7 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
             "inserts_per_s": n_total / tmax, "lookups_per_s": nl / tmax,
             "contigs_per_s": nc / tmax, "verified_vs_truth": ok,
             "phases_ms": {"insert_pipeline_rank0": ins_ms, "build_rank0": build_ms},
+            **({"routed_one_rank": routed} if routed else {}),
             "roofline": {"bound": "hbm", "kernel": "k_part_build_pf (rank 0's region build + chains over the "
                                                      "words it received)",
                          "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,

@@ -132,3 +132,19 @@ def test_bench_world_size_mismatch_fails(tmp_path):
                        cwd=tmp_path, capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_bench_forced_one_rank_routed(tmp_path):
+    """The forced one-rank sharded line (KH_BENCH_FORCE_DIST=1) also times the routed step
+    (records through the one-pass route and the receiver's re-partition, as at P > 1) and checks
+    its text against the ground truth."""
+    import json
+    r = _torchrun(1, 29553, [os.path.join(ROOT, "bench.py"), "--gpus", "1", "--kmers", "2000000", "--steps", "2",
+                             "--warmup", "1", "--no-cpu", "--e2e-steps", "0"], tmp_path,
+                  dict(os.environ, PYTHONPATH=ROOT, KH_BENCH_FORCE_DIST="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert line["n_gpus"] == 1 and line["verified_vs_truth"] is True
+    ro = line["routed_one_rank"]
+    assert ro["verified_vs_truth"] is True and ro["ms_per_step"] > 0

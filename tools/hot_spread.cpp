@@ -112,5 +112,23 @@ int main(int argc, char** argv) {
     top("minimizer regions", l0);
     top("after level 1", l1);
     top("after level 2", l2);
+    // keys by the fill of their region's slice (equal ranges: 2x the mean slots at load 0.5), and
+    // the mean linear-probe length of a successful lookup at that fill, (1 + 1/(1 - a)) / 2
+    {
+        const double bins[] = {0.5, 0.67, 0.8, 0.9, 1.0};
+        uint64_t nb[6] = {0};
+        double probe = 0;
+        for (uint32_t r = 0; r < NR; ++r) {
+            const double a = l2[r] / (2.0 * mean);
+            int b = 0;
+            while (b < 5 && a > bins[b]) ++b;
+            nb[b] += l2[r];
+            const double ac = a < 0.99 ? a : 0.99;
+            probe += l2[r] * 0.5 * (1.0 + 1.0 / (1.0 - ac));
+        }
+        printf("keys by slice fill: <=0.5 %.3f, 0.5-0.67 %.3f, 0.67-0.8 %.3f, 0.8-0.9 %.3f, 0.9-1 %.3f, >1 %.3f;"
+               " mean probe %.2f slots\n", nb[0] / (double)n, nb[1] / (double)n, nb[2] / (double)n,
+               nb[3] / (double)n, nb[4] / (double)n, nb[5] / (double)n, probe / n);
+    }
     kh_gen_destroy(g);
 }

@@ -34,7 +34,7 @@ fi
 # its PMC traffic goes in as workload "c3_dist" (the N > 1 bench line reads it). The env makes
 # rank 0 of a one-rank process group without the torchrun launcher (the profiler runs python).
 if [ -z "${NO_DIST:-}" ]; then
-  D="python3 bench.py --steps 3 --warmup 1 --no-cpu --e2e-steps 0 --no-verify ${BARGS:-}"
+  D="python3 bench.py --steps 3 --warmup 1 --no-cpu --e2e-steps 0 --no-verify --no-routed ${BARGS:-}"
   export KH_BENCH_FORCE_DIST=1 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$OUT/dtrace -- $D > $OUT/dtrace.log 2>&1
   python3 tools/kstats.py $OUT/dtrace > $OUT/kernel_stats_dist.txt
