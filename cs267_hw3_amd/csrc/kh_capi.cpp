@@ -104,7 +104,7 @@ struct kh_table {
     DevBuf mask, mask_off, scratch;          // per insert batch
     DevBuf stage;                            // host-API staging of records / keys
     DevBuf stage2, stage3;
-    DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text;
+    DevBuf contig_len, contig_off, chunk_data, chunk_owner, chunk_seq, text, line_first;
     DevBuf route_hist, route_off, route_scratch, route_own;                       // sharded path
     DevBuf pb_buf1, pb_buf2, pb_cnt, pb_ovf;  // partitioned build
     DevBuf headrec;                           // chain head records (region build -> walker)
@@ -410,7 +410,7 @@ int kh_destroy(kh_table* t) {
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     DevBuf* bufs[] = {&t->slots, &t->starts, &t->ctr, &t->stats, &t->mask, &t->mask_off,
                       &t->scratch, &t->stage, &t->stage2, &t->stage3, &t->contig_len,
-                      &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text,
+                      &t->contig_off, &t->chunk_data, &t->chunk_owner, &t->chunk_seq, &t->text, &t->line_first,
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->splits, &t->splits_w, &t->seg_next,
                       &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id,
                       &t->seg_jump, &t->seg_jsum, &t->seg_anchor, &t->seg_pend,
@@ -909,12 +909,14 @@ int kh_assemble_dev(kh_table* t) {
         if ((rc = t->text.ensure(hv[1] + 64))) return rc;
         break;
     }
+    if ((rc = t->line_first.ensure(kh::line_first_words(t->text.bytes) * 4))) return rc;
+    uint32_t* lf = t->line_first.as<uint32_t>();
     if (kp.split_bits)
         KH_HIP(kh::launch_materialize_seg(kp, wb, sb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                          t->text.as<char>(), ctr, t->stream, kh::MAT_WRITE));
+                                          t->text.as<char>(), ctr, t->stream, kh::MAT_WRITE, lf, t->text.bytes));
     else
         KH_HIP(kh::launch_materialize(kp, wb, t->contig_off.as<uint64_t>(), t->scratch.as<uint64_t>(),
-                                      t->text.as<char>(), ctr, t->stream, kh::MAT_WRITE));
+                                      t->text.as<char>(), ctr, t->stream, kh::MAT_WRITE, lf, t->text.bytes));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = ns;

@@ -16,11 +16,9 @@ static constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;  // 2048 elements per block
 static constexpr int WALK_GRAB = 64;                   // start k-mers per wave batch (one per lane)
 // batches a wave reserves per work-queue atomic: the queue head is ONE global counter, and
 // same-address atomics serialise (~11 ns each): C5's 21M short contigs pulled 64 at a time made
-// 328K of them, ~3.7 ms of the walk
-#ifndef KH_WALK_BATCHES
-#define KH_WALK_BATCHES 8
-#endif
-static constexpr int WALK_BATCHES = KH_WALK_BATCHES;
+// 328K of them, ~3.7 ms of the walk. C5 walk kernel 4.80 ms at 1 batch, 3.27 at 8, 2.99 at 32
+// (but C3 1.18 -> 1.85 ms at 32: long contigs leave a wave's reserved batches to one straggler)
+static constexpr int WALK_BATCHES = 8;
 static constexpr int MAX_R = 17;                       // K <= 60 -> PACKED <= 15 -> R <= 17
 
 // Launch-side dispatch to the compile-time shape (specialize<KT>): f(integral_constant<KT>).

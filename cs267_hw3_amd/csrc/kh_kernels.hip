@@ -758,18 +758,123 @@ __global__ __launch_bounds__(BLOCK) void k_write_heads(KParams p, const uint64_t
     }
 }
 
+// ---- line writer (K >= 16): the text written in output order ---------------------------------
+// A wave owns 1 KiB of the text and stores it with 16-B stores, one per lane, so every 64-B line is
+// written whole, once, by one instruction. The heads + chunks writers above store each contig's
+// head and its bases from two kernels at unaligned byte ranges: at C5 (21M contigs of ~60 bytes)
+// nearly every line was written partially twice. Each lane finds the contig holding its first
+// byte among the <= 62 contigs that start in the wave's KiB (contigs hold >= K + 1 >= 17 bytes) and
+// builds its 16 characters from that contig and the next: head bases from the start k-mer, the
+// bases of the contig's own first chunk (the first CHUNK_BASES bases of its first segment), '\n'.
+// Bytes past those (longer segments, splitter segments) are left to the chunk writer, which runs
+// after it on the same stream over the chunks it does not cover (chunk index >= n_starts).
+static constexpr uint32_t LINE_BYTES = 1024;  // text bytes per wave
+static constexpr uint32_t LINE_KMIN = 16;
+
+// line_first[b] = the contig holding byte b * LINE_BYTES (b < ceil(min(total, cap) / LINE_BYTES))
+__global__ __launch_bounds__(BLOCK) void k_line_first(int K, const uint32_t* clen, uint64_t nc, const uint64_t* off,
+                                                      const unsigned long long* ctr, uint64_t cap, uint32_t* first) {
+    const uint64_t lim = min((uint64_t)ctr[CT_OUT_BYTES], cap);
+    for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < nc; c += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t o = off[c], e = min(o + (uint64_t)K + clen[c], lim);
+        for (uint64_t b = (o + LINE_BYTES - 1) / LINE_BYTES; b * LINE_BYTES < e; ++b) first[b] = (uint32_t)c;
+    }
+}
+
+// 32 bits of the 128-bit value (h:l) from bit s on; s < 0 shifts left (zeros come in)
+__device__ __forceinline__ uint32_t bits32(uint64_t h, uint64_t l, int s) {
+    if (s <= -32 || s >= 128) return 0u;
+    if (s < 0) return (uint32_t)l << (-s);
+    if (s >= 64) return (uint32_t)(h >> (s - 64));
+    return s == 0 ? (uint32_t)l : (uint32_t)((l >> s) | (h << (64 - s)));
+}
+
+template <int W, int KT>
+__global__ __launch_bounds__(BLOCK) void k_write_lines(KParams p_in, const uint64_t* __restrict__ starts, uint64_t nc,
+                                                       const uint32_t* __restrict__ clen,
+                                                       const uint32_t* __restrict__ slen,
+                                                       const uint64_t* __restrict__ chunk_data,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ first,
+                                                       const unsigned long long* ctr, char* out, uint64_t cap) {
+    const KParams p = specialize<KT>(p_in);
+    const uint64_t lim = min((uint64_t)ctr[CT_OUT_BYTES], cap);
+    const uint32_t lane = lane_id();
+    const uint64_t nblk = (lim + LINE_BYTES - 1) / LINE_BYTES;
+    const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
+    const int K = p.K;
+    for (uint64_t blk = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / 64; blk < nblk; blk += waves) {
+        const uint64_t B0 = blk * LINE_BYTES, x0 = B0 + 16u * lane;
+        const uint64_t c0 = first[blk];
+        const uint64_t oj = c0 + lane < nc ? off[c0 + lane] : ~0ull;
+        // the lane's contig: the last of the wave's 64 whose text starts at or before x0
+        uint32_t lo = 0;
+#pragma unroll
+        for (uint32_t st = 32; st > 0; st >>= 1) {
+            const uint64_t v = __shfl(oj, (int)(lo + st), 64);
+            if (v <= x0) lo += st;
+        }
+        const uint64_t oc = __shfl(oj, (int)lo, 64), onx = __shfl(oj, (int)min(lo + 1, 63u), 64);
+        const uint64_t on = lo < 63 ? onx : ~0ull;  // lo <= 61 for K >= 16
+        if (x0 >= lim) continue;
+        const uint64_t c = c0 + lo;
+        const bool two = on < x0 + 16 && c + 1 < nc;  // the next contig starts inside these 16 bytes
+        // per contig q of the lane (c, and c + 1 when two): head window H (head base rel0 + b at
+        // bits 2(15 - b)), chunk window Bw (first-chunk base rel0 - K + b at bits 2b), rel0 = x0 - o_q
+        auto windows = [&](uint64_t q, int64_t rel0, uint32_t& H, uint32_t& Bw, int64_t& L, int64_t& A) {
+            const uint64_t w0 = starts[q * W], w1 = W == 2 ? starts[q * W + 1] : 0;
+            const Key k = slot_key(w0, w1, p);
+            const uint64_t vl = k.lo | (k.hi << 62), vh = k.hi >> 2;  // V as 128 bits
+            H = rel0 < K ? bits32(vh, vl, 2 * (K - 16 - (int)max<int64_t>(rel0, -32))) : 0u;
+            L = (int64_t)K + clen[q];
+            A = min<int64_t>((int64_t)slen[q] - 1, CHUNK_BASES);
+            const int64_t j0 = rel0 - K;
+            Bw = 0;
+            if (j0 + 16 > 0 && j0 < A) {
+                const int64_t w = j0 > 0 ? j0 / 32 : 0;
+                const uint64_t* cw = chunk_data + q * CHUNK_WORDS + w;
+                const uint64_t d0 = cw[0], d1 = w + 1 < CHUNK_WORDS ? cw[1] : 0ull;
+                Bw = bits32(d1, d0, (int)(2 * (j0 - 32 * w)));
+            }
+        };
+        uint32_t Hc, Bc, Hn = 0, Bn = 0;
+        int64_t Lc, Ac, Ln = 0, An = 0;
+        const int64_t rc = (int64_t)(x0 - oc), rn = (int64_t)x0 - (int64_t)on;
+        windows(c, rc, Hc, Bc, Lc, Ac);
+        if (two) windows(c + 1, rn, Hn, Bn, Ln, An);
+        const uint32_t nb = on - x0 < 16 && two ? (uint32_t)(on - x0) : 16u;  // bytes of contig c
+        uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b) {
+            const bool nx = b >= nb;
+            const int64_t rel = (nx ? rn : rc) + b;
+            const uint32_t hc = ((nx ? Hn : Hc) >> (2 * (15 - b))) & 3u;
+            const uint32_t bc = ((nx ? Bn : Bc) >> (2 * b)) & 3u;
+            const uint32_t code = rel < K ? hc : bc;
+            const uint32_t ch = rel == (nx ? Ln : Lc) - 1 ? (uint32_t)'\n' : (0x54474341u >> (8 * code)) & 0xFFu;
+            v[b >> 2] |= ch << (8 * (b & 3));
+        }
+        if (x0 + 16 <= lim) {
+            *reinterpret_cast<uint4*>(out + x0) = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+            for (uint32_t b = 0; x0 + b < lim; ++b) out[x0 + b] = (char)(v[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* chunk_data,
                                                         const uint32_t* owner, const uint32_t* seq,
                                                         const unsigned long long* ctr,
                                                         uint64_t chunk_cap, uint64_t n_first,
                                                         const uint32_t* len,
-                                                        const uint64_t* off, char* out, uint64_t cap) {
+                                                        const uint64_t* off, char* out, uint64_t cap,
+                                                        uint64_t ch_begin = 0) {
     // Chunks [0, n_first) are the contigs' own first chunks; the extra-chunk count is only known
     // on the device (walker allocation head), so the grid is sized for the capacity and bounded
     // here.
     const uint64_t nchunks = min(n_first + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
     const uint64_t nwords = nchunks * CHUNK_WORDS;
-    for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nwords;
+    for (uint64_t t = ch_begin * CHUNK_WORDS + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nwords;
          t += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t ch = t / CHUNK_WORDS;
         const uint32_t w = (uint32_t)(t % CHUNK_WORDS);
@@ -869,9 +974,33 @@ hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t
     return hipGetLastError();
 }
 
+// The line writer for the contigs' heads, first chunks and newlines (K >= 16, line_first sized
+// out_bytes / LINE_BYTES + 2 entries); false: the heads writer instead.
+static bool launch_lines(const KParams& p, const WalkBuffers& wb, const uint32_t* clen, const uint64_t* offsets,
+                         char* out, const unsigned long long* ctr, hipStream_t s, uint64_t cap, uint32_t* line_first,
+                         uint64_t out_bytes) {
+    const uint64_t nc = wb.n_starts;
+    if (!line_first || p.K < (int)LINE_KMIN) return false;
+    const unsigned gf = (unsigned)hmin((nc + BLOCK - 1) / BLOCK, 8192);
+    k_line_first<<<gf, BLOCK, 0, s>>>(p.K, clen, nc, offsets, ctr, cap, line_first);
+    const uint64_t waves = (min(out_bytes, cap) + LINE_BYTES - 1) / LINE_BYTES;
+    const unsigned gl = (unsigned)hmin((waves + BLOCK / 64 - 1) / (BLOCK / 64) + 1, 8192);
+    if (p.W == 1)
+        with_kt<1>(p.K, [&](auto kt) {
+            k_write_lines<1, decltype(kt)::value><<<gl, BLOCK, 0, s>>>(p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data,
+                                                                      offsets, line_first, ctr, out, cap);
+        });
+    else
+        with_kt<2>(p.K, [&](auto kt) {
+            k_write_lines<2, decltype(kt)::value><<<gl, BLOCK, 0, s>>>(p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data,
+                                                                      offsets, line_first, ctr, out, cap);
+        });
+    return true;
+}
+
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
                               uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s,
-                              int phases) {
+                              int phases, uint32_t* line_first, uint64_t out_bytes) {
     const uint64_t nc = wb.n_starts;
     if (nc == 0) return hipSuccess;
     if (phases & MAT_SCAN) {
@@ -881,15 +1010,20 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
     }
     if (!(phases & MAT_WRITE)) return hipSuccess;
     const uint64_t cap = wb.text_cap ? wb.text_cap : ~0ull;
-    const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
-    if (p.W == 1)
-        k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
-    else
-        k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
+    const bool lines = launch_lines(p, wb, wb.contig_len, offsets, out, ctr, s, cap, line_first, out_bytes);
+    if (!lines) {
+        const unsigned gh = (unsigned)hmin((nc * 16 + BLOCK - 1) / BLOCK, 65536);  // 16 lanes per contig
+        if (p.W == 1)
+            k_write_heads<1><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
+        else
+            k_write_heads<2><<<gh, BLOCK, 0, s>>>(p, wb.starts, nc, wb.contig_len, offsets, out, cap);
+    }
+    // chunks the line writer does not cover: every contig's chunks past its first
+    const uint64_t cb = lines ? nc : 0;
     const unsigned gc =
-        (unsigned)hmin((wb.chunk_cap * CHUNK_WORDS + BLOCK - 1) / BLOCK, 8192);
+        (unsigned)hmin(((wb.chunk_cap - min(cb, wb.chunk_cap)) * CHUNK_WORDS + BLOCK - 1) / BLOCK + 1, 8192);
     k_write_chunks<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr,
-                                        wb.chunk_cap, nc, wb.contig_len, offsets, out, cap);
+                                        wb.chunk_cap, nc, wb.contig_len, offsets, out, cap, cb);
     return hipGetLastError();
 }
 
@@ -1091,21 +1225,19 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
 // Four threads per chunk (words q and q + 4 of it): C3 segments (~100 bases) use ~4 of a chunk's
 // 8 words and C5's ~21M contigs of 2-16 k-mers one, so eight threads per chunk (one per word)
 // mostly load the segment metadata only to find their word unused.
-#ifndef KH_WC_TPC
-#define KH_WC_TPC 4
-#endif
-static constexpr uint32_t WC_TPC = KH_WC_TPC;
+static constexpr uint32_t WC_TPC = 4;  // 1: C3 materialize 0.38 -> 0.41 ms, C5 unchanged (round 5)
 __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_t* chunk_data, const uint32_t* owner,
                                                             const uint32_t* seq, const unsigned long long* ctr,
                                                             uint64_t chunk_cap, uint64_t n_starts,
                                                             const unsigned long long* nsp_dev, uint64_t nsp,
                                                             const uint32_t* seg_len, const uint32_t* seg_contig,
                                                             const uint32_t* seg_off, const uint64_t* off,
-                                                            char* out, uint64_t cap) {
+                                                            char* out, uint64_t cap, uint64_t ch_begin = 0) {
     const uint64_t nseg = n_starts + (nsp_dev ? (uint64_t)*nsp_dev : nsp);
     const uint64_t nchunks = min(nseg + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
     const uint64_t nt = nchunks * WC_TPC;
-    for (uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nt; t += (uint64_t)gridDim.x * BLOCK) {
+    for (uint64_t t = ch_begin * WC_TPC + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nt;
+         t += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t ch = t / WC_TPC;
         const uint32_t q = (uint32_t)(t % WC_TPC);
         const uint32_t g = ch < nseg ? (uint32_t)ch : owner[ch];
@@ -1127,7 +1259,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
 
 hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
                                   uint64_t* offsets, uint64_t* scratch, char* out, unsigned long long* ctr,
-                                  hipStream_t s, int phases) {
+                                  hipStream_t s, int phases, uint32_t* line_first, uint64_t out_bytes) {
     const uint64_t nc = wb.n_starts;
     if (nc == 0) return hipSuccess;
     hipError_t e = hipSuccess;
@@ -1138,11 +1270,14 @@ hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const
     }
     if (!(phases & MAT_WRITE)) return hipSuccess;
     const uint64_t cap = wb.text_cap ? wb.text_cap : ~0ull;
-    if ((e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s, cap)) != hipSuccess) return e;
-    const unsigned gc = (unsigned)hmin((wb.chunk_cap * WC_TPC + BLOCK - 1) / BLOCK, 8192);
+    const bool lines = launch_lines(p, wb, sb.clen, offsets, out, ctr, s, cap, line_first, out_bytes);
+    if (!lines && (e = launch_write_heads(p, wb.starts, nc, sb.clen, offsets, out, s, cap)) != hipSuccess) return e;
+    // chunks the line writer does not cover: splitter segments' and every segment's past its first
+    const uint64_t cb = lines ? nc : 0;
+    const unsigned gc = (unsigned)hmin(((wb.chunk_cap - min(cb, wb.chunk_cap)) * WC_TPC + BLOCK - 1) / BLOCK + 1, 8192);
     k_write_chunks_seg<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr, wb.chunk_cap,
                                             nc, wb.n_splits_dev, wb.n_splits, wb.contig_len, sb.seg_contig,
-                                            sb.seg_off, offsets, out, cap);
+                                            sb.seg_off, offsets, out, cap, cb);
     return hipGetLastError();
 }
 

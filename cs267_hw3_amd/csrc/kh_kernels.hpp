@@ -133,12 +133,15 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
 enum MatPhase : int { MAT_SCAN = 1, MAT_WRITE = 2, MAT_ALL = 3 };
 hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
                                   uint64_t* offsets, uint64_t* scratch, char* out, unsigned long long* ctr,
-                                  hipStream_t s, int phases = MAT_ALL);
+                                  hipStream_t s, int phases = MAT_ALL, uint32_t* line_first = nullptr,
+                                  uint64_t out_bytes = 0);
 
 // Contig bytes: offsets = exclusive scan of (K + len) (K + len-1 bases + '\n'), then write chars.
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
                               uint64_t* scratch, char* out, unsigned long long* ctr, hipStream_t s,
-                              int phases = MAT_ALL);
+                              int phases = MAT_ALL, uint32_t* line_first = nullptr, uint64_t out_bytes = 0);
+// line_first: LINE_WORDS(out_bytes) uint32 entries for the line writer (K >= 16), or nullptr
+inline uint64_t line_first_words(uint64_t out_bytes) { return out_bytes / 1024 + 2; }
 
 // ---- migrating-walker rounds (kh_mwalk.hip) -------------------------------------------------
 // message: MSG_WORDS words [key.hi, key.lo, partial word, idx << 32 | bases appended,
