@@ -1780,10 +1780,10 @@ template <int Unused = 0>
 __global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint32_t RC, int slack16, int sample_shift,
                                                   const uint32_t* counts, uint32_t* hot, uint32_t* hot_list,
                                                   unsigned long long* ctr, int allow_new, int list_new, uint32_t Tfix,
-                                                  int ct = CT_HOT) {
+                                                  int ct = CT_HOT, int both = 0) {
     const uint32_t NR = nreg(p);
     const uint32_t r = blockIdx.x * 256u + threadIdx.x;
-    bool h = false, hn = false;
+    bool h = false, hn = false, h2 = false;
     if (r < NR) {
         // equal ranges: what the slice holds; balanced bounds (Tfix): what the largest slice holds
         const uint32_t S = Tfix ? Tfix : (uint32_t)(region_lo(r + 1, cap, p) - region_lo(r, cap, p));
@@ -1795,12 +1795,23 @@ __global__ __launch_bounds__(256) void k_hot_mark(KParams p, uint64_t cap, uint3
                                        : counts[r] > T;
         hn = allow_new && !old && over;
         h = old || hn;
+        if (both) {  // the exact mark: an overfull region is marked at both levels (see hot_fixup)
+            const bool old2 = (hot[HOT_LEVEL_WORDS + (r >> 5)] >> (r & 31u)) & 1u;
+            hn = allow_new && over && !(old && old2);
+            h2 = old2 || (allow_new && over);
+        }
     }
     const uint64_t m = __ballot(h);
     const uint32_t lane = lane_id();
     const uint32_t r0 = r - lane;  // the wave's 64 regions: two bitmap words
     if (r0 < NR && (lane == 0 || lane == 32)) hot[(r0 >> 5) + (lane >> 5)] = (uint32_t)(m >> lane);
     if (lane == 0 && m) atomicAdd(&ctr[ct], (unsigned long long)__popcll(m));
+    if (both) {
+        const uint64_t m2 = __ballot(h2);
+        if (r0 < NR && (lane == 0 || lane == 32))
+            hot[HOT_LEVEL_WORDS + (r0 >> 5) + (lane >> 5)] = (uint32_t)(m2 >> lane);
+        if (lane == 0 && m2) atomicAdd(&ctr[CT_HOT2], (unsigned long long)__popcll(m2));
+    }
     const unsigned long long i = wave_reserve(&ctr[CT_HOTNEW], list_new && hn);
     if (list_new && hn) hot_list[i] = r;
 }
@@ -1904,8 +1915,15 @@ static void hot_fixup(const KParams& p, uint64_t cap, uint64_t n, uint32_t RC, b
                       hipStream_t s) {
     KParams q = p;
     q.hot = B.hot;
+    // Exact counts after pass 2: a region its window or slice cannot hold is marked at both levels —
+    // level 1 remaps its own keys (a hot family the sample missed), level 2 spreads the keys the
+    // level-1 remap sent into it (a family sharing its neighbour window too, which the sampled
+    // level-2 mark missed: C5F had ~37K such keys left to the global CAS insert, whose probe runs
+    // through full slices then made the insert 1.1 ms and the walk's lookups of them ~3 ms).
+    // Then the newly marked regions' words are re-placed.
+    (void)hipMemsetAsync(ctr + CT_HOT2, 0, 8, s);
     k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 0, B.rcnt, B.hot, B.hot_list, ctr,
-                                                     allow_new ? 1 : 0, 1, balanced_T(p, cap, n));
+                                                     allow_new ? 1 : 0, 1, balanced_T(p, cap, n), CT_HOT, 1);
     k_hot_gather<W><<<1024, 256, 0, s>>>(RC, B.rcnt, B.hot_list, B.buf2, B.overflow, ovf_cap, ctr, stats);
     k_ovf_scatter<W><<<2048, 256, 0, s>>>(q, RC, B.rcnt, B.overflow, ovf_cap, B.buf2, B.buf1, ovf2_cap, ctr, stats);
 }

@@ -219,6 +219,13 @@ struct LaneOut {
     uint64_t n_first;        // = number of contigs
 };
 
+// Word w of chunk ch, word-major: word w of every chunk together, so the first words of consecutive
+// contigs are adjacent (the line writer reads 8 B per short contig instead of its 64-B chunk; the
+// walker's first-word stores of a wave's 64 contigs fill whole lines).
+__device__ __forceinline__ uint64_t chunk_word(uint64_t ch, uint32_t w, uint64_t chunk_cap) {
+    return (uint64_t)w * chunk_cap + ch;
+}
+
 // Append base `b` as base number `steps` of contig c (2 bits, 32 per word, 8 words per chunk).
 __device__ __forceinline__ void append_base(const LaneOut& o, uint64_t c, uint32_t b, uint32_t& steps,
                                             uint32_t& chunk, uint64_t& buf, unsigned long long* ctr,
@@ -236,7 +243,7 @@ __device__ __forceinline__ void append_base(const LaneOut& o, uint64_t c, uint32
     }
     buf |= (uint64_t)b << (2 * (steps & 31));
     if ((steps & 31) == 31) {
-        if (chunk < o.chunk_cap) o.chunk_data[(uint64_t)chunk * CHUNK_WORDS + ((steps >> 5) & 7)] = buf;
+        if (chunk < o.chunk_cap) o.chunk_data[chunk_word(chunk, (steps >> 5) & 7, o.chunk_cap)] = buf;
         buf = 0;
     }
     ++steps;
@@ -260,7 +267,7 @@ __device__ __forceinline__ void append_run(const LaneOut& o, uint64_t c, uint64_
     buf |= piece << (2 * (steps & 31));
     steps += m;
     if ((steps & 31) == 0) {
-        if (chunk < o.chunk_cap) o.chunk_data[(uint64_t)chunk * CHUNK_WORDS + (((steps - 1) >> 5) & 7)] = buf;
+        if (chunk < o.chunk_cap) o.chunk_data[chunk_word(chunk, ((steps - 1) >> 5) & 7, o.chunk_cap)] = buf;
         buf = 0;
     }
 }
@@ -292,7 +299,7 @@ __device__ __forceinline__ void finish_contig(const LaneOut& o, uint64_t c, uint
                                               uint64_t buf) {
     o.contig_len[c] = steps + 1;
     if ((steps & 31) && chunk < o.chunk_cap)
-        o.chunk_data[(uint64_t)chunk * CHUNK_WORDS + ((steps >> 5) & 7)] = buf;
+        o.chunk_data[chunk_word(chunk, (steps >> 5) & 7, o.chunk_cap)] = buf;
 }
 
 __device__ __forceinline__ uint64_t walk_splits(const WalkBuffers& wb) {
@@ -793,71 +800,110 @@ template <int W, int KT>
 __global__ __launch_bounds__(BLOCK) void k_write_lines(KParams p_in, const uint64_t* __restrict__ starts, uint64_t nc,
                                                        const uint32_t* __restrict__ clen,
                                                        const uint32_t* __restrict__ slen,
-                                                       const uint64_t* __restrict__ chunk_data,
+                                                       const uint64_t* __restrict__ chunk_data, uint64_t chunk_cap,
                                                        const uint64_t* __restrict__ off,
                                                        const uint32_t* __restrict__ first,
-                                                       const unsigned long long* ctr, char* out, uint64_t cap) {
+                                                       const unsigned long long* ctr, char* __restrict__ out,
+                                                       uint64_t cap) {
     const KParams p = specialize<KT>(p_in);
     const uint64_t lim = min((uint64_t)ctr[CT_OUT_BYTES], cap);
     const uint32_t lane = lane_id();
     const uint64_t nblk = (lim + LINE_BYTES - 1) / LINE_BYTES;
     const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
     const int K = p.K;
-    for (uint64_t blk = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / 64; blk < nblk; blk += waves) {
-        const uint64_t B0 = blk * LINE_BYTES, x0 = B0 + 16u * lane;
-        const uint64_t c0 = first[blk];
-        const uint64_t oj = c0 + lane < nc ? off[c0 + lane] : ~0ull;
-        // the lane's contig: the last of the wave's 64 whose text starts at or before x0
-        uint32_t lo = 0;
+    // U blocks per iteration, each stage's loads issued for all U before any is used: a block is a
+    // chain of three dependent loads (first -> offsets -> the lane's contig), so one block at a time
+    // left the kernel latency-bound (C5: ~160 blocks per wave)
+    constexpr int U = 2;
+    for (uint64_t blk0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / 64; blk0 < nblk; blk0 += U * waves) {
+        uint64_t c0[U], oj[U];
 #pragma unroll
-        for (uint32_t st = 32; st > 0; st >>= 1) {
-            const uint64_t v = __shfl(oj, (int)(lo + st), 64);
-            if (v <= x0) lo += st;
+        for (int u = 0; u < U; ++u) c0[u] = first[min(blk0 + u * waves, nblk - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) oj[u] = c0[u] + lane < nc ? off[c0[u] + lane] : ~0ull;
+        uint64_t x0[U], c[U], on[U];
+        int64_t rc[U];
+        uint32_t nb[U], hb[U];
+        bool live[U], two[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t blk = blk0 + u * waves;
+            x0[u] = blk * LINE_BYTES + 16u * lane;
+            // the lane's contig: the last of the wave's 64 whose text starts at or before x0
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t st = 32; st > 0; st >>= 1) {
+                const uint64_t v = __shfl(oj[u], (int)(lo + st), 64);
+                if (v <= x0[u]) lo += st;
+            }
+            const uint64_t oc = __shfl(oj[u], (int)lo, 64), onx = __shfl(oj[u], (int)min(lo + 1, 63u), 64);
+            on[u] = lo < 63 ? onx : ~0ull;  // lo <= 61 for K >= 16
+            live[u] = blk < nblk && x0[u] < lim;
+            c[u] = c0[u] + lo;
+            two[u] = on[u] < x0[u] + 16 && c[u] + 1 < nc;  // the next contig starts inside these 16 bytes
+            rc[u] = (int64_t)(x0[u] - oc);
+            nb[u] = two[u] ? (uint32_t)(on[u] - x0[u]) : 16u;  // bytes of contig c
+            hb[u] = rc[u] >= K ? 0u : (uint32_t)min<int64_t>(K - rc[u], nb[u]);
         }
-        const uint64_t oc = __shfl(oj, (int)lo, 64), onx = __shfl(oj, (int)min(lo + 1, 63u), 64);
-        const uint64_t on = lo < 63 ? onx : ~0ull;  // lo <= 61 for K >= 16
-        if (x0 >= lim) continue;
-        const uint64_t c = c0 + lo;
-        const bool two = on < x0 + 16 && c + 1 < nc;  // the next contig starts inside these 16 bytes
-        // per contig q of the lane (c, and c + 1 when two): head window H (head base rel0 + b at
-        // bits 2(15 - b)), chunk window Bw (first-chunk base rel0 - K + b at bits 2b), rel0 = x0 - o_q
-        auto windows = [&](uint64_t q, int64_t rel0, uint32_t& H, uint32_t& Bw, int64_t& L, int64_t& A) {
-            const uint64_t w0 = starts[q * W], w1 = W == 2 ? starts[q * W + 1] : 0;
+        // 2-bit codes of the 16 bytes (byte b at bits 2b), then 4 characters per v_perm_b32: the
+        // selector bytes are codes (0-3: "ACGT") or 4 ('\n'). Contig c holds bytes [0, nb): head
+        // bases [0, hb), then first-chunk bases (bytes past the chunk are the chunk writer's), '\n'
+        // at nl; contig c + 1 bytes [nb, 16), all head bases (nb >= 1, 16 - nb < K).
+        auto head_low = [&](uint64_t w0, uint64_t w1, int64_t rel0) {  // head base rel0 + b at bits 2b
             const Key k = slot_key(w0, w1, p);
             const uint64_t vl = k.lo | (k.hi << 62), vh = k.hi >> 2;  // V as 128 bits
-            H = rel0 < K ? bits32(vh, vl, 2 * (K - 16 - (int)max<int64_t>(rel0, -32))) : 0u;
-            L = (int64_t)K + clen[q];
-            A = min<int64_t>((int64_t)slen[q] - 1, CHUNK_BASES);
-            const int64_t j0 = rel0 - K;
-            Bw = 0;
-            if (j0 + 16 > 0 && j0 < A) {
-                const int64_t w = j0 > 0 ? j0 / 32 : 0;
-                const uint64_t* cw = chunk_data + q * CHUNK_WORDS + w;
-                const uint64_t d0 = cw[0], d1 = w + 1 < CHUNK_WORDS ? cw[1] : 0ull;
-                Bw = bits32(d1, d0, (int)(2 * (j0 - 32 * w)));
-            }
+            uint32_t r = __builtin_bitreverse32(bits32(vh, vl, 2 * (K - 16 - (int)rel0)));
+            return ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);  // 2-bit groups reversed
         };
-        uint32_t Hc, Bc, Hn = 0, Bn = 0;
-        int64_t Lc, Ac, Ln = 0, An = 0;
-        const int64_t rc = (int64_t)(x0 - oc), rn = (int64_t)x0 - (int64_t)on;
-        windows(c, rc, Hc, Bc, Lc, Ac);
-        if (two) windows(c + 1, rn, Hn, Bn, Ln, An);
-        const uint32_t nb = on - x0 < 16 && two ? (uint32_t)(on - x0) : 16u;  // bytes of contig c
-        uint32_t v[4] = {0, 0, 0, 0};
+        uint64_t kc0[U], kc1[U], kn0[U], kn1[U], d0[U], d1[U];
+        uint32_t cl[U], sl[U];
 #pragma unroll
-        for (uint32_t b = 0; b < 16; ++b) {
-            const bool nx = b >= nb;
-            const int64_t rel = (nx ? rn : rc) + b;
-            const uint32_t hc = ((nx ? Hn : Hc) >> (2 * (15 - b))) & 3u;
-            const uint32_t bc = ((nx ? Bn : Bc) >> (2 * b)) & 3u;
-            const uint32_t code = rel < K ? hc : bc;
-            const uint32_t ch = rel == (nx ? Ln : Lc) - 1 ? (uint32_t)'\n' : (0x54474341u >> (8 * code)) & 0xFFu;
-            v[b >> 2] |= ch << (8 * (b & 3));
+        for (int u = 0; u < U; ++u) {  // every load of both blocks before any use
+            const uint64_t cc = live[u] ? c[u] : 0, cn = live[u] && two[u] ? c[u] + 1 : cc;
+            kc0[u] = starts[cc * W];
+            kc1[u] = W == 2 ? starts[cc * W + 1] : 0;
+            kn0[u] = starts[cn * W];
+            kn1[u] = W == 2 ? starts[cn * W + 1] : 0;
+            cl[u] = clen[cc];
+            sl[u] = slen[cc];
+            const int64_t j0 = rc[u] - K;
+            const uint32_t w = j0 > 0 ? (uint32_t)min<int64_t>(j0 / 32, CHUNK_WORDS - 1) : 0u;
+            const bool need = live[u] && hb[u] < nb[u] && j0 < CHUNK_BASES;
+            d0[u] = need ? chunk_data[chunk_word(cc, w, chunk_cap)] : 0ull;
+            d1[u] = need && w + 1 < CHUNK_WORDS ? chunk_data[chunk_word(cc, w + 1, chunk_cap)] : 0ull;
         }
-        if (x0 + 16 <= lim) {
-            *reinterpret_cast<uint4*>(out + x0) = make_uint4(v[0], v[1], v[2], v[3]);
-        } else {
-            for (uint32_t b = 0; x0 + b < lim; ++b) out[x0 + b] = (char)(v[b >> 2] >> (8 * (b & 3)));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;
+            uint32_t codes = hb[u] ? head_low(kc0[u], kc1[u], rc[u]) : 0u;
+            if (hb[u] < nb[u]) {  // first-chunk bases j0 + b
+                const int64_t A = min<int64_t>((int64_t)sl[u] - 1, CHUNK_BASES), j0 = rc[u] - K;
+                if (j0 + 16 > 0 && j0 < A) {
+                    const uint32_t w = j0 > 0 ? (uint32_t)(j0 / 32) : 0u;
+                    const uint32_t bw = bits32(d1[u], d0[u], (int)(2 * (j0 - 32 * (int64_t)w)));
+                    const uint32_t mh = hb[u] ? 0xFFFFFFFFu >> (32 - 2 * hb[u]) : 0u;
+                    codes = (codes & mh) | (bw & ~mh);
+                }
+            }
+            if (two[u]) {
+                const uint32_t mn = 0xFFFFFFFFu << (2 * nb[u]);
+                codes = (codes & ~mn) | ((head_low(kn0[u], kn1[u], 0) << (2 * nb[u])) & mn);
+            }
+            const int64_t nl = (int64_t)K + cl[u] - 1 - rc[u];
+            uint32_t v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t x = (codes >> (8 * i)) & 0xFFu;
+                uint32_t sel = (x & 3u) | ((x << 6) & 0x300u) | ((x << 12) & 0x30000u) | ((x << 18) & 0x3000000u);
+                if (nl >= 4 * i && nl < 4 * i + 4 && nl < nb[u])
+                    sel = (sel & ~(0xFFu << (8 * (nl - 4 * i)))) | (4u << (8 * (nl - 4 * i)));
+                v[i] = __builtin_amdgcn_perm(0x0A0A0A0Au, 0x54474341u, sel);
+            }
+            if (x0[u] + 16 <= lim) {
+                *reinterpret_cast<uint4*>(out + x0[u]) = make_uint4(v[0], v[1], v[2], v[3]);
+            } else {
+                for (uint32_t b = 0; x0[u] + b < lim; ++b) out[x0[u] + b] = (char)(v[b >> 2] >> (8 * (b & 3)));
+            }
         }
     }
 }
@@ -884,7 +930,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* c
         if (j0 >= app) continue;
         const uint32_t cntb = (uint32_t)min<uint64_t>(32, app - j0);
         if (off[c] + K + j0 + cntb > cap) continue;
-        const uint64_t word = chunk_data[t];
+        const uint64_t word = chunk_data[chunk_word(ch, w, chunk_cap)];
         char* o = out + off[c] + K + j0;
         store_chars(o, cntb, [&](uint32_t i) { return codes4_chars((uint32_t)(word >> (8 * i)) & 0xFFu); });
     }
@@ -988,12 +1034,12 @@ static bool launch_lines(const KParams& p, const WalkBuffers& wb, const uint32_t
     if (p.W == 1)
         with_kt<1>(p.K, [&](auto kt) {
             k_write_lines<1, decltype(kt)::value><<<gl, BLOCK, 0, s>>>(p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data,
-                                                                      offsets, line_first, ctr, out, cap);
+                                                                      wb.chunk_cap, offsets, line_first, ctr, out, cap);
         });
     else
         with_kt<2>(p.K, [&](auto kt) {
             k_write_lines<2, decltype(kt)::value><<<gl, BLOCK, 0, s>>>(p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data,
-                                                                      offsets, line_first, ctr, out, cap);
+                                                                      wb.chunk_cap, offsets, line_first, ctr, out, cap);
         });
     return true;
 }
@@ -1250,7 +1296,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
         if (off[c] + K + seg_off[g] + cb + cnt > cap) continue;  // past the buffer: not written
         char* o = out + off[c] + K + seg_off[g] + cb;
         for (uint32_t w = q; 32 * w < cnt; w += WC_TPC) {
-            const uint64_t word = chunk_data[ch * CHUNK_WORDS + w];
+            const uint64_t word = chunk_data[chunk_word(ch, w, chunk_cap)];
             store_chars(o + 32 * w, min(32u, cnt - 32 * w),
                         [&](uint32_t i) { return codes4_chars((uint32_t)(word >> (8 * i)) & 0xFFu); });
         }
