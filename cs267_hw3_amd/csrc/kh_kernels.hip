@@ -346,13 +346,10 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
     Key k{0, 0};
     uint32_t fwd = 0, steps = 0, chunk = 0;
     uint32_t nrec = 0;  // the last record's successor run (head-record index + 1 in its region)
-    // look up key k: s = its home slot (the hit may carry a head-record index)
-    auto lookup = [&]() {
-        const Place pl = place(k, p);
-        reg = pl.r;
-        s = home_of(pl, cap, p);
-        resolved = false;
-    };
+    // k needs its placement this iteration: its home slot for a lookup, or its region for the
+    // record the last record named. One place() site for both (and for a new walker's own start
+    // k-mer): a wave whose lanes take different paths runs the minimizer scan once, not per path.
+    bool do_place = false;
     while (true) {
         while (true) {
             const bool need = !active && !done;
@@ -415,11 +412,8 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                         nrec = 0;
                         active = true;
                         entry = chains;
-                        if (chains) {
-                            lookup();  // its own slot tells whether a record covers its run
-                        } else {
-                            resolved = true;
-                        }
+                        resolved = !chains;  // with chains: its own slot tells whether a record covers its run
+                        do_place = chains;
                     } else {
                         done = true;
                     }
@@ -443,15 +437,21 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                 wb.seg_key[2 * c] = k.hi;
                 wb.seg_key[2 * c + 1] = k.lo;
                 active = false;
-            } else if (nrec) {
-                // the record named the run that starts at k (k_rec_succ): read it, no probe
-                reg = place(k, p).r;
-                s = WQ_REC | ((uint64_t)reg * wb.hcap + nrec - 1);
-                resolved = false;
-                nrec = 0;
             } else {
-                lookup();
+                do_place = true;
             }
+        }
+        if (do_place) {
+            const Place pl = place(k, p);
+            reg = pl.r;
+            if (nrec) {  // the record named the run that starts at k (k_rec_succ): read it, no probe
+                s = WQ_REC | ((uint64_t)reg * wb.hcap + nrec - 1);
+                nrec = 0;
+            } else {     // look up k: s = its home slot (the hit may carry a head-record index)
+                s = home_of(pl, cap, p);
+            }
+            resolved = false;
+            do_place = false;
         }
         // -- quad loads: a probe reads 4 slots per lane, one per quad member's block; a record
         //    read loads the same 16 B in all 4 lanes (one request) ------------------------------
@@ -1130,7 +1130,9 @@ __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, const uint64
 // those links (k_seg_jump, all segments in parallel); the contig walks the jump pointers only,
 // marking the segments it lands on (k_seg_chain_jump); each marked segment fills in the
 // SEG_JUMP - 1 segments after it (k_seg_fill). Without the flag those three kernels return at once.
-static constexpr uint32_t SEG_SERIAL = 256, SEG_JUMP = 16;
+// C5 (chains of ~3.9K segments): 256 serial + 228 jumps of 16 = ~500 dependent hops (seg_chain 0.36 +
+// chain_jump 0.27 ms); 128 serial + jumps of 64 (~sqrt of the chain) + 64-hop jump and fill passes: ~320
+static constexpr uint32_t SEG_SERIAL = 128, SEG_JUMP = 64;
 __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
     for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < wb.n_starts; c += (uint64_t)gridDim.x * BLOCK) {
@@ -1139,8 +1141,13 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers 
         uint32_t pend = SEG_NONE;
         while (true) {
             // a segment another contig reached first: two walks overlap (malformed input); the
-            // segment text would be written once, so kh_assemble redoes the walk unsegmented
-            if (atomicExch(&sb.seg_contig[g], (uint32_t)c) != SEG_NONE) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+            // segment text would be written once, so kh_assemble redoes the walk unsegmented.
+            // Segment links lead to splitter segments only, so the contig's own start segment is
+            // reached by this thread alone: a plain store (C5: 21M atomics fewer)
+            if (hops == 0)
+                sb.seg_contig[g] = (uint32_t)c;
+            else if (atomicExch(&sb.seg_contig[g], (uint32_t)c) != SEG_NONE)
+                atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
             sb.seg_off[g] = (uint32_t)off;
             off += wb.contig_len[g] - 1;
             g = wb.seg_next[g];

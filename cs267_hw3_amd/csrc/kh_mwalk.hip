@@ -76,6 +76,9 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
         mw.dst[jj] = MW_NONE;
     };
     while (true) {
+        // one minimizer scan site per iteration, for a new message's lookup and for a stepped
+        // walker's next k-mer (owner + region): lanes on either path share one scan, not one each
+        bool scan = false, fresh = false;
         if (!active && j < n_live) {
             const uint64_t* m = mw.in + j * MSG_WORDS;
             k.hi = m[0];
@@ -95,14 +98,13 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             if (st == MW_READREC) {
                 s = WQ_REC | ((m4 >> 32) - 1);
             } else if (probing) {
-                const Place pl = place(k, p);
-                reg = pl.r;
-                s = home_of(pl, cap, p);
+                scan = fresh = true;  // s: its home slot, below
             }
         }
         if (!__any(active)) break;
-        if (active && !probing) {
-            bool fin = false, ovf = false;
+        bool fin = false, ovf = false;
+        const bool stepped = active && !probing;
+        if (stepped) {
             if (st > 3) {
                 if (st != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
                 fin = true;
@@ -123,17 +125,26 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                     ++nrec;
                     fin = true;
                 }
-                // one minimizer scan gives both the owner rank and the placement region
-                const uint32_t mn = fin ? 0u : mini_scan(k, p);
-                const uint32_t mv = fin ? 0u : mini_window(k, mn, p);
-                const uint32_t q = fin ? mw.rank
-                                       : (mw.P == 1 ? 0u
-                                                    : (p.owner_mode == 1 ? owner_key(k, p, mw.P)
-                                                                         : owner_of_mini(mv, mw.P)));
-                const Place pl = place_w(mv, k, p, (int)(mn & 63u));
-                if (fin) {
-                    // finished below (length record, no message)
-                } else if (q != mw.rank || nwords >= MW_RUN_WORDS) {
+                scan = !fin;
+            }
+        }
+        // one minimizer scan gives both the owner rank and the placement region
+        uint32_t mv = 0;
+        Place pl{0u, 0u};
+        if (scan) {
+            const uint32_t mn = mini_scan(k, p);
+            mv = mini_window(k, mn, p);
+            pl = place_w(mv, k, p, (int)(mn & 63u));
+        }
+        if (fresh) {
+            reg = pl.r;
+            s = home_of(pl, cap, p);
+        }
+        if (stepped) {
+            if (scan) {
+                const uint32_t q = mw.P == 1 ? 0u
+                                             : (p.owner_mode == 1 ? owner_key(k, p, mw.P) : owner_of_mini(mv, mw.P));
+                if (q != mw.rank || nwords >= MW_RUN_WORDS) {
                     // to the owner (or to itself, bounding this round's text): a successor record
                     // is only meaningful on this rank
                     uint64_t* o = mw.tmp + j * MSG_WORDS;
@@ -154,8 +165,8 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                     s = (nsucc && nwords + 3 <= MW_RUN_WORDS) ? WQ_REC | ((uint64_t)reg * mw.hcap + nsucc - 1)
                                                               : home_of(pl, cap, p);
                 }
-                nsucc = 0;
             }
+            nsucc = 0;
             if (fin) finish(j);
             if (fin || ovf) {
                 mw.nrec[j] = (uint8_t)nrec;

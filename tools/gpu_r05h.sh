@@ -1,0 +1,16 @@
+#!/bin/bash
+# Full GPU suite, then C3 / C5 / C5H / C2 benches and the forced one-rank sharded line. ON the GPU box.
+set -eo pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+( while true; do sleep 50; date >> gpurun_out/heartbeat.log; done ) &
+HB=$!
+trap 'kill $HB' EXIT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --durations=8 --timeout 600 --timeout-method thread \
+  > gpurun_out/t_gpu.log 2>&1
+for w in c3 c5 c5h c2; do
+  AB_ARGS="--workload $w" timeout -k 10 300 bash tools/ab_libs.sh .ab/prev/libkmerhash_amd.so >> gpurun_out/ab_r05h.txt 2>&1
+done
+KH_BENCH_FORCE_DIST=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+  --master-addr 127.0.0.1 --master-port 29544 bench.py --gpus 1 --no-cpu --e2e-steps 0 --steps 5 --warmup 2 \
+  > gpurun_out/b_dist.log 2>&1
