@@ -1080,10 +1080,21 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
 // dependent steps on its critical path instead of L (C5 chains of 10^6 k-mers;
 // C2 chains of ~800 walked by only ~13 K lanes). Afterwards each segment's successor is looked
 // up in a small splitter table and each contig's chain of segments is followed once.
+// The splitter table holds 2x the walked splitters (+64): sized on the device from the walked count
+// (C3: 49K of the 780K collected, whose bound sizes the allocation), so it stays in L2.
+__device__ __forceinline__ uint64_t stab_cap(const WalkBuffers& wb, uint64_t cap2) {
+    return min(cap2, 2 * walk_splits(wb) + 64);
+}
+__global__ __launch_bounds__(BLOCK) void k_stab_init(WalkBuffers wb, uint64_t* stab, uint64_t cap2_max) {
+    const uint64_t cap2 = stab_cap(wb, cap2_max);
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < cap2; i += (uint64_t)gridDim.x * BLOCK)
+        stab[2 * i] = EMPTY;
+}
 __global__ __launch_bounds__(BLOCK) void k_stab_build(KParams p, WalkBuffers wb, uint64_t* stab, uint32_t* id,
-                                                      uint64_t cap2) {
+                                                      uint64_t cap2_max) {
     const uint64_t* splits = wb.splits;
     const uint64_t nsp = walk_splits(wb);
+    const uint64_t cap2 = stab_cap(wb, cap2_max);
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nsp; i += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t w0 = splits[i * p.W], w1 = p.W == 2 ? splits[i * p.W + 1] : 0;
         const Key k = slot_key(w0, w1, p);
@@ -1102,8 +1113,9 @@ __global__ __launch_bounds__(BLOCK) void k_stab_build(KParams p, WalkBuffers wb,
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, const uint64_t* stab, const uint32_t* id,
-                                                    uint64_t cap2, unsigned long long* stats) {
+                                                    uint64_t cap2_max, unsigned long long* stats) {
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
+    const uint64_t cap2 = stab_cap(wb, cap2_max);
     for (uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; g < nseg; g += (uint64_t)gridDim.x * BLOCK) {
         if (wb.seg_next[g] != SEG_AT_SPLIT) continue;
         const Key k{wb.seg_key[2 * g], wb.seg_key[2 * g + 1]};
@@ -1254,8 +1266,8 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
                            unsigned long long* stats, hipStream_t s) {
     const uint64_t nseg = wb.n_starts + wb.n_splits;
     if (nseg == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(sb.stab, 0xff, sb.cap2 * 16, s);
-    if (e != hipSuccess) return e;
+    k_stab_init<<<(unsigned)hmin((sb.cap2 + BLOCK - 1) / BLOCK, 2048), BLOCK, 0, s>>>(wb, sb.stab, sb.cap2);
+    hipError_t e;
     if ((e = hipMemsetAsync(sb.seg_contig, 0xff, nseg * 4, s)) != hipSuccess) return e;
     if (wb.n_splits)
         k_stab_build<<<(unsigned)hmin((wb.n_splits + BLOCK - 1) / BLOCK, 4096), BLOCK, 0, s>>>(

@@ -365,6 +365,27 @@ def test_gpu_splitters_off_equals_on(monkeypatch):
     assert texts[0] == texts[1] == g.truth()
 
 
+# ---- the line writer (k_write_lines, K >= 16; K < 16 keeps the heads writer) ------------------
+# 1 KiB of text per wave: the shortest contigs (single k-mers, K + 1 bytes) put the most contig
+# starts in one KiB (62 at K = 16) and a contig boundary in most 16-B lanes; contigs past their first
+# 256-base chunk leave bytes to the chunk writer (splitters off: extra chunks; dense splitters:
+# splitter segments as well); the text's last vector is partial.
+@pytest.mark.parametrize("k,n,lmin,lmax,single", [
+    (15, 200_000, 1, 40, 40), (16, 200_000, 1, 40, 40), (17, 200_000, 1, 4, 60),
+    (16, 300_000, 200, 900, 0), (51, 300_000, 1, 3, 50), (60, 400_000, 250, 700, 5),
+])
+@pytest.mark.parametrize("bits", ["0", "3", None])
+def test_gpu_line_writer_vs_oracle(monkeypatch, k, n, lmin, lmax, single, bits):
+    if bits is not None:
+        monkeypatch.setenv("KH_SPLIT_BITS", bits)
+    g = kh.SyntheticKmers(k, n, lmin, lmax, single, seed=k * 11 + lmin)
+    recs = g.records()
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0 and want == g.truth()
+    _, got, gnc = run(k, recs)
+    assert gnc == nc and got == want
+
+
 # ---- the region build's two kernels: prefetching (default) and one-region-at-a-time (windows
 # above 12 words per thread, > ~760M k-mers per table; forced here with KH_DEBUG=plain_build) ----
 @pytest.mark.parametrize("build", ["plain_build", ""])
