@@ -40,6 +40,8 @@ class KhStats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+ABI_VERSION = 3  # KH_ABI_VERSION of include/kmer_hash_amd.h
+
 # name -> (restype, argtypes)
 MSG_WORDS = 5  # KH_MSG_WORDS: migrating-walker message
 TEXT_REC_WORDS = 2  # KH_TEXT_REC_WORDS
@@ -164,6 +166,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        if L.kh_abi_version() != ABI_VERSION:  # KhStats and the signatures above are version 3's
+            raise ImportError(f"{LIB_PATH}: ABI version {L.kh_abi_version()}, this binding is "
+                              f"version {ABI_VERSION} (include/kmer_hash_amd.h KH_ABI_VERSION)")
         _lib = L
     return _lib
 

@@ -875,6 +875,7 @@ int kh_assemble_dev(kh_table* t) {
             if (succ_side) KH_HIP(hipEventRecord(t->ev_conv, t->side));
         }
         // three walker blocks per CU for 16-B slots at load <= 0.6, else two (kh_kernels.hip)
+        // (round 5, after the single place() site: 4 / 5 blocks per CU C3 walk 1.40 / 1.43 ms vs 1.16)
         KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, (kp.W == 2 && t->load <= 0.6) ? -3 : -2, t->stream));
         if (succ_side) KH_HIP(hipStreamWaitEvent(t->stream, t->ev_conv, 0));
         KH_HIP(hipEventRecord(t->ev_wk1, t->stream));
