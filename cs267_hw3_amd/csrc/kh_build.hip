@@ -61,6 +61,9 @@ constexpr size_t sort_lds_nb(int tile, int nb) { return (size_t)tile * 16 + tile
 static_assert(sort_lds(WIN_TILE) + 64 <= 160 * 1024, "k_win LDS");
 static constexpr int REC_TILE = 3584;  // records pass 1 (k_win1_rec): two blocks per CU
 static_assert(2 * (sort_lds(REC_TILE) + 64) <= 160 * 1024, "k_win1_rec LDS");
+// records pass 1: 512 threads per block (640 threads over 3840-record tiles, 20 waves per CU
+// instead of 16: C3 8.50 -> 9.07 ms; profiles/r05/ab/ab_rec640.txt)
+static constexpr int REC_TB = 512, REC_TILE_P1 = REC_TILE;
 static uint64_t win_blocks1(uint64_t n) { return (n + (uint64_t)T1 * WIN_TILE - 1) / ((uint64_t)T1 * WIN_TILE); }
 // pass-2 blocks per bucket
 static uint64_t win_G(uint64_t n) {
@@ -1513,6 +1516,10 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
 }
 
 static constexpr size_t WIN_LDS = sort_lds(WIN_TILE);
+// words passes (k_win1 on words, k_win2): 1024 threads (8 words each) instead of 512 (16 each):
+// one 152-KiB block per CU, so the thread count is the CU's whole occupancy (C5H insert 7.39 ->
+// 7.24 ms, routed one-rank step 11.04 -> 10.85, C3 unchanged; profiles/r05/ab/ab_win_passes_1024.txt)
+static constexpr int WIN_TB = 1024;
 
 // pass 1 on words (routed words, or records converted by k_part1_convert); wsplits: collect the
 // splitter k-mers of the words (sharded path)
@@ -1526,14 +1533,15 @@ static hipError_t win1_launch(const KParams& p, const uint64_t* words, uint64_t 
     return with_kt<W>(p.K, [&](auto kt) {
         constexpr int KT = decltype(kt)::value;
         hipError_t e;
+        constexpr int TB = WIN_TB;
         if (wsplits) {
-            if ((e = allow_lds(k_win1<W, 512, true, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
-            k_win1<W, 512, true, WIN_TILE, KT><<<nb, 512, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
-                                                                        ovf_cap, ctr, stats, wsplits, wsplits_cap, ji);
+            if ((e = allow_lds(k_win1<W, TB, true, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
+            k_win1<W, TB, true, WIN_TILE, KT><<<nb, TB, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
+                                                                      ovf_cap, ctr, stats, wsplits, wsplits_cap, ji);
         } else {
-            if ((e = allow_lds(k_win1<W, 512, false, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
-            k_win1<W, 512, false, WIN_TILE, KT><<<nb, 512, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
-                                                                         ovf_cap, ctr, stats, nullptr, 0, ji);
+            if ((e = allow_lds(k_win1<W, TB, false, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
+            k_win1<W, TB, false, WIN_TILE, KT><<<nb, TB, WIN_LDS, s>>>(p, words, n, CAP1, wcnt, B.buf1, B.overflow,
+                                                                       ovf_cap, ctr, stats, nullptr, 0, ji);
         }
         return hipSuccess;
     });
@@ -1562,13 +1570,13 @@ static hipError_t win1_rec_launch(const KParams& p, const uint8_t* recs, uint64_
         return with_kt<W>(p.K, [&](auto kt) {
             constexpr int KT = decltype(kt)::value;
             hipError_t e;
-            if ((e = allow_lds(k_win1_rec<W, 512, TILE, PK, KT>, lds)) != hipSuccess) return e;
-            k_win1_rec<W, 512, TILE, PK, KT><<<(unsigned)grid, 512, lds, s>>>(
+            if ((e = allow_lds(k_win1_rec<W, REC_TB, TILE, PK, KT>, lds)) != hipSuccess) return e;
+            k_win1_rec<W, REC_TB, TILE, PK, KT><<<(unsigned)grid, REC_TB, lds, s>>>(
                 p, recs, n, CAP1, wcnt, B.buf1, start_mask, split_mask, B.overflow, ovf_cap, ctr, stats);
             return hipSuccess;
         });
     };
-    return go(std::integral_constant<int, REC_TILE>{});
+    return go(std::integral_constant<int, REC_TILE_P1>{});
 }
 
 // One-pass route (sharded insert): records -> owner windows, start bits in the same pass.
@@ -1627,8 +1635,8 @@ static hipError_t win2_launch(const KParams& p, const PartBuffers& B, uint64_t n
     return with_kt<W>(p.K, [&](auto kt) {
         constexpr int KT = decltype(kt)::value;
         hipError_t e;
-        if ((e = allow_lds(k_win2<W, 512, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
-        k_win2<W, 512, WIN_TILE, KT><<<(unsigned)(NB1 * G), 512, WIN_LDS, s>>>(p, B.buf1, G, RC, rcnt, B.buf2,
+        if ((e = allow_lds(k_win2<W, WIN_TB, WIN_TILE, KT>, WIN_LDS)) != hipSuccess) return e;
+        k_win2<W, WIN_TB, WIN_TILE, KT><<<(unsigned)(NB1 * G), WIN_TB, WIN_LDS, s>>>(p, B.buf1, G, RC, rcnt, B.buf2,
                                                                               B.overflow, ovf_cap, ctr, stats, CAP1,
                                                                               wcnt);
         return hipSuccess;
