@@ -814,7 +814,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_lines(KParams p_in, const uint6
     // U blocks per iteration, each stage's loads issued for all U before any is used: a block is a
     // chain of three dependent loads (first -> offsets -> the lane's contig), so one block at a time
     // left the kernel latency-bound (C5: ~160 blocks per wave)
-    constexpr int U = 2;
+    constexpr int U = 2;  // 4: C5 text 0.95 -> 1.01 ms, C3 0.30 -> 0.32 (profiles/r05/ab/ab_misc.txt)
     for (uint64_t blk0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / 64; blk0 < nblk; blk0 += U * waves) {
         uint64_t c0[U], oj[U];
 #pragma unroll
@@ -1144,6 +1144,8 @@ __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, const uint64
 // SEG_JUMP - 1 segments after it (k_seg_fill). Without the flag those three kernels return at once.
 // C5 (chains of ~3.9K segments): 256 serial + 228 jumps of 16 = ~500 dependent hops (seg_chain 0.36 +
 // chain_jump 0.27 ms); 128 serial + jumps of 64 (~sqrt of the chain) + 64-hop jump and fill passes: ~320
+// (32 / 64 serial hops: C5 -0.08 / 0 ms but C2 1.24 -> 1.44 / 1.46 ms: C2's ~100-segment contigs then
+// take the jump passes; profiles/r05/ab/ab_misc.txt)
 static constexpr uint32_t SEG_SERIAL = 128, SEG_JUMP = 64;
 __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
