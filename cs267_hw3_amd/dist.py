@@ -677,7 +677,7 @@ class DistributedKmerHashMap:
             self._caps, self._rounds_hint = [], 0
         self._cap_floor = 0
         check_at = self._rounds_hint or self.CHECK_EVERY
-        # rounds without splitter segments (KH_MW_SEGMENTS=0) grow with the longest chain; a
+        # rounds without splitter segments (KH_SPLIT_BITS=0) grow with the longest chain; a
         # walker advances every round it is not held back, so total_kmers bounds them
         limit = self.MAX_ROUNDS if self._splitters else max(self.MAX_ROUNDS, total_kmers + self.MAX_ROUNDS)
         # [in flight, largest per-destination count] of the rounds since the last check

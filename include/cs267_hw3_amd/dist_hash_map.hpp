@@ -348,7 +348,7 @@ public:
         }
         cap_floor_ = 0;
         int check_at = rounds_hint_ ? rounds_hint_ : kCheckEvery;
-        // rounds without splitter segments (KH_MW_SEGMENTS=0) grow with the longest chain; a
+        // rounds without splitter segments (KH_SPLIT_BITS=0) grow with the longest chain; a
         // walker advances every round it is not held back, so total_kmers bounds them
         const uint64_t limit = splitters_ ? (uint64_t)kMaxRounds : std::max<uint64_t>(kMaxRounds, total_kmers + kMaxRounds);
         // [in flight, largest per-destination count] of the rounds since the last check
