@@ -202,7 +202,7 @@ __global__ __launch_bounds__(PB) void k_part1_convert(KParams p_in, const uint8_
         const uint64_t wb = sub + (threadIdx.x & ~63u);
         if ((threadIdx.x & 63) == 0 && wb < b1 && start_mask) start_mask[wb >> 6] = bal;
         if (split_mask) {
-            const uint64_t sb = __ballot(valid && !is_start && is_splitter(key_hash32(k), p));
+            const uint64_t sb = __ballot(valid && !is_start && is_splitter(k, p));
             if ((threadIdx.x & 63) == 0 && wb < b1) split_mask[wb >> 6] = sb;
         }
         if (valid) {
@@ -488,7 +488,7 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const Slice<W>&
         if (win_order(win_bits(y, 0, p)) <= win_order(mw)) return NO_SUCC;
     }
     const uint32_t hy = key_hash32(y);
-    if (is_splitter(hy, p)) return NO_SUCC;
+    if (is_splitter(y, p)) return NO_SUCC;
     // (y holds x's minimizer one window further: j* + 1)
     const uint64_t home = MTOP ? home_in(lo, lo + S, hy) : home_of(place_w(mw, y, p, (int)j + 1), cap, p);
     if (home < lo || home >= lo + S) return NO_SUCC;
@@ -1262,7 +1262,7 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p_in, const uint64_t* __res
             bin[j] = part_region(mini_window(kk, mn, p), kk, p, hot_on, (int)(mn & 63u)) >> (p.rbits - B1);
             const bool live = a[j] != EMPTY;
             // splitter k-mers this shard owns (they head migrating-walk segments, kh_mseg.hip)
-            if (COLLECT && live && ext_bwd(slot_ext(a[j])) != EXT_F && is_splitter(key_hash32(kk), p)) {
+            if (COLLECT && live && ext_bwd(slot_ext(a[j])) != EXT_F && is_splitter(kk, p)) {
                 const uint32_t pos = atomicAdd(scount, 1u);
                 if (pos < WIN_SPLIT_LCAP) {
                     sbuf[pos * W] = a[j];
@@ -1405,7 +1405,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
             if (s0 < n) {  // uniform: one start / splitter word per 64 consecutive records
                 const bool is_start = valid && ext_bwd(ext) == EXT_F;
                 const uint64_t bal = __ballot(is_start);
-                const uint64_t sb = split_mask ? __ballot(valid && !is_start && is_splitter(key_hash32(k), p)) : 0;
+                const uint64_t sb = split_mask ? __ballot(valid && !is_start && is_splitter(k, p)) : 0;
                 const uint64_t wb = s0 + (threadIdx.x & ~63u);
                 if ((threadIdx.x & 63) == 0 && wb < n) {
                     if (start_mask) start_mask[wb >> 6] = bal;
@@ -1417,7 +1417,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
             if (ROUTE) {
                 bin[j] = P == 1 ? 0u
                                 : (p.owner_mode == 1 ? owner_key(k, p, P) : owner_of_mini(mini_window(k, mn, p), P));
-                if (spl && valid && ext_bwd(ext) != EXT_F && is_splitter(key_hash32(k), p))
+                if (spl && valid && ext_bwd(ext) != EXT_F && is_splitter(k, p))
                     atomicAdd(&rspl[bin[j]], 1u);
             } else
                 bin[j] = part_region(mini_window(k, mn, p), k, p, hot_on, (int)(mn & 63u)) >> (p.rbits - B1);

@@ -53,7 +53,7 @@ struct KParams {
     uint64_t v_mask;    // W=1: mask of V (2K bits)
     int M;              // minimizer length (bases): placement region and sharded owner
     int owner_mode;     // sharded owner: 0 = minimizer hash (default), 1 = low key_hash bits
-    int split_bits;     // walk splitters: k-mers with (key_hash32 & (2^split_bits - 1)) == 0 and a
+    int split_bits;     // walk splitters: k-mers passing split_test(k, split_bits) and a
                         // predecessor start extra walkers (0 = off); see kh_kernels.hip k_walk
     uint64_t kmask;     // key bits of (word0 >> 6): hi_mask (W=2) or v_mask (W=1)
     int chain;          // word0 has room for j* and a head-record index (chain links, kh_build.hip)
@@ -412,11 +412,13 @@ KH_HD uint32_t owner_key(Key k, const KParams& p, uint32_t nranks) {
     return owner_of_mini(mini_window(k, mini_scan(k, p), p), nranks);
 }
 
-// Splitter k-mer: cuts long contigs into independently walked segments (sparse ruling set).
-// h = key_hash32 of the k-mer.
-KH_HD bool is_splitter(uint64_t h, const KParams& p) {
-    return p.split_bits && (h & ((1ull << p.split_bits) - 1)) == 0;
-}
+// Splitter k-mer: cuts long contigs into independently walked segments (sparse ruling set). The
+// top `bits` bits of a one-multiply hash of the key's low word are zero (nested in bits, as the
+// walk's density filter needs). One multiply instead of key_hash32's three: the walker tests every
+// k-mer it appends and the records pass every record (key_hash32 was ~7 % of k_win1_rec's VALU).
+KH_HD uint32_t split_hash(Key k) { return ((uint32_t)k.lo ^ (uint32_t)(k.lo >> 32)) * 0x9E3779B1u; }
+KH_HD bool split_test(Key k, int bits) { return bits && split_hash(k) < (1u << (32 - bits)); }
+KH_HD bool is_splitter(Key k, const KParams& p) { return split_test(k, p.split_bits); }
 
 // ---- slot encode/decode ---------------------------------------------------------------
 KH_HD uint64_t slot_w0(Key k, uint32_t ext, const KParams& p) {

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(BLOCK) void k_insert(KParams p, const uint8_t* __re
         const uint64_t wbase = base + (threadIdx.x & ~63u);
         if ((threadIdx.x & 63) == 0 && wbase < n) start_mask[wbase >> 6] = bal;
         if (split_mask) {
-            const uint64_t sb = __ballot(valid && !is_start && is_splitter(key_hash32(k), p));
+            const uint64_t sb = __ballot(valid && !is_start && is_splitter(k, p));
             if ((threadIdx.x & 63) == 0 && wbase < n) split_mask[wbase >> 6] = sb;
         }
         if (valid) {
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
         if (active && resolved) {
             append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
             k = key_next(k, fwd, p);
-            if (is_splitter(key_hash32(k), p)) {
+            if (is_splitter(k, p)) {
                 finish_contig(o, c, steps, chunk, buf);
                 wb.seg_next[c] = SEG_AT_SPLIT;
                 wb.seg_key[2 * c] = k.hi;
@@ -1240,10 +1240,10 @@ __global__ __launch_bounds__(BLOCK) void k_seg_fill(WalkBuffers wb, SegBuffers s
 struct SplitKeepF {
     KParams p;
     const uint64_t* splits;
-    uint64_t mask;
+    int bits;
     __device__ uint64_t operator()(uint64_t i) const {
         const uint64_t w0 = splits[i * p.W], w1 = p.W == 2 ? splits[i * p.W + 1] : 0;
-        return (key_hash32(slot_key(w0, w1, p)) & mask) == 0;
+        return split_test(slot_key(w0, w1, p), bits);
     }
 };
 
@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(BLOCK) void k_filter_splits(SplitKeepF f, uint64_t 
 hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64_t n, int bits, uint64_t* off,
                                 uint64_t* scratch, uint64_t* out, unsigned long long* count, hipStream_t s) {
     if (n == 0) return hipMemsetAsync(count, 0, 8, s);
-    const SplitKeepF f{p, splits, (1ull << bits) - 1};
+    const SplitKeepF f{p, splits, bits};
     hipError_t e = scan_exclusive(f, n, off, scratch, (unsigned long long*)nullptr, count, s);
     if (e != hipSuccess) return e;
     k_filter_splits<<<(unsigned)hmin((n + BLOCK - 1) / BLOCK, 8192), BLOCK, 0, s>>>(f, n, off, out);
@@ -1433,7 +1433,7 @@ __global__ __launch_bounds__(BLOCK) void k_route_own(KParams p_in, const uint8_t
             own[sub + threadIdx.x] = mn;
             const uint32_t q = owner_mn(k, mn, p, P);
             atomicAdd(&h[q], 1u);
-            if (spl && ext_bwd(ext) != EXT_F && is_splitter(key_hash32(k), p)) atomicAdd(&hs[q], 1u);
+            if (spl && ext_bwd(ext) != EXT_F && is_splitter(k, p)) atomicAdd(&hs[q], 1u);
         }
         if (start_mask) {  // kmer_hash.cpp:27-31 start bits, same pass (ROUTE_TILE is 64-aligned)
             const uint64_t bal = __ballot(threadIdx.x < cnt && ext_bwd(ext) == EXT_F);

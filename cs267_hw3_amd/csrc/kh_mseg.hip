@@ -53,7 +53,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_collect(KParams p, const uint64
         const uint64_t c1 = min(c0 + SPLIT_CHUNK, m);
         for (uint64_t i = c0 + threadIdx.x; i < c1; i += BLOCK) {
             const uint64_t w0 = words[i * W], w1 = (W == 2) ? words[i * W + 1] : 0;
-            if (ext_bwd(slot_ext(w0)) == EXT_F || !is_splitter(key_hash32(slot_key(w0, w1, p)), p)) continue;
+            if (ext_bwd(slot_ext(w0)) == EXT_F || !is_splitter(slot_key(w0, w1, p), p)) continue;
             const uint32_t pos = atomicAdd(&lcount, 1u);
             if (pos < SPLIT_LCAP) {
                 lbuf[pos * W] = w0;

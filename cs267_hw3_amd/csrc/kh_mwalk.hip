@@ -114,8 +114,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             } else {
                 put(st, 1, buf, steps, nrec, nwords, rec, origin, idx);
                 k = key_next(k, st, p);
-                const uint64_t hk = key_hash32(k);
-                if (mw.split_bits && (hk & ((1ull << mw.split_bits) - 1)) == 0) {
+                if (split_test(k, (int)mw.split_bits)) {
                     // the next k-mer heads a segment of its own: report it as this segment's link
                     rec[2 * nrec] = rec_tag(origin, true, 1, idx);
                     rec[2 * nrec + 1] = k.hi;
