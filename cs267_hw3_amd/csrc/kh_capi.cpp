@@ -873,8 +873,12 @@ int kh_assemble_dev(kh_table* t) {
                 succ_side = true;
             }
             KH_HIP(kh::launch_rec_succ(kp, view(t), t->headrec.as<uint64_t>(), wb.hcap, rs, blocks));
-            if (succ_side) KH_HIP(hipEventRecord(t->ev_conv, t->side));
         }
+        // the splitter table reads only the splitter list: behind the resolve, beside the walk
+        // (walk bracket C3 1.35 -> 1.33, C2 0.61 -> 0.59, C5 3.46 -> 3.43 ms;
+        // profiles/r05/ab/ab_seg_table_beside_walk.txt)
+        if (kp.split_bits) KH_HIP(kh::launch_seg_table(kp, wb, sb, succ_side ? t->side : t->stream));
+        if (succ_side) KH_HIP(hipEventRecord(t->ev_conv, t->side));
         // three walker blocks per CU for 16-B slots at load <= 0.6, else two (kh_kernels.hip)
         // (round 5, after the single place() site: 4 / 5 blocks per CU C3 walk 1.40 / 1.43 ms vs 1.16)
         KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, (kp.W == 2 && t->load <= 0.6) ? -3 : -2, t->stream));

@@ -1112,20 +1112,23 @@ __global__ __launch_bounds__(BLOCK) void k_stab_build(KParams p, WalkBuffers wb,
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, const uint64_t* stab, const uint32_t* id,
-                                                    uint64_t cap2_max, unsigned long long* stats) {
+// The successor of every segment a walker ended before a splitter (SEG_AT_SPLIT + its key), from
+// the splitter table, all segments in parallel. Resolving lazily inside k_seg_chain instead (one
+// lookup per hop on the contig's serial path) measured C3 -0.03 ms but C2 (~80 segments per
+// contig) 0.60 -> 1.00 ms walk bracket (profiles/r05/ab/ab_seg_lazy_link.txt).
+__global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
-    const uint64_t cap2 = stab_cap(wb, cap2_max);
+    const uint64_t cap2 = stab_cap(wb, sb.cap2);
     for (uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; g < nseg; g += (uint64_t)gridDim.x * BLOCK) {
         if (wb.seg_next[g] != SEG_AT_SPLIT) continue;
         const Key k{wb.seg_key[2 * g], wb.seg_key[2 * g + 1]};
         uint64_t s = mulhi64(fmix64(key_hash(k)), cap2);
         uint32_t nx = SEG_NONE;
         for (uint64_t pr = 0; pr < cap2; ++pr) {
-            const uint64_t lo = stab[2 * s];
+            const uint64_t lo = sb.stab[2 * s];
             if (lo == EMPTY) break;
-            if (lo == k.lo && stab[2 * s + 1] == k.hi) {
-                nx = (uint32_t)(wb.n_starts + id[s]);
+            if (lo == k.lo && sb.stab[2 * s + 1] == k.hi) {
+                nx = (uint32_t)(wb.n_starts + sb.stab_id[s]);
                 break;
             }
             s = (s + 1 == cap2) ? 0 : s + 1;
@@ -1264,8 +1267,9 @@ hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64
     return hipGetLastError();
 }
 
-hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
-                           unsigned long long* stats, hipStream_t s) {
+// The splitter table (key -> segment id) and the segment owners' reset: they read only the walked
+// splitter list, so they run before or beside the walk (on the resolve's side stream).
+hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb, hipStream_t s) {
     const uint64_t nseg = wb.n_starts + wb.n_splits;
     if (nseg == 0) return hipSuccess;
     k_stab_init<<<(unsigned)hmin((sb.cap2 + BLOCK - 1) / BLOCK, 2048), BLOCK, 0, s>>>(wb, sb.stab, sb.cap2);
@@ -1274,17 +1278,25 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
     if (wb.n_splits)
         k_stab_build<<<(unsigned)hmin((wb.n_splits + BLOCK - 1) / BLOCK, 4096), BLOCK, 0, s>>>(
             p, wb, sb.stab, sb.stab_id, sb.cap2);
-    k_seg_link<<<(unsigned)hmin((nseg + BLOCK - 1) / BLOCK, 8192), BLOCK, 0, s>>>(wb, sb.stab, sb.stab_id, sb.cap2,
-                                                                                   stats);
-    if (wb.n_starts) {
-        const unsigned gs = (unsigned)hmin((nseg + BLOCK - 1) / BLOCK, 8192);
-        const unsigned gc = (unsigned)hmin((wb.n_starts + BLOCK - 1) / BLOCK, 8192);
-        if ((e = hipMemsetAsync(sb.long_flag, 0, 4, s)) != hipSuccess) return e;
-        k_seg_chain<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
-        k_seg_jump<<<gs, BLOCK, 0, s>>>(wb, sb);
-        k_seg_chain_jump<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
-        k_seg_fill<<<gs, BLOCK, 0, s>>>(wb, sb, stats);
-    }
+    return hipGetLastError();
+}
+
+// After the walk (and launch_seg_table): links, chains, offsets.
+hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
+                           unsigned long long* stats, hipStream_t s) {
+    (void)p;
+    const uint64_t nseg = wb.n_starts + wb.n_splits;
+    if (nseg == 0) return hipSuccess;
+    hipError_t e;
+    const unsigned gs = (unsigned)hmin((nseg + BLOCK - 1) / BLOCK, 8192);
+    k_seg_link<<<gs, BLOCK, 0, s>>>(wb, sb, stats);
+    if (wb.n_starts == 0) return hipGetLastError();
+    const unsigned gc = (unsigned)hmin((wb.n_starts + BLOCK - 1) / BLOCK, 8192);
+    if ((e = hipMemsetAsync(sb.long_flag, 0, 4, s)) != hipSuccess) return e;
+    k_seg_chain<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
+    k_seg_jump<<<gs, BLOCK, 0, s>>>(wb, sb);
+    k_seg_chain_jump<<<gc, BLOCK, 0, s>>>(wb, sb, stats);
+    k_seg_fill<<<gs, BLOCK, 0, s>>>(wb, sb, stats);
     return hipGetLastError();
 }
 

@@ -126,6 +126,7 @@ struct SegBuffers {
 // splits with (hash & (2^bits - 1)) == 0 -> out (count to *count)
 hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64_t n, int bits, uint64_t* off,
                                 uint64_t* scratch, uint64_t* out, unsigned long long* count, hipStream_t s);
+hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb, hipStream_t s);
 hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
                            unsigned long long* stats, hipStream_t s);
 // phases: MAT_SCAN = offsets + ctr[CT_OUT_BYTES]; MAT_WRITE = the text (out must hold the
