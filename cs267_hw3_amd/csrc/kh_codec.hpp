@@ -243,15 +243,30 @@ KH_HD uint32_t key_hash32(Key k) {
 }
 
 // ---- minimizer ---------------------------------------------------------------------------------
-// Window j (0 = the last M bases, K-M = the first M) = bits [2j, 2j + 2M) of V. Its order key is
-// (w[23:0] * C + w) mod 2^32 (one v_mad_u32_u24 with w itself as the addend: the top 8 bits of
-// w enter the top of the key; an addend of w >> 8 cost a shift per window, ~36 VALU per scan in
-// the convert pass and in every walk hop), top 26 bits; the minimizer is the
-// window of smallest order, ties to the smallest j (j*). Packed result: order26 << 6 | j*. The
-// region and the owner rank hash the minimizer window's *content* (2M bits), never its order
-// (26 bits: distinct windows share values).
-static constexpr uint32_t MINI_C = 0x9E3779u;
-KH_HD uint32_t win_order(uint32_t w) { return ((w & 0xFFFFFFu) * MINI_C + w) >> 6; }
+// Window j (0 = the last M bases, K-M = the first M) = bits [2j, 2j + 2M) of V. Its order is
+// (w[23:0] * C) mod 2^26 for an odd 18-bit C (a bijection of the window's low 12 bases), and the
+// scan's key is w[23:0] * (C << 6) + j: one v_mad_u32_u24 with j as an inline addend per window,
+// the order in the top 26 bits and j* in the low 6 (round 4's key, (w[23:0] * C' + w) >> 6 << 6 | j,
+// took one v_and_or more per window: 36 VALU per scan, in the records pass and in every walk hop).
+// The minimizer is the window of smallest order, ties to the smallest j (j*). Packed result:
+// order26 << 6 | j*. The region and the owner rank hash the minimizer window's *content* (2M bits),
+// never its order (distinct windows share an order when their low 12 bases agree).
+static constexpr uint32_t MINI_C6 = 0x278DDu << 6;  // < 2^24: the u24 multiplier operand
+KH_HD uint32_t win_order(uint32_t w) { return ((w & 0xFFFFFFu) * MINI_C6) >> 6; }
+KH_HD uint32_t win_key(uint32_t w, uint32_t j) { return (w & 0xFFFFFFu) * MINI_C6 + j; }
+#if defined(__HIP_DEVICE_COMPILE__)
+// c = MINI_C6 passed through an empty asm: with the constant visible the compiler proves the
+// product's low 6 bits zero, turns "+ j" into an or and no longer folds the pair into one
+// v_mad_u32_u24 (it emitted v_mul_u32_u24 + v_or_b32 per window)
+__device__ __forceinline__ uint32_t mini_c6() {
+    uint32_t c = MINI_C6;
+    asm volatile("" : "+s"(c));
+    return c;
+}
+__device__ __forceinline__ uint32_t win_key_d(uint32_t w, uint32_t c, uint32_t j) {
+    return (uint32_t)__umul24(w, c) + j;
+}
+#endif
 
 KH_HD uint32_t win_bits(Key k, int j, const KParams& p) {
     const int b = 2 * j;  // V = hi * 2^62 + lo
@@ -267,12 +282,13 @@ __device__ __forceinline__ uint32_t mini_scan_t(Key k) {
     const uint32_t v[5] = {(uint32_t)k.lo, (uint32_t)(k.lo >> 32) | (uint32_t)(k.hi << 30), (uint32_t)(k.hi >> 2),
                            (uint32_t)(k.hi >> 34), 0u};
     constexpr uint32_t mmask = (uint32_t)((1ull << (2 * M)) - 1);
+    const uint32_t c6 = mini_c6();
     uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
     for (int j = 0; j <= K - M; ++j) {
         const int b = 2 * j;
         const uint32_t w = (b & 31) ? __builtin_amdgcn_alignbit(v[(b >> 5) + 1], v[b >> 5], b & 31) : v[b >> 5];
-        const uint32_t o = (win_order(w & mmask) << 6) | (uint32_t)j;
+        const uint32_t o = win_key_d(w & mmask, c6, (uint32_t)j);
         best = o < best ? o : best;
     }
     return best;
@@ -287,13 +303,14 @@ KH_HD uint32_t mini_scan(Key k, const KParams& p) {
                            (uint32_t)(k.hi >> 34), 0u};
     const uint32_t mmask = (uint32_t)((1ull << (2 * p.M)) - 1);
     const int last = p.K - p.M;
+    const uint32_t c6 = mini_c6();
     uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
     for (int j = 0; j <= KMAX - 1; ++j) {
         if (j <= last) {
             const int b = 2 * j;
             const uint32_t w = (b & 31) ? __builtin_amdgcn_alignbit(v[(b >> 5) + 1], v[b >> 5], b & 31) : v[b >> 5];
-            const uint32_t o = (win_order(w & mmask) << 6) | (uint32_t)j;
+            const uint32_t o = win_key_d(w & mmask, c6, (uint32_t)j);
             best = o < best ? o : best;
         }
     }
@@ -301,7 +318,7 @@ KH_HD uint32_t mini_scan(Key k, const KParams& p) {
 #else
     uint32_t best = 0xFFFFFFFFu;
     for (int j = 0; j <= p.K - p.M; ++j) {
-        const uint32_t o = (win_order(win_bits(k, j, p)) << 6) | (uint32_t)j;
+        const uint32_t o = win_key(win_bits(k, j, p), (uint32_t)j);
         best = o < best ? o : best;
     }
     return best;
