@@ -1123,11 +1123,17 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
 #ifndef KH_SORT_SPLIT
 #define KH_SORT_SPLIT 1
 #endif
+#ifndef KH_EARLY_RESERVE
+#define KH_EARLY_RESERVE 1
+#endif
 // Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
 // with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
 // out[window(bin) + reserved + rank] (positions past cap -> overflow list).
 // WRANK: ranks by wave_rank_all (few bins: the route's owners) instead of one LDS atomic per item
-template <int W, int TB, int NB, int TILE, bool WRANK = false, class CtrF, class WinF, class NextF>
+// LATE: g is published after next() issues the next tile's loads; only where those loads are
+// unconditional (the waitcnt for g then leaves them in flight: vmcnt(N)); behind conditional loads
+// the compiler waits for vmcnt(0), i.e. for the prefetch itself, so g is published before next().
+template <int W, int TB, int NB, int TILE, bool WRANK = false, bool LATE = true, class CtrF, class WinF, class NextF>
 __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, const uint32_t* bin, uint64_t* items,
                                                    uint16_t* sbin, uint32_t* hist, uint32_t* start, uint32_t* gpos,
                                                    uint32_t* wsum, CtrF counter, WinF window, uint32_t cap,
@@ -1149,13 +1155,20 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
     }
     lds_barrier();
     const uint32_t hv = threadIdx.x < NB ? hist[threadIdx.x] : 0u;
+    // the bin's window reservation goes out first: its round trip (~1-2 us) overlaps the scan, the
+    // LDS scatter and the next tile's load issue; g is published for the write-out just before its
+    // barrier (lds_barrier waits for LDS only, so the atomic stays in flight across the others)
+    uint32_t g = 0;
+    if (KH_EARLY_RESERVE && threadIdx.x < NB && hv) g = atomicAdd(counter(threadIdx.x), hv);
     uint32_t total;
     const uint32_t st = block_scan_u32<TB>(hv, total, wsum);
     if (threadIdx.x < NB) {
         start[threadIdx.x] = st;
-        const uint32_t g = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
-        gpos[threadIdx.x] = g;
-        if (hv && g + hv > cap) spill = 1;
+        if (!KH_EARLY_RESERVE) {
+            g = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
+            gpos[threadIdx.x] = g;
+            if (hv && g + hv > cap) spill = 1;
+        }
     }
     lds_barrier();
 #pragma unroll
@@ -1168,8 +1181,16 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
             sbin[pos] = (uint16_t)bin[j];
         }
     }
+    if (KH_EARLY_RESERVE && !LATE && threadIdx.x < NB) {
+        gpos[threadIdx.x] = g;
+        if (hv && g + hv > cap) spill = 1;
+    }
     __builtin_amdgcn_sched_barrier(0);
     next();  // the next tile's loads are in flight while this one is written
+    if (KH_EARLY_RESERVE && LATE && threadIdx.x < NB) {
+        gpos[threadIdx.x] = g;
+        if (hv && g + hv > cap) spill = 1;
+    }
     lds_barrier();
 #pragma unroll 4
     for (uint32_t x = threadIdx.x; x < total; x += TB) {
@@ -1451,7 +1472,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
             load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase);
             lds_barrier();  // every lane has read rg before the next tile's counts
         } else {
-            sort_reserve_write<W, TB, NB, TILE>(
+            sort_reserve_write<W, TB, NB, TILE, false, false>(
                 a, b, bin, items, sbin, hist, start, gpos, wsum, [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
                 [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
                 [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
