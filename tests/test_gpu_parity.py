@@ -193,6 +193,24 @@ def test_bad_extension_is_reported():
     assert e.value.code == _lib.KH_ERR_BAD_BASE
 
 
+@pytest.mark.parametrize("bad", [b"N", b"a", b"\x00", b"\x87", b"\xc1"])
+def test_bad_extension_is_reported_partitioned(bad):
+    """The records pass (batches >= 2^20 records) decodes both extension bytes with a byte table
+    (ext_codes2): a byte outside {A,C,G,T,F} is EXT_BAD as in base_code, including bytes whose low 3
+    bits index a valid character (0x87 -> 'G''s slot, 0xC1 -> 'A''s)."""
+    k = 51
+    g = kh.SyntheticKmers(k, 1_200_000, 8, 200, 10, seed=77)
+    recs = g.records().copy()
+    P = (k + 3) // 4
+    interior = np.where((recs[:, P] != ord("F")) & (recs[:, P + 1] != ord("F")))[0][1000]
+    recs[interior, P + 1] = bad[0]
+    with pytest.raises(kh.KmerHashError) as e:
+        with kh.KmerHashTable(k, len(recs), device=0) as t:
+            t.insert_all(recs)
+            t.assemble()
+    assert e.value.code == _lib.KH_ERR_BAD_BASE
+
+
 @pytest.mark.parametrize("k,n,lmin,lmax,single,seed", [
     (19, 1_000_000, 200, 1374, 0, 19),        # C2-like length mix, reduced n
     (51, 1_000_000, 8, 200, 10, 51),          # C3-like length mix, reduced n
