@@ -256,6 +256,9 @@ __device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, in
 // reads and atomicOr of the build touch one word of a slot, and with 16-B interleaving those
 // words sit only in every other bank pair (a 32-lane group of ds_read_b64 spread over 16 bank pairs
 // instead of 32). KH_LDS_SPLIT=0 compiles the interleaved layout (A/B).
+#ifndef KH_REC_UNCOND
+#define KH_REC_UNCOND 1
+#endif
 #ifndef KH_LDS_SPLIT
 #define KH_LDS_SPLIT 1
 #endif
@@ -1393,11 +1396,26 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nbytes = n * (uint64_t)R;
     uint64_t a[IPT], b[IPT];  // raw 16-B blocks until parsed, then the words
+    // ROUTE (and KH_REC_UNCOND=0): loads only where a block is needed. Otherwise every lane loads
+    // (its address clamped into the records): blocks 62 and 63 and those of a wave past the batch
+    // are never read (a record's two blocks are <= 61; past the batch no record is valid), and
+    // unconditional loads let the compiler count them, so the sort's reservation wait leaves the
+    // next tile's loads in flight (vmcnt(N) instead of vmcnt(0))
+    constexpr bool UNCOND = KH_REC_UNCOND && !ROUTE;
+    // the block holding the last record byte: the conditional path loads it whole as well (the
+    // records buffer is read 16 B at a time up to that block's end)
+    const uint64_t glast = nbytes ? (nbytes - 1) & ~15ull : 0;
     auto load = [&](uint64_t base, uint64_t end) {
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             const uint64_t r0 = base + (uint64_t)j * TB + (threadIdx.x & ~63u);  // the wave's first record
             const uint64_t g = ((r0 * R) & ~15ull) + 16ull * lane;
+            if (UNCOND) {
+                const ulonglong2 v = ld_stream16(recs + (g < glast ? g : glast));
+                a[j] = v.x;
+                b[j] = v.y;
+                continue;
+            }
             a[j] = b[j] = 0;
             if (r0 < end && lane < 62 && g < nbytes) {
                 const ulonglong2 v = ld_stream16(recs + g);
@@ -1488,7 +1506,7 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
             load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase);
             lds_barrier();  // every lane has read rg before the next tile's counts
         } else {
-            sort_reserve_write<W, TB, NB, TILE, false, false>(
+            sort_reserve_write<W, TB, NB, TILE, false, UNCOND>(
                 a, b, bin, items, sbin, hist, start, gpos, wsum, [&](uint32_t q) { return &wcnt[q * S1 + sub]; },
                 [&](uint32_t q) { return (uint64_t)(q * S1 + sub) * CAP1; }, CAP1, buf1, ovf, ovf_cap, ctr, stats,
                 [&]() { load(nbase, nt < ntiles ? min(nbase + TILE, n) : nbase); });
