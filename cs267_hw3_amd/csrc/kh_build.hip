@@ -35,10 +35,8 @@
 namespace kh {
 
 static constexpr int PB = 256;                    // threads per block of the small kernels
-#ifndef KH_B1
-#define KH_B1 9
-#endif
-static constexpr int B1 = KH_B1, B2 = REGION_BITS_MAX - KH_B1;  // radix bits per pass (pass 2: p.rbits - B1)
+// radix bits per pass (pass 2: p.rbits - B1); 8 pass-1 bits measured the same (round 4)
+static constexpr int B1 = 9, B2 = REGION_BITS_MAX - B1;
 static constexpr int NB1 = 1 << B1, NB2 = 1 << B2;
 static constexpr int NBX = NB1 > NB2 ? NB1 : NB2;  // bins of the larger pass (LDS layout)
 static constexpr uint32_t NREG_MAX = 1u << (B1 + B2);
@@ -255,40 +253,23 @@ __device__ __forceinline__ void parse_record_regs_t(uint64_t x0, uint64_t x1, in
 // at w[sm + i], sm = the block's slice capacity) rather than 16-B pairs: the random 8-B CAS, probe
 // reads and atomicOr of the build touch one word of a slot, and with 16-B interleaving those
 // words sit only in every other bank pair (a 32-lane group of ds_read_b64 spread over 16 bank pairs
-// instead of 32). KH_LDS_SPLIT=0 compiles the interleaved layout (A/B).
-#ifndef KH_REC_UNCOND
-#define KH_REC_UNCOND 1
-#endif
-#ifndef KH_LDS_SPLIT
-#define KH_LDS_SPLIT 1
-#endif
+// instead of 32; the interleaved layout measured 3.64 -> 3.75 ms at C3, round 4).
 template <int W>
 struct Slice {
     unsigned long long* w;
     uint32_t sm;
-    static constexpr bool SPLIT = W == 2 && KH_LDS_SPLIT;
-    __device__ __forceinline__ unsigned long long* p0(uint32_t i) const { return w + (SPLIT ? i : W * i); }
-    __device__ __forceinline__ unsigned long long* p1(uint32_t i) const { return w + (SPLIT ? sm + i : W * i + 1); }
+    static constexpr bool SPLIT = W == 2;
+    __device__ __forceinline__ unsigned long long* p0(uint32_t i) const { return w + i; }
+    __device__ __forceinline__ unsigned long long* p1(uint32_t i) const { return w + (sm + i); }  // W == 2 only
     __device__ __forceinline__ uint64_t w0(uint32_t i) const { return *p0(i); }
     __device__ __forceinline__ uint64_t w1(uint32_t i) const { return W == 2 ? *p1(i) : 0ull; }
-    // both words (one 16-B LDS read when interleaved)
     __device__ __forceinline__ void get(uint32_t i, uint64_t& a, uint64_t& b) const {
-        if (W == 2 && !SPLIT) {
-            const ulonglong2 v = reinterpret_cast<const ulonglong2*>(w)[i];
-            a = v.x;
-            b = v.y;
-        } else {
-            a = *p0(i);
-            b = W == 2 ? *p1(i) : 0ull;
-        }
+        a = *p0(i);
+        b = W == 2 ? *p1(i) : 0ull;
     }
     __device__ __forceinline__ void put(uint32_t i, uint64_t a, uint64_t b) const {
-        if (W == 2 && !SPLIT) {
-            reinterpret_cast<ulonglong2*>(w)[i] = make_ulonglong2(a, b);
-        } else {
-            *p0(i) = a;
-            if (W == 2) *p1(i) = b;
-        }
+        *p0(i) = a;
+        if (W == 2) *p1(i) = b;
     }
 };
 
@@ -337,15 +318,6 @@ __device__ __forceinline__ int lds_insert(const KParams& p, const Slice<W>& lt, 
 // test), so a probe run of d slots costs ~d/4 steps. The build's phases run the lanes' keys in
 // lockstep, so a wave waits for its longest run: this shortens exactly that tail. Slots are
 // taken in the same order (first EMPTY at or after home) as lds_insert.
-#ifndef KH_LDS_BLOCK
-#define KH_LDS_BLOCK 1
-#endif
-#ifndef KH_FUSE_INIT
-#define KH_FUSE_INIT 1
-#endif
-#ifndef KH_HEAD_REG
-#define KH_HEAD_REG 1
-#endif
 template <int W>
 __device__ __forceinline__ int lds_insert_blk(const KParams& p, const Slice<W>& lt, uint32_t S, uint32_t loc,
                                               uint64_t w0, uint64_t w1, unsigned long long* stats) {
@@ -442,19 +414,13 @@ __device__ __forceinline__ void clean_out(uint64_t& w0, uint64_t& w1, const KPar
 // Block-step search of a slice for key (want0, lo) from slot t: BLK slots per step (word 0 of each,
 // 16-B LDS reads with the split layout), the first slot at or after t that is EMPTY (absent) or
 // holds the key's high word (then word 1 decides).
-#ifndef KH_LINK_BLK
-#define KH_LINK_BLK 2
-#endif
-#ifndef KH_LINK_B128
-#define KH_LINK_B128 1
-#endif
 template <int W, int BLK>
 __device__ __forceinline__ uint32_t link_probe(const KParams& p, const Slice<W>& lt, uint32_t S, uint32_t t,
                                                uint64_t want0, uint64_t lo) {
     while (t < S) {
         const uint32_t base = t & ~(uint32_t)(BLK - 1);
         uint64_t v[BLK];
-        if constexpr (KH_LINK_B128 && Slice<W>::SPLIT && BLK % 2 == 0) {
+        if constexpr (Slice<W>::SPLIT && BLK % 2 == 0) {
 #pragma unroll
             for (int q = 0; q < BLK; q += 2) {
                 const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(lt.p0(base + q));
@@ -512,17 +478,13 @@ __device__ __forceinline__ uint32_t chain_link(const KParams& p, const Slice<W>&
     const uint64_t home = MTOP ? home_in(lo, lo + S, hy) : home_of(place_w(mw, y, p, (int)j + 1), cap, p);
     if (home < lo || home >= lo + S) return NO_SUCC;
     const uint64_t want0 = W == 1 ? y.lo : y.hi;
-#ifndef KH_LINK_MODE
-#define KH_LINK_MODE 1
-#endif
-    // block steps (see lds_insert_blk): ~d/4 steps for a run of d slots (KH_LINK_MODE: 0 slot
-    // steps, 1 block steps, 2 block steps in dense slices)
-    if (KH_LDS_BLOCK && MTOP && (KH_LINK_MODE == 1 || (KH_LINK_MODE == 2 && dense))) {
+    // block steps (see lds_insert_blk): ~d/4 steps for a run of d slots
+    if (MTOP) {
         // sparse slices (load 0.5: y sits at or right after its home): 2-slot steps, one 16-B
         // LDS read each (C3 build 2.89 -> 2.76 ms, LDS bank conflicts 0.47 -> 0.41 of LDS cycles);
         // dense slices (> 2/3 full, longer runs): 4-slot steps (load 0.85: 4.96 vs 5.11 ms)
         return dense ? link_probe<W, 4>(p, lt, S, (uint32_t)(home - lo), want0, y.lo)
-                     : link_probe<W, KH_LINK_BLK>(p, lt, S, (uint32_t)(home - lo), want0, y.lo);
+                     : link_probe<W, 2>(p, lt, S, (uint32_t)(home - lo), want0, y.lo);
     }
     for (uint32_t t = (uint32_t)(home - lo); t < S; ++t) {
         uint64_t v0, v1;
@@ -796,7 +758,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
     uint32_t m_cur = fill(r);
     load(r, m_cur, a, b);
     const uint32_t NR = nreg(p);
-    if (SORT && KH_FUSE_INIT)  // the whole LDS slice reset once (see the sorted insert below)
+    if (SORT)  // the whole LDS slice reset once (see the sorted insert below)
         for (uint32_t i = threadIdx.x; i < smax; i += BUILD_THREADS) {
             *lt.p0(i) = EMPTY;
             *lt.p1(i) = 0ull;
@@ -807,23 +769,18 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
         const uint32_t m_next = fill(r + gridDim.x);  // in flight during this region
         // block-step probing (lds_insert_blk) where the slice fills above ~2/3 (balanced tables at
         // load 0.85: build 21.3 -> 13.0 ms); slot steps below (C3 at 0.5: 3.71 vs 3.90 ms)
-        const bool dense = KH_LDS_BLOCK && 3u * m_cur > 2u * S;
+        const bool dense = 3u * m_cur > 2u * S;
         if (threadIdx.x == 0) hcnt = 0;
         int pos[IPT];  // LDS slot of each word inserted here (chains walk from these)
         if constexpr (SORT) {
             static_assert(FRESH && Slice<W>::SPLIT, "the sorted slice needs a fresh table and the split layout");
-            // sorted slice (FRESH only): word 0 EMPTY, the word-1 array holds the home counts. With
-            // KH_FUSE_INIT every slot of the LDS slice is already reset (word 0 EMPTY, word 1 zero:
-            // zero home counts): before the first region, then by each write-out for the slots it
-            // reads; slots past a region's S are never written. The write-out then needs no
-            // barrier of its own: this one orders it before the next region's count atomics.
+            // sorted slice (FRESH only): word 0 EMPTY, the word-1 array holds the home counts.
+            // Every slot of the LDS slice is already reset (word 0 EMPTY, word 1 zero: zero home
+            // counts): before the first region, then by each write-out for the slots it reads;
+            // slots past a region's S are never written. The write-out then needs no barrier of
+            // its own: this one orders it before the next region's count atomics (a separate
+            // reset pass per region measured 2.91-2.92 vs 2.90 ms, round 4).
             uint32_t* hist = reinterpret_cast<uint32_t*>(lt.p1(0));
-            if (!KH_FUSE_INIT) {
-                for (uint32_t i = threadIdx.x; i < S; i += BUILD_THREADS) {
-                    *lt.p0(i) = EMPTY;
-                    hist[i] = 0;
-                }
-            }
             lds_barrier();
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {  // home | rank among the keys of that home << 16
@@ -929,7 +886,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 if (pos[j] >= 0) {
                     const uint32_t nx = chain_link<W, true>(p, lt, S, lo, cap, a[j], b[j], dense);
                     put_link<W>(lt, (uint32_t)pos[j], nx, p);
-                    if (KH_HEAD_REG && nx != NO_SUCC) pos[j] |= HAS_SUCC;
+                    if (nx != NO_SUCC) pos[j] |= HAS_SUCC;
                 }
             load(r + gridDim.x, m_next, a, b);
             lds_barrier();
@@ -937,9 +894,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
             for (int j = 0; j < IPT; ++j) {
                 if (pos[j] < 0) continue;
                 const uint32_t sl = (uint32_t)pos[j] & 0xFFFFu;
-                if (KH_HEAD_REG ? (!(pos[j] & HAS_SUCC) || (*pred_word<W>(lt, sl) & PRED))
-                                : !is_head<W>(lt, sl, p))
-                    continue;
+                if (!(pos[j] & HAS_SUCC) || (*pred_word<W>(lt, sl) & PRED)) continue;
                 const uint32_t id = atomicAdd(&hcnt, 1u);
                 if (id < hcap)
                     hlist[id] = (uint16_t)sl;
@@ -971,7 +926,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 }
                 if (hcap && x != EMPTY) clean_out<W>(x, y, p);
                 if (hcap && x2 != EMPTY) clean_out<W>(x2, y2, p);
-                if (SORT && KH_FUSE_INIT) {  // this thread's slots, read above: reset for the next region
+                if (SORT) {  // this thread's slots, read above: reset for the next region
                     *lt.p0(i) = EMPTY;
                     *lt.p1(i) = 0ull;
                     if (two) {
@@ -989,7 +944,7 @@ __global__ __launch_bounds__(BUILD_THREADS) __attribute__((amdgpu_waves_per_eu(6
                 slots[lo + i] = v;
             }
         }
-        if (!(SORT && KH_FUSE_INIT)) lds_barrier();  // fused: the next region's first barrier orders it
+        if (!SORT) lds_barrier();  // fused: the next region's first barrier orders it
         m_cur = m_next;
     }
 }
@@ -1139,12 +1094,6 @@ __device__ __forceinline__ void load_words_win_tb(const uint64_t* __restrict__ b
     }
 }
 
-#ifndef KH_SORT_SPLIT
-#define KH_SORT_SPLIT 1
-#endif
-#ifndef KH_EARLY_RESERVE
-#define KH_EARLY_RESERVE 1
-#endif
 // Counting-sort one tile (items in registers) by bin in LDS, reserve each bin's run in its window
 // with one atomicAdd (counter(bin)), prefetch the next tile (next()), write the runs to
 // out[window(bin) + reserved + rank] (positions past cap -> overflow list).
@@ -1178,35 +1127,29 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
     // LDS scatter and the next tile's load issue; g is published for the write-out just before its
     // barrier (lds_barrier waits for LDS only, so the atomic stays in flight across the others)
     uint32_t g = 0;
-    if (KH_EARLY_RESERVE && threadIdx.x < NB && hv) g = atomicAdd(counter(threadIdx.x), hv);
+    if (threadIdx.x < NB && hv) g = atomicAdd(counter(threadIdx.x), hv);
     uint32_t total;
     const uint32_t st = block_scan_u32<TB>(hv, total, wsum);
-    if (threadIdx.x < NB) {
-        start[threadIdx.x] = st;
-        if (!KH_EARLY_RESERVE) {
-            g = hv ? atomicAdd(counter(threadIdx.x), hv) : 0u;
-            gpos[threadIdx.x] = g;
-            if (hv && g + hv > cap) spill = 1;
-        }
-    }
+    if (threadIdx.x < NB) start[threadIdx.x] = st;
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
         if (a[j] != EMPTY) {
             const uint32_t pos = start[bin[j]] + rank[j];
-            // words 0 and 1 in two arrays (KH_SORT_SPLIT): random 8-B stores over every bank pair
-            items[KH_SORT_SPLIT ? pos : W * pos] = a[j];
-            if (W == 2) items[KH_SORT_SPLIT ? TILE + pos : 2 * pos + 1] = b[j];
+            // words 0 and 1 in two arrays: random 8-B stores over every bank pair (interleaved
+            // 16-B items measured the same, round 4)
+            items[pos] = a[j];
+            if (W == 2) items[TILE + pos] = b[j];
             sbin[pos] = (uint16_t)bin[j];
         }
     }
-    if (KH_EARLY_RESERVE && !LATE && threadIdx.x < NB) {
+    if (!LATE && threadIdx.x < NB) {
         gpos[threadIdx.x] = g;
         if (hv && g + hv > cap) spill = 1;
     }
     __builtin_amdgcn_sched_barrier(0);
     next();  // the next tile's loads are in flight while this one is written
-    if (KH_EARLY_RESERVE && LATE && threadIdx.x < NB) {
+    if (LATE && threadIdx.x < NB) {
         gpos[threadIdx.x] = g;
         if (hv && g + hv > cap) spill = 1;
     }
@@ -1216,8 +1159,7 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
         const uint32_t q = sbin[x];
         const uint32_t w = gpos[q] + (x - start[q]);
         if (w < cap) {
-            const uint64_t v0 = items[KH_SORT_SPLIT ? x : W * x],
-                           v1 = (W == 2) ? items[KH_SORT_SPLIT ? TILE + x : 2 * x + 1] : 0;
+            const uint64_t v0 = items[x], v1 = (W == 2) ? items[TILE + x] : 0;
             const uint64_t g = window(q) + w;
             if (W == 2) {
                 *reinterpret_cast<ulonglong2*>(out + g * 2) = make_ulonglong2(v0, v1);
@@ -1250,8 +1192,8 @@ __device__ __forceinline__ void sort_reserve_write(uint64_t* a, uint64_t* b, con
             if (rr >= keepv[q]) {
                 const uint64_t d = sbase + hist[q] + (rr - keepv[q]);
                 if (d < ovf_cap) {
-                    ovf[d * W] = items[KH_SORT_SPLIT ? x : W * x];
-                    if (W == 2) ovf[d * W + 1] = items[KH_SORT_SPLIT ? TILE + x : 2 * x + 1];
+                    ovf[d * W] = items[x];
+                    if (W == 2) ovf[d * W + 1] = items[TILE + x];
                 } else {
                     atomicAdd(&stats[ST_FULL], 1ull);
                 }
@@ -1340,7 +1282,7 @@ __global__ __launch_bounds__(TB) void k_win1(KParams p_in, const uint64_t* __res
     }
 }
 
-// pass 1 on records (KH_P1=recwin, k with a compile-time packed size PK): the windowed pass 1
+// pass 1 on records (k with a compile-time packed size PK): the windowed pass 1
 // reading the reference records itself — one unaligned 16-B load per record (a record is PK + 2
 // <= 16 bytes), parsed in registers after the tile's loads land, with the start / splitter bits
 // of the record pass — instead of a record -> word copy and a second pass over the copy.
@@ -1396,12 +1338,12 @@ __global__ __launch_bounds__(TB) void k_win1_rec(KParams p_in, const uint8_t* __
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nbytes = n * (uint64_t)R;
     uint64_t a[IPT], b[IPT];  // raw 16-B blocks until parsed, then the words
-    // ROUTE (and KH_REC_UNCOND=0): loads only where a block is needed. Otherwise every lane loads
+    // ROUTE: loads only where a block is needed. Otherwise every lane loads
     // (its address clamped into the records): blocks 62 and 63 and those of a wave past the batch
     // are never read (a record's two blocks are <= 61; past the batch no record is valid), and
     // unconditional loads let the compiler count them, so the sort's reservation wait leaves the
     // next tile's loads in flight (vmcnt(N) instead of vmcnt(0))
-    constexpr bool UNCOND = KH_REC_UNCOND && !ROUTE;
+    constexpr bool UNCOND = !ROUTE;
     // the block holding the last record byte: the conditional path loads it whole as well (the
     // records buffer is read 16 B at a time up to that block's end)
     const uint64_t glast = nbytes ? (nbytes - 1) & ~15ull : 0;

@@ -9,6 +9,7 @@ import pytest
 import cs267_hw3_amd as kh
 from cs267_hw3_amd import _lib
 import oracle_bind as ob
+from cases import merging_walks_text
 
 pytestmark = pytest.mark.gpu
 
@@ -102,27 +103,8 @@ def test_explicit_start_list():
 
 
 def merging_walks(k, L, seed, every=1):
-    """Malformed input whose start walks overlap: one chain C_0..C_{L-1} plus, at every `every`-th
-    position j, three extra start k-mers x + C_{j-1}[1:] (bwd 'F') whose next_kmer is C_j. Every
-    start walks the shared tail again (kmer_hash.cpp:41-53 does not care), so the text is ~3L^2/2
-    bases, far past the table-start bound n + (K+1)·starts that kh_assemble_dev sizes first."""
-    rng = np.random.default_rng(seed)
-    B = "ACGT"
-    seq = "".join(B[x] for x in rng.integers(0, 4, L + k - 1))
-    lines = []
-    for i in range(L):
-        lines.append((seq[i:i + k], "F" if i == 0 else seq[i - 1], "F" if i == L - 1 else seq[i + k]))
-    seen = {x[0] for x in lines}
-    for j in range(1, L, every):
-        for x in B:
-            z = x + seq[j:j + k - 1]
-            if x == seq[j - 1] or z in seen:
-                continue
-            seen.add(z)
-            lines.append((z, "F", seq[j + k - 1]))
-    order = rng.permutation(len(lines))
-    text = "".join(f"{lines[i][0]} {lines[i][1]}{lines[i][2]}\n" for i in order).encode()
-    return kh.pack_text(k, text)
+    """Packed records of cases.merging_walks_text (overlapping start walks, malformed input)."""
+    return kh.pack_text(k, merging_walks_text(k, L, seed, every))
 
 
 @pytest.mark.parametrize("k,L,every", [(19, 3000, 1), (51, 2000, 3)])

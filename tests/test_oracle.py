@@ -95,3 +95,26 @@ def test_parallel_oracle_generated_and_errors():
     assert ob.assemble_par(51, np.delete(recs, interior, axis=0), 4)[0] == -1
     rc, text, nc, nl, _, _ = ob.assemble_par(19, np.zeros((0, 7), np.uint8), 5)
     assert rc == 0 and text == b"" and nc == 0
+
+
+@pytest.mark.parametrize("k,L,every", [(19, 3000, 1), (51, 2000, 3)])
+def test_oracle_asan_merging_walks(tmp_path, k, L, every):
+    """The oracle built with -fsanitize=address (oracle/_asan/oracle_asan, CPU only) on the
+    overlapping-walks input of test_overlapping_walks_redo: text ~3L^2/2 bases, past every bound
+    sized from the record count. Round 5 lost a GPU-box test process to a SIGSEGV from a heap
+    overflow in ko_assemble on exactly this input (fixed by its realloc guards); ASan makes any
+    regression fail here. The serial and thread-parallel oracles must agree, and equal the
+    ctypes-loaded oracle's text."""
+    import subprocess
+    from cases import merging_walks_text
+    subprocess.run(["make", "-s", "-C", ob.ORACLE_DIR, "asan"], check=True)
+    text = merging_walks_text(k, L, seed=7 + k, every=every)
+    src, out = tmp_path / "in.txt", tmp_path / "out.dat"
+    src.write_bytes(text)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=99")
+    r = subprocess.run([os.path.join(ob.ORACLE_DIR, "_asan", "oracle_asan"), str(k), "3", str(src), str(out)],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = out.read_bytes()
+    rc, want, _, _, _, _ = ob.assemble(k, ob.parse_text(k, text))
+    assert rc == 0 and got == want and len(got) > 4 * len(text) // (k + 4)
