@@ -23,8 +23,12 @@ The SPMD driver below is written against two small interfaces so that the same c
 The C++ host of the same protocol is include/cs267_hw3_amd/dist_hash_map.hpp.
 """
 import ctypes
+import datetime
+import faulthandler
 import os
+import sys
 import threading
+import time
 
 import torch  # before the C ABI library is loaded: one HIP runtime for both
 
@@ -34,7 +38,14 @@ from ._lib import check
 
 # --------------------------------------------------------------------------------------------
 # Communicators
-def init_rank_process_group():
+# A collective that never completes (a rank that died or took another branch) must end the job,
+# naming where it stopped: the process group times out after KH_DIST_TIMEOUT seconds (RCCL: torch's
+# watchdog tears the communicator down, TORCH_NCCL_ASYNC_ERROR_HANDLING=1), and StepWatchdog ends a
+# rank whose step outlives its limit, printing the phase it was in and every thread's stack.
+DIST_TIMEOUT_S = float(os.environ.get("KH_DIST_TIMEOUT", "300"))
+
+
+def init_rank_process_group(timeout_s=None):
     """One process per GPU: LOCAL_RANK's device, RCCL (backend "nccl") over xGMI. Returns the
     device index. Rehearsal of the multi-process path on a box with fewer GPUs than ranks:
     KH_DIST_DEVICE=<d> puts every local rank on device d and KH_DIST_BACKEND=gloo moves the
@@ -46,8 +57,89 @@ def init_rank_process_group():
     dev = int(shared) if shared else local
     torch.cuda.set_device(dev)
     backend = os.environ.get("KH_DIST_BACKEND", "nccl")
-    dist.init_process_group(backend, device_id=torch.device("cuda", dev) if backend == "nccl" else None)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    to = datetime.timedelta(seconds=timeout_s if timeout_s is not None else DIST_TIMEOUT_S)
+    dist.init_process_group(backend, timeout=to,
+                            device_id=torch.device("cuda", dev) if backend == "nccl" else None)
     return dev
+
+
+class StepWatchdog:
+    """Ends this rank (exit status 3) when a step outlives `limit_s`, after printing the phase the
+    driver was in (DistributedKmerHashMap.phase) and every thread's Python stack: a stuck
+    collective then names itself instead of hanging the job. faulthandler's own timer (which
+    needs no GIL) backs it up 30 s later."""
+
+    EXIT_CODE = 3
+
+    def __init__(self, limit_s, rank, phase_of):
+        self.limit_s = float(limit_s)
+        self.rank = rank
+        self.phase_of = phase_of
+        self._timer = None
+
+    def _fire(self):
+        print(f"[rank {self.rank}] step exceeded {self.limit_s:.0f} s in phase "
+              f"'{self.phase_of()}': exiting", file=sys.stderr, flush=True)
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        sys.stderr.flush()
+        os._exit(self.EXIT_CODE)
+
+    def arm(self):
+        self.disarm()
+        self._timer = threading.Timer(self.limit_s, self._fire)
+        self._timer.daemon = True
+        self._timer.start()
+        faulthandler.dump_traceback_later(self.limit_s + 30, exit=True)
+
+    def disarm(self):
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+            faulthandler.cancel_dump_traceback_later()
+
+
+def guarded_step(dm, dog, body):
+    """Run one SPMD step under the watchdog; any exception (a collective that timed out, a peer's
+    failure) ends this rank with StepWatchdog.EXIT_CODE after naming the driver's phase."""
+    dog.arm()
+    try:
+        body()
+    except Exception as ex:
+        print(f"[rank {dog.rank}] step failed in phase '{dm.phase}': {ex!r}", file=sys.stderr, flush=True)
+        sys.stderr.flush()
+        os._exit(StepWatchdog.EXIT_CODE)
+    dog.disarm()
+
+
+class PhaseTimer:
+    """Time of each driver phase on this rank's stream: mark(name) ends the interval named `name`
+    (HIP events on the current stream, read after the step's synchronize; host clock on CPU)."""
+
+    def __init__(self, cuda):
+        self.cuda = cuda
+        self.marks = []
+
+    def reset(self):
+        self.marks = []
+
+    def mark(self, name):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.marks.append((name, e))
+        else:
+            self.marks.append((name, time.perf_counter()))
+
+    def totals(self):
+        """{phase: ms} summed over the step's intervals (call after synchronize)."""
+        out, prev = {}, None
+        for name, e in self.marks:
+            if prev is not None:
+                dt = prev.elapsed_time(e) if self.cuda else 1e3 * (e - prev)
+                out[name] = out.get(name, 0.0) + dt
+            prev = e
+        return out
 
 
 class TorchComm:
@@ -399,6 +491,33 @@ class DistributedKmerHashMap:
         self._caps_walkers = 0  # ... whose walker count (another count: another input, not used)
         self._cap_floor = 0     # this assemble: the demand of rounds that held messages back
         self._rounds_hint = 0   # its round count (the next assemble checks for the end there first)
+        self.phase = "idle"     # the driver phase running now (StepWatchdog names it on a hang)
+        self._cur = None
+        self.timer = None       # a PhaseTimer: per-phase stream time of the step (bench)
+        self.xbytes = 0         # bytes this rank sent to other ranks in the step (all exchanges)
+
+    # tests: stall this rank when it begins phase HANG_AT[0] (HANG_AT[1] = the rank) — a rank that
+    # never reaches the next collective, as a crashed or diverged peer would look to the others
+    HANG_AT = None
+
+    def _begin(self, name):
+        """Phase `name` begins (and the one before it ends: the timer labels the interval)."""
+        if self.timer is not None:
+            self.timer.mark(self._cur)
+        self._cur = name
+        self.phase = name
+        if self.HANG_AT is not None and tuple(self.HANG_AT) == (name, self.comm.rank):
+            time.sleep(3600)
+
+    def _end(self):
+        if self.timer is not None and self._cur is not None:
+            self.timer.mark(self._cur)
+        self._cur = None
+        self.phase = "idle"
+
+    def _sent(self, splits, elem_bytes):
+        """Count the bytes of an exchange's splits that leave this rank (not its own block)."""
+        self.xbytes += sum(int(x) for q, x in enumerate(splits) if q != self.comm.rank) * elem_bytes
 
     def close(self):
         pass
@@ -442,6 +561,7 @@ class DistributedKmerHashMap:
         send = torch.stack([counts[:P], counts[P:P + 1].expand(P), mx.expand(P), ex.expand(P)], 1)
         send = send.contiguous().view(-1)
         recv = torch.empty_like(send)
+        self._sent([4] * P, 8)
         self.comm.all_to_all(recv, send, [4] * P, [4] * P)
         host = self._host(torch.cat([send, recv])).view(2, P, 4)
         send_splits = host[0, :, 0].tolist()
@@ -458,6 +578,7 @@ class DistributedKmerHashMap:
         limit = max(1, self.A2A_CHUNK_BYTES // inp.element_size())
         rounds = (gmax_elems + limit - 1) // limit
         P = self.P
+        self._sent(in_splits, inp.element_size())
         if rounds <= 1 and in_off is None:
             self.comm.all_to_all(out, inp, out_splits, in_splits)
             return
@@ -519,6 +640,7 @@ class DistributedKmerHashMap:
             recv = send
         else:
             recv = torch.empty_like(send)
+            self._sent([w] * P, 8)
             self.comm.all_to_all(recv, send, [w] * P, [w] * P)
         host = self._host(torch.cat([send, recv])).view(2, P, w)
         send_c = [[int(host[0, q, c]) for q in range(P)] for c in range(nch)]
@@ -540,11 +662,17 @@ class DistributedKmerHashMap:
         n = recs.shape[0]
         exchange = P > 1 or self.SELF_EXCHANGE
         self._err = None
+        if self.timer is not None:  # a step = insert_all + assemble
+            self.timer.reset()
+            self._cur = None
+        self.xbytes = 0
         if not exchange and not self.ROUTE_ONE_RANK and hasattr(sh, "insert_records"):
             # one rank: every key is this shard's and nothing moves (as the count exchanges are
             # skipped): the records pass partitions them itself, no owner route + word re-partition
+            self._begin("insert")
             sh.reserve(n)
             sh.insert_records(recs)
+            self._begin("counts")
             c = self._host(sh.counters())      # the walk's start / splitter counts
             self._ns, self._nsp = int(c[0]), int(c[1])
             self._walkers, self._splitters = self._ns + self._nsp, self._nsp
@@ -570,6 +698,7 @@ class DistributedKmerHashMap:
         else:
             words = self._grow("_ins_words", max(n, 1) * W, torch.int64, recs.device)
         counts = []
+        self._begin("route")
         for c in range(nch):
             c0, c1 = bounds[c], bounds[c + 1]
             if windows:
@@ -584,6 +713,7 @@ class DistributedKmerHashMap:
             else:
                 offs = [c0 * W + sum(send[:q]) * W for q in range(P)]
             return [words[offs[q]:offs[q] + send[q] * W] for q in range(P)], offs
+        self._begin("counts")
         spl = sh.route_splitters(P)
         cnt = sh.counters()
         mine = torch.stack([cnt[0], spl[:P].sum()])
@@ -596,13 +726,16 @@ class DistributedKmerHashMap:
         except RuntimeError as ex:  # KmerHashError (NOMEM) or a test shard's error
             self._err, ok = ex, False
         if not exchange:
+            self._begin("partition_build")
             if ok:
                 sh.insert_words(words, m)      # one rank: the routed words are this shard's
             return m
         recv = self._grow("_ins_recv", max(m, 1) * W, torch.int64, recs.device)
         if nch == 1:
+            self._begin("exchange_wait")
             self._all_to_all(recv[:m * W], words, [x * W for x in recv_c[0]],
                              [x * W for x in send_c[0]], gmax * W, in_off=views(0, send_c[0])[1])
+            self._begin("partition_build")
             if ok:
                 sh.insert_words(recv, m)
             return m
@@ -613,18 +746,24 @@ class DistributedKmerHashMap:
             for q in range(P):
                 outs.append(recv[o * W:(o + recv_c[c][q]) * W])
                 o += recv_c[c][q]
+            self._sent(send_c[c], W * 8)
             works.append(self.comm.all_to_all_views_async(outs, views(c, send_c[c])[0]))
             spans.append((pos, mc))
             pos += mc
             if c > 0:  # previous chunk received: partition it while this one is on the wire
+                self._begin("exchange_wait")
                 works[c - 1].wait()
+                self._begin("partition")
                 p0, pm = spans[c - 1]
                 if ok:
                     sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
+        self._begin("exchange_wait")
         works[-1].wait()
+        self._begin("partition")
         p0, pm = spans[-1]
         if ok:
             sh.stage_words(recv[p0 * W:(p0 + pm) * W], pm, m)
+            self._begin("build")
             sh.finish_words()
         return m
 
@@ -668,6 +807,7 @@ class DistributedKmerHashMap:
         dev = sh.zeros(1, torch.int64).device
         local = P == 1 and not self.SELF_EXCHANGE
         failed = self._err is not None  # this shard could not be sized: it sends nothing until the check
+        self._begin("walk_init")
         if not failed:
             sh.mw_begin(P, self.comm.rank, total_kmers, self._ns, self._nsp, self._walkers)
         self.rounds = self.checks = 0
@@ -689,6 +829,7 @@ class DistributedKmerHashMap:
             sw = _lib.slot_words(cap)
             out = self._grow("_mw_out_%d" % (self.rounds & 1), P * sw, torch.int64, dev)
             lv = 2 * (self.rounds - base)
+            self._begin("walk_rounds")
             if failed:
                 out.view(-1)[:P * sw].view(P, sw)[:, 0] = 0
                 live[lv:lv + 2] = 0
@@ -698,11 +839,14 @@ class DistributedKmerHashMap:
                 nxt = out      # one rank: slot 0 is the next round's input
             else:
                 nxt = self._grow("_mw_in_%d" % (self.rounds & 1), P * sw, torch.int64, dev)
+                self._begin("walk_exchange")
+                self._sent([sw] * P, 8)
                 self.comm.all_to_all(nxt[:P * sw], out[:P * sw], [sw] * P, [sw] * P)
             inp, cap_in = nxt, cap
             self.rounds += 1
             if self.rounds >= check_at or self.rounds >= limit:
                 # global max of the window's [in flight, largest per-destination] + errors
+                self._begin("walk_check")
                 nw = 2 * (self.rounds - base)
                 if local:  # one rank: no reduction, the error is this rank's own
                     h = self._host(live[:nw]).tolist() + [1 if self._err is not None else 0]
@@ -732,6 +876,7 @@ class DistributedKmerHashMap:
         self._caps = [max(256, int(x) * 5 // 4 + 256) for x in maxes]
         self._rounds_hint = self.rounds
         self._caps_walkers = self._walkers
+        self._begin("text_group")
         tb = sh.mw_text_bound()
         tout = self._grow("_mw_tout", max(tb, 1) * T, torch.int64, dev)
         counts = sh.mw_text(tout)
@@ -740,6 +885,7 @@ class DistributedKmerHashMap:
         if local:
             trecv = tout
         else:
+            self._begin("text_exchange")
             trecv = self._grow("_mw_trecv", max(r, 1) * T, torch.int64, dev)
             self._all_to_all(trecv[:r * T], tout[:sum(send_splits) * T], [c * T for c in recv_splits],
                              [c * T for c in send_splits], gmax * T)
@@ -747,12 +893,18 @@ class DistributedKmerHashMap:
         if self._splitters and hasattr(sh, "mw_segments"):
             self._segments_end(trecv, r, self._ns + self._nsp)
         else:
+            self._begin("materialize")
             sh.mw_end(trecv, r)
         sh.sync()  # the library counts this one (kh_sync)
+        self._end()
         return self.rounds
 
     CHECK_EVERY = 4
-    MAX_ROUNDS = 4096  # with splitter segments (the default) C5's 10^6-k-mer chains take ~11
+    MAX_ROUNDS = 4096
+    # every phase name _begin uses, in step order (the bench line reports them in this order)
+    PHASES = ("insert", "route", "counts", "exchange_wait", "partition", "partition_build", "build",
+              "walk_init", "walk_rounds", "walk_exchange", "walk_check", "text_group", "text_exchange",
+              "seg_link", "seg_resolve", "seg_retag", "materialize")  # with splitter segments (the default) C5's 10^6-k-mer chains take ~11
 
     def _segments_end(self, trecv, r, nseg):
         """Splitter segments: link each segment to its successor's owner, all-gather every rank's
@@ -762,6 +914,7 @@ class DistributedKmerHashMap:
         dev = trecv.device
         L, S, PW = sh.LINK_WORDS, sh.SEG_REC_WORDS, sh.PRED_WORDS
         local = P == 1 and not self.SELF_EXCHANGE  # one rank: every exchange is the identity
+        self._begin("seg_link")
         lout = self._grow("_ms_links", max(nseg, 1) * L, torch.int64, dev)
         counts = sh.mw_link(trecv, r, lout)
         if local:
@@ -777,6 +930,7 @@ class DistributedKmerHashMap:
             lin = self._grow("_ms_links_in", max(m, 1) * L, torch.int64, dev)
             self._all_to_all(lin[:m * L], lout[:sum(send_splits) * L], [c * L for c in recv_splits],
                              [c * L for c in send_splits], gmax * L)
+        self._begin("seg_resolve")
         stride = max(int(x) for x in nsps)
         preds = self._grow("_ms_preds", max(stride, 1) * PW, torch.int64, dev)
         sh.mw_pred(lin, m, preds, stride)
@@ -784,8 +938,10 @@ class DistributedKmerHashMap:
             allp = preds
         else:
             allp = self._grow("_ms_allp", max(P * stride, 1) * PW, torch.int64, dev)
+            self.xbytes += (P - 1) * stride * PW * 8
             self.comm.all_gather(allp[:P * stride * PW], preds[:stride * PW])
         sh.mw_resolve(allp, stride)
+        self._begin("seg_retag")
         tout = self._grow("_ms_t", max(r + nseg, 1) * S, torch.int64, dev)
         counts = sh.mw_retag(trecv, r, tout)
         send_splits, recv_splits, _, gmax, _ = self._exchange_counts(counts)
@@ -796,6 +952,7 @@ class DistributedKmerHashMap:
             tin = self._grow("_ms_tin", max(m, 1) * S, torch.int64, dev)
             self._all_to_all(tin[:m * S], tout[:sum(send_splits) * S], [c * S for c in recv_splits],
                              [c * S for c in send_splits], gmax * S)
+        self._begin("materialize")
         sh.mw_end_seg(trecv, r, tin, m)
 
     def contigs_text(self):
@@ -915,29 +1072,54 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
     # each shard holds ~n_total/world keys (it grows to what it is routed); 2 % slack
     shard = GpuShard(k, int(n_per * 1.02) + 4096, device=local, load_factor=getattr(args, "load", 0.5))
     dm = DistributedKmerHashMap(comm, shard)
+    dm.timer = PhaseTimer(cuda=True)
     R = record_size(k)
+    # a step (or the warmup, which also sizes every buffer) that outlives this ends the rank,
+    # naming the phase it is stuck in (a hung collective must not hang the job silently)
+    dog = StepWatchdog(float(os.environ.get("KH_DIST_STEP_TIMEOUT", DIST_TIMEOUT_S)), rank, lambda: dm.phase)
 
-    def step():
+    def body():
         with torch.cuda.stream(shard.stream):
             shard.clear()
             dm.insert_all(recs)
             dm.assemble(n_total)
 
+    def step():
+        guarded_step(dm, dog, body)
+
     for _ in range(args.warmup):
         step()
-    times, phases = [], []
+    times, phases, ptimes, xbytes, syncs = [], [], [], [], []
     for _ in range(args.steps):
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        s0 = dm.host_syncs()
         step()
         torch.cuda.synchronize()
         dist.barrier()
         times.append(time.perf_counter() - t0)
         phases.append(shard.stats())
+        ptimes.append(dm.timer.totals())
+        xbytes.append(dm.xbytes)
+        syncs.append(dm.host_syncs() - s0)
     print(f"[rank {rank}] step ms: " + " ".join(f"{1e3 * x:.2f}" for x in times), file=sys.stderr, flush=True)
     mine = sum(times) / len(times)
     tmax = comm.all_reduce_max(mine)
+    # per-rank phase times (mean over the timed steps) -> max / min over ranks, in PHASES order
+    names = list(DistributedKmerHashMap.PHASES)
+    mean_ph = [sum(p.get(nm, 0.0) for p in ptimes) / len(ptimes) for nm in names]
+    st0 = phases[-1]
+    per_rank = mean_ph + [sum(xbytes) / len(xbytes), max(syncs), st0["ms_build"], st0["ms_insert_kernel"],
+                          float(dm.rounds)]
+    hi = torch.tensor(per_rank, dtype=torch.float64, device="cuda")
+    lo = -hi.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MAX)
+    hi, lo = hi.tolist(), (-lo).tolist()
+    nph = len(names)
+    rank_phases = {nm: {"max": round(hi[i], 4), "min": round(lo[i], 4)} for i, nm in enumerate(names)
+                   if hi[i] > 0 or lo[i] > 0}
     st = phases[-1]
     tot = torch.tensor([st["n_starts"], st["n_lookups"]], dtype=torch.int64, device="cuda")
     dist.all_reduce(tot)
@@ -971,6 +1153,7 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
             rt.append(time.perf_counter() - t0)
         routed = {"ms_per_step": 1e3 * sum(rt) / len(rt),
                   "insert_pipeline_ms": shard.stats()["ms_insert_kernel"],
+                  "phases_ms": {nm: round(v, 4) for nm, v in dm.timer.totals().items()},
                   "verified_vs_truth": verify() if truth is not None else None}
         dm.ROUTE_ONE_RANK = False
     cpu = None
@@ -1009,6 +1192,13 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
             "inserts_per_s": n_total / tmax, "lookups_per_s": nl / tmax,
             "contigs_per_s": nc / tmax, "verified_vs_truth": ok,
             "phases_ms": {"insert_pipeline_rank0": ins_ms, "build_rank0": build_ms},
+            # per-rank stream time of each driver phase (HIP events), max / min over the ranks
+            "rank_phases_ms": rank_phases,
+            "rank_step_ms": {"max": tmax * 1e3, "mean_rank0": mine * 1e3},
+            "exchange_bytes_per_step": {"max": hi[nph], "min": lo[nph]},
+            "host_syncs_per_step": {"max": hi[nph + 1], "min": lo[nph + 1]},
+            "build_ms": {"max": hi[nph + 2], "min": lo[nph + 2]},
+            "insert_pipeline_ms": {"max": hi[nph + 3], "min": lo[nph + 3]},
             **({"routed_one_rank": routed} if routed else {}),
             "roofline": {"bound": "hbm", "kernel": "k_part_build_pf (rank 0's region build + chains over the "
                                                      "words it received)",

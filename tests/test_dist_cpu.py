@@ -143,3 +143,50 @@ def test_sharded_tiny_slots_gloo(tmp_path, name, world, cap):
     for r in range(world):
         b, e = g.block(world, r)
         assert open(tmp_path / f"test_{r}.dat", "rb").read() == g.truth(b, e)
+
+
+_HANG_SCRIPT = r"""
+import os, sys, datetime
+sys.path.insert(0, {tests!r}); sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+import cs267_hw3_amd as kh
+from cs267_hw3_amd.dist import DistributedKmerHashMap, TorchComm, StepWatchdog, guarded_step
+from dist_fake_shard import FakeShard
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                        timeout=datetime.timedelta(seconds={pg_timeout}))
+recs = torch.from_numpy(kh.read_kmers({path!r}, {k}, world, rank))
+dm = DistributedKmerHashMap(TorchComm(), FakeShard({k}))
+dm.HANG_AT = ({phase!r}, 1)
+dog = StepWatchdog({step_timeout}, rank, lambda: dm.phase)
+guarded_step(dm, dog, lambda: (dm.insert_all(recs), dm.assemble({n})))
+print("finished", flush=True)
+"""
+
+
+@pytest.mark.parametrize("phase", ["walk_rounds", "counts"])
+def test_sharded_hang_exits_nonzero(tmp_path, phase):
+    """A rank that never reaches the next collective (stalled at the start of `phase`): the peer's
+    collective times out with the process group (gloo, 4 s) and the stalled rank's StepWatchdog
+    (8 s) ends it; both exit with StepWatchdog.EXIT_CODE within the limits, each naming the phase
+    it was in — the behaviour an 8-GPU run needs when a collective hangs."""
+    import subprocess
+    import sys
+    import time
+    name = "small51"
+    m = MANIFEST[name]
+    script = _HANG_SCRIPT.format(tests=HERE, root=os.path.dirname(HERE), port=_free_port(), pg_timeout=4,
+                                 path=os.path.join(GOLDEN, f"{name}.txt"), k=m["k"], n=m["n"], phase=phase,
+                                 step_timeout=8)
+    t0 = time.time()
+    procs = [subprocess.Popen([sys.executable, "-c", script], env=dict(os.environ, RANK=str(r), WORLD_SIZE="2"),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    elapsed = time.time() - t0
+    from cs267_hw3_amd.dist import StepWatchdog
+    for r, (p, (out, err)) in enumerate(zip(procs, outs)):
+        assert p.returncode == StepWatchdog.EXIT_CODE, (r, p.returncode, err[-2000:])
+        assert "finished" not in out
+        assert f"[rank {r}]" in err and "phase '" in err, err[-2000:]
+    assert f"phase '{phase}'" in outs[1][1]       # the stalled rank names where it stopped
+    assert elapsed < 60

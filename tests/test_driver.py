@@ -121,6 +121,15 @@ def test_bench_self_launch(tmp_path):
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
     assert line["n_gpus"] == 2 and line["verified_vs_truth"] is True
     assert line["config"]["n_kmers_total"] == 4_000_000
+    # the diagnosable N > 1 line: per-rank phase times (max / min over ranks), bytes sent to other
+    # ranks per step, host syncs per step
+    ph = line["rank_phases_ms"]
+    for name in ("route", "counts", "exchange_wait", "partition", "build", "walk_rounds", "walk_exchange",
+                 "text_group", "text_exchange", "materialize"):
+        assert name in ph and ph[name]["max"] >= ph[name]["min"] >= 0, (name, ph)
+    assert line["exchange_bytes_per_step"]["min"] > 0
+    assert 1 <= line["host_syncs_per_step"]["max"] <= 12
+    assert line["rank_step_ms"]["max"] > 0
 
 
 def test_bench_world_size_mismatch_fails(tmp_path):
