@@ -93,6 +93,7 @@ _SIGS = {
     "kh_host_syncs": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "kh_route_splitters_dev": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int]),
     "kh_counters_dev": (ctypes.c_int, [c_vp, c_vp]),
+    "kh_counters": (ctypes.c_int, [c_vp, c_vp]),
     "kh_mwalk_begin": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, c_u64, c_u64, c_u64, c_u64,
                                       ctypes.POINTER(c_u64)]),
     "kh_mwalk_round_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_u64, c_vp]),

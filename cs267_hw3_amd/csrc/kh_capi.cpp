@@ -116,9 +116,10 @@ struct kh_table {
     uint64_t stage_total = 0, stage_n = 0;
     uint64_t collected_n = 0;  // records passed to kh_route_starts_dev since the last clear
     bool slots_stale = true;   // cleared lazily: a partitioned build of an empty table writes every slot
-    DevBuf mw_init, mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
+    DevBuf mw_tmp, mw_dst, mw_stage, mw_nrec, mw_off, mw_misc, mw_store;  // migrating walk
     // splitter segments of the migrating walk (kh_mseg.hip)
     DevBuf ms_len, ms_hi, ms_lo, ms_has, ms_done, ms_jump, ms_acc, ms_stab, ms_stab_id, ms_qsrc, ms_misc;
+    bool ms_chunks = false;  // the record scan filled the origin's first chunks (line writer)
     DevBuf mw_cnt, mw_list, mw_carry[2], mw_carry_dst[2];  // fixed-slot rounds
     DevBuf ms_res[6], ms_pend;               // pointer jumping over the gathered predecessor tables
     DevBuf route_spl;                        // splitter k-mers routed to each owner (MAX_RANKS words)
@@ -414,7 +415,7 @@ int kh_destroy(kh_table* t) {
                       &t->route_hist, &t->route_off, &t->route_scratch, &t->route_own, &t->splits, &t->splits_w, &t->seg_next,
                       &t->seg_key, &t->seg_contig, &t->seg_off, &t->clen, &t->stab, &t->stab_id,
                       &t->seg_jump, &t->seg_jsum, &t->seg_anchor, &t->seg_pend,
-                      &t->mw_init, &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
+                      &t->mw_tmp, &t->mw_dst, &t->mw_stage, &t->mw_nrec, &t->mw_off,
                       &t->mw_misc, &t->mw_store, &t->ms_len, &t->ms_hi, &t->ms_lo, &t->ms_has, &t->ms_done,
                       &t->ms_jump, &t->ms_acc, &t->ms_stab, &t->ms_stab_id, &t->ms_qsrc, &t->ms_misc,
                       &t->mw_cnt, &t->mw_list, &t->mw_carry[0], &t->mw_carry[1], &t->mw_carry_dst[0],
@@ -1243,6 +1244,23 @@ int kh_counters_dev(kh_table* t, void* dev_out) {
     return KH_OK;
 }
 
+int kh_counters(kh_table* t, uint64_t* out) {
+    if (!t || !out) return fail(KH_ERR_ARG, "null argument");
+    if (int rc = set_device(t)) return rc;
+    unsigned long long cv[kh::CT_NUM];
+    ++t->host_syncs;
+    if (t->ctr_early) {  // copied beside the build (kh_insert_dev): wait for that copy, not the build
+        KH_HIP(hipEventSynchronize(t->ev_ctr));
+        memcpy(cv, t->hctr, sizeof cv);
+    } else {
+        KH_HIP(hipMemcpyAsync(cv, t->ctr.p, sizeof cv, hipMemcpyDeviceToHost, t->stream));
+        KH_HIP(hipStreamSynchronize(t->stream));
+    }
+    out[0] = cv[kh::CT_N_STARTS];
+    out[1] = cv[kh::CT_N_SPLIT];
+    return KH_OK;
+}
+
 int kh_insert_words_dev(kh_table* t, const void* words, uint64_t m) {
     if (!t) return fail(KH_ERR_ARG, "null table");
     t->ctr_early = false;  // counters may change: assemble reads them on the stream
@@ -1417,8 +1435,7 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     // and leaves at most a partial word, its finish record and a 2-record link where it ends
     // (held-back walkers flush nothing extra): shard / 32 + 4 per walker of every rank, doubled
     const uint64_t store_cap = 2 * (t->n_inserted / 32 + 4 * t->mw_wg) + 4096;
-    if ((rc = t->mw_init.ensure((nseg + 1) * kh::MSG_WORDS * 8)) || (rc = t->mw_misc.ensure(64)) ||
-        (rc = t->mw_store.ensure(store_cap * 16)))
+    if ((rc = t->mw_misc.ensure(64)) || (rc = t->mw_store.ensure(store_cap * 16)))
         return rc;
     t->ms_ns = ns;
     t->ms_nsp = nsp;
@@ -1449,15 +1466,10 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     KH_HIP(hipMemsetAsync(mw_word(t, 2), 0, 8 * 4, t->stream));  // store count, walkers, carries
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
     t->wk_timed = false;
-    // chain records: every walker whose k-mer heads a record starts from it (k_mw_init), and the
-    // records' successor runs are resolved beside the first round (k_rec_succ, as on one GPU)
+    // chain records: the first round's walkers read the start and splitter lists themselves and
+    // look up their own k-mer first (a record covering its run is read next, as on one GPU), and
+    // the records' successor runs are resolved beside the first round (k_rec_succ)
     kh::KParams ikp = t->kp;
-    const uint32_t hcap = (t->headrec.p && t->kp.chain &&
-                           (uint64_t)t->hcap * (1ull << t->kp.rbits) < 0xFFFFFFFFull)
-                              ? t->hcap
-                              : 0u;
-    KH_HIP(kh::launch_mw_init(ikp, view(t), hcap, t->starts.as<uint64_t>(), ns, (uint32_t)rank,
-                              t->mw_init.as<uint64_t>(), t->stream));
     if (t->headrec.p && t->hcap && kh::rec_succ_fits(ikp, t->hcap)) {
         hipStream_t rs = t->stream;
         if (kh::rec_succ_side(ikp) && t->side) {
@@ -1468,11 +1480,12 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
         }
         KH_HIP(kh::launch_rec_succ(ikp, view(t), t->headrec.as<uint64_t>(), t->hcap, rs,
                                    t->succ_pending ? 1024u : 0u));
-        if (t->succ_pending) KH_HIP(hipEventRecord(t->ev_conv, t->side));
     }
+    if (t->succ_pending) KH_HIP(hipEventRecord(t->ev_conv, t->side));
     if (t->ms_on) {
-        KH_HIP(kh::launch_mw_init(ikp, view(t), hcap, t->splits.as<uint64_t>(), nsp, (uint32_t)rank,
-                                  t->mw_init.as<uint64_t>() + ns * kh::MSG_WORDS, t->stream, ns));
+        // (on the side stream beside the first round, behind the record resolve, the splitter
+        // table's 780K CAS slowed the round as much as they saved: C3 walk init + rounds 1.51 vs
+        // 1.53 ms)
         KH_HIP(kh::launch_mseg_init(ns, nseg, (uint32_t)rank, mseg_state(t), t->stream));
         KH_HIP(kh::launch_mseg_stab(t->kp, t->splits.as<uint64_t>(), nsp, t->ms_stab.as<uint64_t>(),
                                     t->ms_stab_id.as<uint32_t>(), t->ms_cap2, t->stream));
@@ -1492,8 +1505,8 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
     if (int rc = set_device(t)) return rc;
     const uint32_t P = t->mw_P;
     int rc;
-    // this round's walkers: the begin's (first round), or the P slots received
-    const uint64_t* src = t->mw_init.as<uint64_t>();
+    // this round's walkers: the start and splitter lists (first round), or the P slots received
+    const uint64_t* src = nullptr;
     uint64_t nb = t->rw_n;  // bound (every walker is live in the first round)
     unsigned long long* n_dev = mw_word(t, 3);
     if (t->mw_stepped) {
@@ -1501,7 +1514,7 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
         if (nb > t->mw_wg) nb = t->mw_wg;  // walkers never multiply
         if ((rc = t->mw_list.ensure((nb + 1) * kh::MSG_WORDS * 8))) return rc;
         KH_HIP(kh::launch_slot_gather((const uint64_t*)in_slots, P, in_cap, t->mw_list.as<uint64_t>(), n_dev, nb,
-                                      t->stream));
+                                      t->stream, t->stats.as<unsigned long long>()));
         src = t->mw_list.as<uint64_t>();
     } else {
         KH_HIP(kh::launch_add_count(n_dev, t->rw_n, nullptr, 0, t->stream));
@@ -1523,6 +1536,9 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
     mw.hcap = t->headrec.p ? t->hcap : 0u;
     mw.max_steps = t->rw_total;
     mw.in = src;
+    mw.starts = t->starts.as<uint64_t>();
+    mw.splits = t->splits.as<uint64_t>();
+    mw.ns = t->ms_ns;
     mw.n_in = nb;
     mw.n_dev = n_dev;
     mw.hot_on = t->ctr.as<unsigned long long>() + kh::CT_HOT;  // the kernel skips the bitmap when 0
@@ -1584,6 +1600,40 @@ int kh_mwalk_text_dev(kh_table* t, void* out, void* counts) {
     return KH_OK;
 }
 
+// The origin's line writer (K >= 16): its word-major first chunks (chunk c = contig c, filled by
+// the record scan, k_mw_lens / k_mseg_scan), or null at K < 16.
+static uint64_t* origin_chunks(kh_table* t, uint64_t nc) {
+    if (t->kp.K < 16 || nc == 0 || t->chunk_data.ensure(nc * kh::CHUNK_WORDS * 8)) return nullptr;
+    return t->chunk_data.as<uint64_t>();
+}
+
+// The origin's text, first part (after the contig offsets): at K >= 16 the line writer stores
+// every line whole — heads, each contig's first CHUNK_BASES bases of its start segment (from the
+// first chunks origin_chunks gave the record scan), newlines — and the word writers that follow
+// cover the rest (start-segment words >= CHUNK_WORDS, splitter segments); at K < 16 the heads
+// writer runs and the word writers cover every word. Returns the word writers' first word number
+// (kh::WMIN_ERR: no memory). slen[c] + slen_add = k-mers of contig c's start segment.
+static uint32_t origin_lines(kh_table* t, uint64_t nc, const uint32_t* clen, int slen_add, const uint32_t* slen,
+                             bool chunks) {
+    unsigned long long* ctr = t->ctr.as<unsigned long long>();
+    if (chunks && t->kp.K >= 16 && nc) {
+        if (t->line_first.ensure(kh::line_first_words(t->text.bytes) * 4)) return kh::WMIN_ERR;
+        kh::WalkBuffers wb{};
+        wb.starts = t->starts.as<uint64_t>();
+        wb.n_starts = nc;
+        wb.contig_len = const_cast<uint32_t*>(slen);
+        wb.chunk_data = t->chunk_data.as<uint64_t>();
+        wb.chunk_cap = nc;
+        if (kh::launch_text_lines(t->kp, wb, clen, slen_add, t->contig_off.as<uint64_t>(), t->text.as<char>(), ctr,
+                                  t->stream, t->text.bytes, t->line_first.as<uint32_t>(), t->text.bytes))
+            return kh::CHUNK_WORDS;
+    }
+    if (kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, clen, t->contig_off.as<uint64_t>(),
+                               t->text.as<char>(), t->stream, t->text.bytes) != hipSuccess)
+        return kh::WMIN_ERR;
+    return 0;
+}
+
 // the contig text bytes: at most K + 1 per contig + 32 per word record (no device read)
 static int text_for(kh_table* t, uint64_t nc, uint64_t word_recs) {
     return t->text.ensure(nc * (uint64_t)(t->kp.K + 1) + 32 * word_recs + 64);
@@ -1604,8 +1654,9 @@ int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
     KH_HIP(hipEventRecord(t->ev_walk1, t->stream));
     KH_HIP(hipMemsetD32Async((hipDeviceptr_t)t->contig_len.p, 1, nc + 1, t->stream));
     KH_HIP(hipMemsetAsync(ctr + kh::CT_MW_FIN, 0, 8, t->stream));
+    uint64_t* chunks = origin_chunks(t, nc);
     KH_HIP(kh::launch_mw_lens((const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(), ctr + kh::CT_MW_FIN,
-                              t->stream));
+                              t->stream, chunks));
     // every walker came home (else kh_sync reports KH_ERR_NOT_FOUND)
     KH_HIP(kh::launch_fin_check(ctr + kh::CT_MW_FIN, nc, nullptr, 0, t->stats.as<unsigned long long>(), t->stream));
     KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
@@ -1613,10 +1664,10 @@ int kh_mwalk_end_dev(kh_table* t, const void* recs, uint64_t n) {
     if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
     // the text is sized from a host bound (no device read): every writer stops at its end, so a
     // corrupt length or an overflowed store fails at kh_sync instead of writing past it
-    KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
-                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream, t->text.bytes));
+    const uint32_t wmin = origin_lines(t, nc, t->contig_len.as<uint32_t>(), 0, t->contig_len.as<uint32_t>(), chunks);
+    if (wmin == kh::WMIN_ERR) return KH_ERR_NOMEM;
     KH_HIP(kh::launch_mw_words(t->kp.K, (const uint64_t*)recs, n, nc, t->contig_len.as<uint32_t>(),
-                               t->contig_off.as<uint64_t>(), t->text.as<char>(), t->text.bytes, t->stream));
+                               t->contig_off.as<uint64_t>(), t->text.as<char>(), t->text.bytes, t->stream, wmin));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = nc;
@@ -1640,9 +1691,13 @@ int kh_mwalk_link_dev(kh_table* t, const void* recs, uint64_t n, void* out, void
     if (nseg && !out) return fail(KH_ERR_ARG, "null output");
     if (int rc = ensure_route(t, nseg, (int)t->mw_P)) return rc;
     unsigned long long* fin = t->ms_misc.as<unsigned long long>();
-    KH_HIP(hipMemsetAsync(fin, 0, 8, t->stream));
+    // [0] finished segments, [1] the splitter count (kh_mwalk_pred_dev), [2] start-segment words
+    // past the line writer's first chunks
+    KH_HIP(hipMemsetAsync(fin, 0, 24, t->stream));
     const kh::MSegState st = mseg_state(t);
-    KH_HIP(kh::launch_mseg_scan((const uint64_t*)recs, n, nseg, st, fin, t->stream));
+    t->ms_chunks = origin_chunks(t, t->ms_ns) != nullptr;
+    KH_HIP(kh::launch_mseg_scan((const uint64_t*)recs, n, nseg, st, fin, t->stream,
+                                t->ms_chunks ? t->chunk_data.as<uint64_t>() : nullptr, t->ms_ns, fin + 2));
     // every segment's walker came home (else kh_sync reports KH_ERR_NOT_FOUND)
     KH_HIP(kh::launch_fin_check(fin, nseg, nullptr, 0, t->stats.as<unsigned long long>(), t->stream));
     KH_HIP(kh::launch_mseg_link(t->kp, st, t->ms_ns, nseg, t->mw_P, t->mw_rank, t->route_hist.as<uint64_t>(),
@@ -1719,10 +1774,11 @@ int kh_mwalk_end_seg_dev(kh_table* t, const void* recs, uint64_t n, const void* 
     KH_HIP(kh::launch_contig_offsets(t->kp.K, t->contig_len.as<uint32_t>(), nc, t->contig_off.as<uint64_t>(),
                                      t->scratch.as<uint64_t>(), ctr + kh::CT_OUT_BYTES, t->stream));
     if (nc == 0) KH_HIP(hipMemsetAsync(ctr + kh::CT_OUT_BYTES, 0, 8, t->stream));
-    KH_HIP(kh::launch_write_heads(t->kp, t->starts.as<uint64_t>(), nc, t->contig_len.as<uint32_t>(),
-                                  t->contig_off.as<uint64_t>(), t->text.as<char>(), t->stream, t->text.bytes));
+    const uint32_t wmin = origin_lines(t, nc, t->contig_len.as<uint32_t>(), 1, st.len, t->ms_chunks);
+    if (wmin == kh::WMIN_ERR) return KH_ERR_NOMEM;
     KH_HIP(kh::launch_mseg_words(t->kp.K, (const uint64_t*)recs, n, (const uint64_t*)seg_recs, m, nc, st,
-                                 t->contig_off.as<uint64_t>(), t->text.as<char>(), t->text.bytes, t->stream));
+                                 t->contig_off.as<uint64_t>(), t->text.as<char>(), t->text.bytes, t->stream, wmin,
+                                 wmin ? t->ms_misc.as<unsigned long long>() + 2 : nullptr));
     KH_HIP(hipEventRecord(t->ev_mat1, t->stream));
     t->walk_timed = true;
     t->last_contigs = nc;

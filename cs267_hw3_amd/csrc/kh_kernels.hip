@@ -341,7 +341,8 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
 
     bool active = false, done = false, resolved = false;
     bool entry = false;  // looking up the walker's own start k-mer (fwd = the start record's)
-    uint64_t c = 0, s = 0, buf = 0;
+    uint64_t c = 0, s = 0, buf = 0, pb = 0;   // pb: 4-slot blocks probed for the current k-mer
+    const uint64_t pb_max = (cap >> 2) + 1;   // every block once: the k-mer is absent (a full table)
     uint32_t reg = 0;  // region of the k-mer being looked up (its head records live there)
     Key k{0, 0};
     uint32_t fwd = 0, steps = 0, chunk = 0;
@@ -449,6 +450,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                 nrec = 0;
             } else {     // look up k: s = its home slot (the hit may carry a head-record index)
                 s = home_of(pl, cap, p);
+                pb = 0;
             }
             resolved = false;
             do_place = false;
@@ -539,7 +541,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                     }
                 }
                 entry = false;
-            } else if (myfe < 4u) {
+            } else if (myfe < 4u || ++pb > pb_max) {
                 if (entry) {  // a start k-mer need not be in the table (kh_set_starts)
                     resolved = true;
                     entry = false;
@@ -580,9 +582,10 @@ __global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t
     const uint32_t r_end = min(r + rpw, NR);
     uint32_t id = 0;
     // lane state: its record (index + 1, 0 = idle), y, the probe position (WQ_IDLE: record load)
-    uint64_t rec = 0, s = WQ_IDLE, x0 = 0;
+    uint64_t rec = 0, s = WQ_IDLE, x0 = 0, pb = 0;  // pb: 4-slot blocks probed for y
     Key y{0, 0};
     bool fetch = false;
+    const uint64_t pb_max = (cap >> 2) + 1;  // every block once: y is absent (a full table)
     while (true) {
         // refill idle lanes from the queue (uniform loop: one region per sub-step)
         uint64_t idle = __ballot(rec == 0);
@@ -656,6 +659,7 @@ __global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t
                 if (f <= 3u) {
                     y = key_next(slot_key(rv.x, rv.y, p), f, p);
                     s = home_of(place(y, p), cap, p);
+                    pb = 0;
                 } else {
                     done = true;  // the run ends its contig: no successor
                 }
@@ -663,7 +667,7 @@ __global__ __launch_bounds__(BLOCK) void k_rec_succ(KParams p_in, const uint64_t
             } else if (myfh < myfe) {
                 succ = myidx;
                 done = true;
-            } else if (myfe < 4u) {
+            } else if (myfe < 4u || ++pb > pb_max) {
                 done = true;      // y is not in the table (the walker reports it)
             } else {
                 const uint64_t nx = (s & ~3ull) + 4;
@@ -804,7 +808,9 @@ __global__ __launch_bounds__(BLOCK) void k_write_lines(KParams p_in, const uint6
                                                        const uint64_t* __restrict__ off,
                                                        const uint32_t* __restrict__ first,
                                                        const unsigned long long* ctr, char* __restrict__ out,
-                                                       uint64_t cap) {
+                                                       uint64_t cap, int slen_add) {
+    // slen[c] + slen_add = k-mers of contig c's first segment (the migrating walk's origin passes
+    // the bases it appended, slen_add = 1)
     const KParams p = specialize<KT>(p_in);
     const uint64_t lim = min((uint64_t)ctr[CT_OUT_BYTES], cap);
     const uint32_t lane = lane_id();
@@ -877,7 +883,7 @@ __global__ __launch_bounds__(BLOCK) void k_write_lines(KParams p_in, const uint6
             if (!live[u]) continue;
             uint32_t codes = hb[u] ? head_low(kc0[u], kc1[u], rc[u]) : 0u;
             if (hb[u] < nb[u]) {  // first-chunk bases j0 + b
-                const int64_t A = min<int64_t>((int64_t)sl[u] - 1, CHUNK_BASES), j0 = rc[u] - K;
+                const int64_t A = min<int64_t>((int64_t)sl[u] + slen_add - 1, CHUNK_BASES), j0 = rc[u] - K;
                 if (j0 + 16 > 0 && j0 < A) {
                     const uint32_t w = j0 > 0 ? (uint32_t)(j0 / 32) : 0u;
                     const uint32_t bw = bits32(d1[u], d0[u], (int)(2 * (j0 - 32 * (int64_t)w)));
@@ -1024,7 +1030,7 @@ hipError_t launch_write_heads(const KParams& p, const uint64_t* starts, uint64_t
 // out_bytes / LINE_BYTES + 2 entries); false: the heads writer instead.
 static bool launch_lines(const KParams& p, const WalkBuffers& wb, const uint32_t* clen, const uint64_t* offsets,
                          char* out, const unsigned long long* ctr, hipStream_t s, uint64_t cap, uint32_t* line_first,
-                         uint64_t out_bytes) {
+                         uint64_t out_bytes, int slen_add = 0) {
     const uint64_t nc = wb.n_starts;
     if (!line_first || p.K < (int)LINE_KMIN) return false;
     const unsigned gf = (unsigned)hmin((nc + BLOCK - 1) / BLOCK, 8192);
@@ -1034,14 +1040,22 @@ static bool launch_lines(const KParams& p, const WalkBuffers& wb, const uint32_t
     if (p.W == 1)
         with_kt<1>(p.K, [&](auto kt) {
             k_write_lines<1, decltype(kt)::value><<<gl, BLOCK, 0, s>>>(p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data,
-                                                                      wb.chunk_cap, offsets, line_first, ctr, out, cap);
+                                                                      wb.chunk_cap, offsets, line_first, ctr, out, cap,
+                                                                      slen_add);
         });
     else
         with_kt<2>(p.K, [&](auto kt) {
             k_write_lines<2, decltype(kt)::value><<<gl, BLOCK, 0, s>>>(p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data,
-                                                                      wb.chunk_cap, offsets, line_first, ctr, out, cap);
+                                                                      wb.chunk_cap, offsets, line_first, ctr, out, cap,
+                                                                      slen_add);
         });
     return true;
+}
+
+bool launch_text_lines(const KParams& p, const WalkBuffers& wb, const uint32_t* clen, int slen_add,
+                       const uint64_t* offsets, char* out, const unsigned long long* ctr, hipStream_t s, uint64_t cap,
+                       uint32_t* line_first, uint64_t out_bytes) {
+    return launch_lines(p, wb, clen, offsets, out, ctr, s, cap, line_first, out_bytes, slen_add);
 }
 
 hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t* offsets,
@@ -1133,7 +1147,12 @@ __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, SegBuffers s
             }
             s = (s + 1 == cap2) ? 0 : s + 1;
         }
-        if (nx == SEG_NONE) atomicAdd(&stats[ST_MISSING], 1ull);  // the splitter k-mer is absent
+        // not a collected splitter: a start k-mer that passes split_test (starts are not collected),
+        // reached by another contig's walk (overlapping walks, malformed input: the reference walks
+        // on through it, kmer_hash.cpp:44 tests only the forward extension), or a k-mer missing from
+        // the table. Both are counted as an overlap: kh_assemble redoes the walk unsegmented, whose
+        // walker steps through the start and reports a k-mer that is really missing.
+        if (nx == SEG_NONE) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
         wb.seg_next[g] = nx;
     }
 }

@@ -43,6 +43,7 @@ enum CtrIdx : int {
 
 // Chunk of appended bases: 8 words x 32 bases (2 bits each) = 256 bases.
 static constexpr int CHUNK_WORDS = 8;
+static constexpr uint32_t WMIN_ERR = 0xFFFFFFFFu;  // origin_lines (kh_capi.cpp): no memory
 static constexpr int CHUNK_BASES = 256;
 
 struct TableView {
@@ -143,6 +144,13 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
                               int phases = MAT_ALL, uint32_t* line_first = nullptr, uint64_t out_bytes = 0);
 // line_first: LINE_WORDS(out_bytes) uint32 entries for the line writer (K >= 16), or nullptr
 inline uint64_t line_first_words(uint64_t out_bytes) { return out_bytes / 1024 + 2; }
+// The line writer alone (K >= 16; false otherwise, nothing launched): heads, the first
+// CHUNK_BASES bases of each contig's first segment from wb.chunk_data (word-major chunk c =
+// contig c, chunk_cap = wb.chunk_cap), newlines; wb.contig_len[c] + slen_add = that segment's
+// k-mers. Bytes past the first chunk are left to a writer that runs after it.
+bool launch_text_lines(const KParams& p, const WalkBuffers& wb, const uint32_t* clen, int slen_add,
+                       const uint64_t* offsets, char* out, const unsigned long long* ctr, hipStream_t s, uint64_t cap,
+                       uint32_t* line_first, uint64_t out_bytes);
 
 // ---- migrating-walker rounds (kh_mwalk.hip) -------------------------------------------------
 // message: MSG_WORDS words [key.hi, key.lo, partial word, idx << 32 | bases appended,
@@ -155,7 +163,11 @@ struct MWalkRound {
     uint32_t P, rank;
     uint32_t split_bits = 0;  // > 0: walkers stop before splitter k-mers (kh_mseg.hip)
     uint64_t max_steps;
-    const uint64_t* in;   // n_in messages
+    const uint64_t* in;   // n_in messages; null in the first round: the walkers are the start
+                          // k-mers (starts[0, ns)) and then the splitters (splits), read directly
+    const uint64_t* starts = nullptr;
+    const uint64_t* splits = nullptr;
+    uint64_t ns = 0;
     uint64_t n_in;        // bound (grids, buffers)
     const unsigned long long* n_dev = nullptr;  // live inputs on the device (null: n_in)
     const unsigned long long* hot_on = nullptr;  // ctr[CT_HOT]: remapped regions exist (null: use p.hot)
@@ -166,9 +178,6 @@ struct MWalkRound {
     const uint64_t* headrec = nullptr;  // chain head records of this shard's build (hcap 0 = none)
     uint32_t hcap = 0;
 };
-// initial messages; hcap > 0: a walker whose own k-mer heads a chain record starts by reading it
-hipError_t launch_mw_init(const KParams& p, TableView t, uint32_t hcap, const uint64_t* starts, uint64_t n,
-                          uint32_t rank, uint64_t* msgs, hipStream_t s, uint64_t idx0 = 0);
 
 // ---- splitter segments of the migrating walk (kh_mseg.hip) ----------------------------------
 struct MSegState {       // per local segment: starts [0, ns), splitter segments [ns, ns + nsp)
@@ -185,8 +194,11 @@ hipError_t launch_split_collect(const KParams& p, const uint64_t* words, uint64_
 hipError_t launch_mseg_stab(const KParams& p, const uint64_t* splits, uint64_t nsp, uint64_t* stab, uint32_t* id,
                             uint64_t cap2, hipStream_t s);
 hipError_t launch_mseg_init(uint64_t ns, uint64_t nseg, uint32_t rank, const MSegState& st, hipStream_t s);
+// chunk_data (K >= 16, else null): start segments' first CHUNK_WORDS words into word-major first
+// chunks (chunk c = contig c < ns); *late counts their later words
 hipError_t launch_mseg_scan(const uint64_t* recs, uint64_t n, uint64_t nseg, const MSegState& st,
-                            unsigned long long* fin, hipStream_t s);
+                            unsigned long long* fin, hipStream_t s, uint64_t* chunk_data = nullptr, uint64_t ns = 0,
+                            unsigned long long* late = nullptr);
 hipError_t launch_mseg_link(const KParams& p, const MSegState& st, uint64_t ns, uint64_t nseg, uint32_t P, uint32_t rank,
                             uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out, uint64_t* counts,
                             hipStream_t s);
@@ -211,7 +223,8 @@ hipError_t launch_mseg_retag(const uint64_t* recs, uint64_t n, uint64_t ns, uint
 hipError_t launch_mseg_lens(const uint64_t* in3, uint64_t m, uint64_t ns, const MSegState& st, uint32_t* contig_len,
                             hipStream_t s);
 hipError_t launch_mseg_words(int K, const uint64_t* recs, uint64_t n, const uint64_t* in3, uint64_t m, uint64_t ns,
-                             const MSegState& st, const uint64_t* off, char* out, uint64_t cap, hipStream_t s);
+                             const MSegState& st, const uint64_t* off, char* out, uint64_t cap, hipStream_t s,
+                             uint32_t wmin, const unsigned long long* late = nullptr);
 hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
                          hipStream_t s);
 // ---- fixed-size exchange slots (no host read per round) ----------------------------------------
@@ -219,7 +232,7 @@ hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, un
 __host__ __device__ inline uint64_t slot_words(uint64_t cap) { return 2 + cap * MSG_WORDS; }
 // messages of P slots -> list (contiguous, n_max at most), *n = their number
 hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
-                              unsigned long long* n, uint64_t n_max, hipStream_t s);
+                              unsigned long long* n, uint64_t n_max, hipStream_t s, unsigned long long* stats);
 // this round's outgoing messages (walk outputs j < *n_dev with a destination, then the messages
 // held back last round) -> P slots of cap (overflow held back in carry_out / carry_dst_out,
 // *carry_n_out); live = [messages in flight, largest per-destination count].
@@ -260,10 +273,10 @@ hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, ui
 hipError_t launch_fin_check(const unsigned long long* fin, uint64_t want, const unsigned long long* want_dev,
                             uint64_t want_max, unsigned long long* stats, hipStream_t s);
 hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,
-                          unsigned long long* fin, hipStream_t s);
+                          unsigned long long* fin, hipStream_t s, uint64_t* chunk_data = nullptr);
 // cap: bytes of `out` (words past it are skipped: a bad length fails at kh_sync, never overruns)
 hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
-                           const uint64_t* off, char* out, uint64_t cap, hipStream_t s);
+                           const uint64_t* off, char* out, uint64_t cap, hipStream_t s, uint32_t wmin);
 
 // read_kmers.hpp:62-76 on the device: n fixed-width "KMER BF\n" lines (K+4 bytes) -> kmer_pair
 // records; lines with a non-ACGT k-mer character count in stats[ST_BAD_BASE].

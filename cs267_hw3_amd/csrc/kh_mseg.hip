@@ -128,17 +128,31 @@ hipError_t launch_mseg_stab(const KParams& p, const uint64_t* splits, uint64_t n
 }
 
 // ---- segment records (this rank's text records after they came home) ---------------------------
-// finish records: word_no field = 0 length (bases appended), 1 / 2 = link key hi / lo
+// finish records: word_no field = 0 length (bases appended), 1 / 2 = link key hi / lo. With
+// chunk_data (the origin's line writer, K >= 16) the same pass scatters the first CHUNK_WORDS words
+// of every start segment into the word-major first chunks (chunk c = contig c < ns) and counts the
+// start segments' later words into *late (their character writer runs only when there are any).
 __global__ __launch_bounds__(BLOCK) void k_mseg_scan(const uint64_t* recs, uint64_t n, uint64_t nseg, MSegState st,
-                                                     unsigned long long* fin) {
-    uint64_t f = 0;
+                                                     unsigned long long* fin, uint64_t* chunk_data, uint64_t ns,
+                                                     unsigned long long* late) {
+    uint64_t f = 0, lw = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t t = recs[2 * i];
-        if (!((t >> 55) & 1)) continue;
+        const ulonglong2 r = reinterpret_cast<const ulonglong2*>(recs)[i];
+        const uint64_t t = r.x;
+        if (!((t >> 55) & 1)) {
+            const uint64_t c = t & 0x7FFFFFFFull, wn = (t >> 31) & 0xFFFFFFull;
+            if (chunk_data && c < ns) {
+                if (wn < CHUNK_WORDS)
+                    chunk_data[wn * ns + c] = r.y;
+                else
+                    ++lw;
+            }
+            continue;
+        }
         const uint64_t c = t & 0x7FFFFFFFull;
         if (c >= nseg) continue;
         const uint32_t sub = (uint32_t)((t >> 31) & 0xFFFFFFull);
-        const uint64_t v = recs[2 * i + 1];
+        const uint64_t v = r.y;
         if (sub == 0) {
             st.len[c] = (uint32_t)v;
             ++f;
@@ -152,6 +166,10 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_scan(const uint64_t* recs, uint6
     uint64_t tot;
     block_excl_scan(f, tot);
     if (threadIdx.x == 0 && tot) atomicAdd(fin, (unsigned long long)tot);
+    if (late) {
+        block_excl_scan(lw, tot);
+        if (threadIdx.x == 0 && tot) atomicAdd(late, (unsigned long long)tot);
+    }
 }
 
 // link message: [key.hi, key.lo, predecessor gid, predecessor length]
@@ -255,7 +273,11 @@ __global__ __launch_bounds__(BLOCK) void k_res_init(const uint64_t* all, uint64_
 }
 
 // pass k: in -> out; pend[k] = entries still pending after it (pass k returns at once when pass
-// k - 1 left none: the last written buffer is final)
+// k - 1 left none: the last written buffer is final). An entry follows up to RES_HOPS pointers of
+// the previous pass (read-only here, so no races): a pointer spanning S segments becomes one
+// spanning (RES_HOPS + 1) S, so log_{RES_HOPS+1} N passes rank any chain instead of log_2 N (each
+// launch costs ~4.6 us even when it returns at once: 22 of them at C3's 780K splitter segments).
+static constexpr uint32_t RES_HOPS = 7;
 __global__ __launch_bounds__(BLOCK) void k_res_pass(uint32_t k, ResBuf in, ResBuf out, uint64_t N, uint64_t stride,
                                                     unsigned long long* pend) {
     if (k > 0 && pend[k - 1] == 0) return;
@@ -264,14 +286,16 @@ __global__ __launch_bounds__(BLOCK) void k_res_pass(uint32_t k, ResBuf in, ResBu
         uint64_t j = in.J[g], a = in.A[g];
         uint8_t d = in.D[g];
         if (!d && j != GID_NONE) {
-            const uint64_t t = (uint64_t)gid_rank(j) * stride + (gid_idx(j) & ~GID_SPLIT);
-            if (t < N) {
-                const uint64_t jt = in.J[t];
-                a += in.A[t];
-                d = in.D[t];
-                j = jt;  // a broken predecessor (GID_NONE, not done) breaks this chain too
-            } else {
-                j = GID_NONE;
+            for (uint32_t h = 0; h < RES_HOPS && !d && j != GID_NONE; ++h) {
+                const uint64_t t = (uint64_t)gid_rank(j) * stride + (gid_idx(j) & ~GID_SPLIT);
+                if (t < N) {
+                    const uint64_t jt = in.J[t];
+                    a += in.A[t];
+                    d = in.D[t];
+                    j = jt;  // a broken predecessor (GID_NONE, not done) breaks this chain too
+                } else {
+                    j = GID_NONE;
+                }
             }
             left += (!d && j != GID_NONE) ? 1 : 0;
         }
@@ -390,16 +414,20 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_lens_remote(const uint64_t* in3,
     }
 }
 
-// start segments' own words (bounded by the start segment's length, not the contig's)
+// start segments' own words numbered >= wmin (bounded by the start segment's length, not the
+// contig's); the line writer covers the first CHUNK_WORDS when it runs (wmin = CHUNK_WORDS)
 __global__ __launch_bounds__(BLOCK) void k_mseg_words_local(int K, const uint64_t* recs, uint64_t n, uint64_t ns,
                                                             MSegState st, const uint64_t* off, char* out,
-                                                            uint64_t cap) {
+                                                            uint64_t cap, uint32_t wmin,
+                                                            const unsigned long long* late) {
+    if (late && *late == 0) return;  // no start segment has words past the line writer's
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t t = recs[2 * i];
         if ((t >> 55) & 1) continue;
         const uint64_t c = t & 0x7FFFFFFFull;
         if (c >= ns) continue;
         const uint64_t wn = (t >> 31) & 0xFFFFFFull;
+        if (wn < wmin) continue;
         const uint64_t app = st.len[c], j0 = wn * 32;
         if (j0 >= app) continue;
         const uint32_t cnt = (uint32_t)(app - j0 < 32 ? app - j0 : 32);
@@ -433,9 +461,10 @@ static unsigned grid_n(uint64_t n, uint64_t cap) {
 }
 
 hipError_t launch_mseg_scan(const uint64_t* recs, uint64_t n, uint64_t nseg, const MSegState& st,
-                            unsigned long long* fin, hipStream_t s) {
+                            unsigned long long* fin, hipStream_t s, uint64_t* chunk_data, uint64_t ns,
+                            unsigned long long* late) {
     if (n == 0) return hipSuccess;
-    k_mseg_scan<<<grid_n(n, 2048), BLOCK, 0, s>>>(recs, n, nseg, st, fin);
+    k_mseg_scan<<<grid_n(n, 2048), BLOCK, 0, s>>>(recs, n, nseg, st, fin, chunk_data, ns, late);
     return hipGetLastError();
 }
 
@@ -459,10 +488,14 @@ hipError_t launch_mseg_preds_out(const MSegState& st, uint64_t ns, const unsigne
     return hipGetLastError();
 }
 
-// passes for any chain of <= N segments: pointer jumping halves the distance to the head each pass
+// passes for any chain of <= N segments: each pass multiplies a pointer's span by RES_HOPS + 1
 uint32_t mseg_resolve_passes(uint64_t N) {
     uint32_t k = 1;
-    while (k < 62 && (1ull << (k - 1)) < N + 1) ++k;
+    unsigned __int128 span = 1;
+    while (k < 62 && span < (unsigned __int128)N + 1) {
+        span *= RES_HOPS + 1;
+        ++k;
+    }
     return k + 1;
 }
 
@@ -491,8 +524,9 @@ hipError_t launch_mseg_lens(const uint64_t* in3, uint64_t m, uint64_t ns, const 
 }
 
 hipError_t launch_mseg_words(int K, const uint64_t* recs, uint64_t n, const uint64_t* in3, uint64_t m, uint64_t ns,
-                             const MSegState& st, const uint64_t* off, char* out, uint64_t cap, hipStream_t s) {
-    if (n) k_mseg_words_local<<<grid_n(n, 8192), BLOCK, 0, s>>>(K, recs, n, ns, st, off, out, cap);
+                             const MSegState& st, const uint64_t* off, char* out, uint64_t cap, hipStream_t s,
+                             uint32_t wmin, const unsigned long long* late) {
+    if (n) k_mseg_words_local<<<grid_n(n, 8192), BLOCK, 0, s>>>(K, recs, n, ns, st, off, out, cap, wmin, late);
     if (m) k_mseg_words_remote<<<grid_n(m, 8192), BLOCK, 0, s>>>(K, in3, m, ns, off, out, cap);
     return hipGetLastError();
 }

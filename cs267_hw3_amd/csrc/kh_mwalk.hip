@@ -19,6 +19,9 @@ namespace kh {
 static constexpr uint32_t MW_LOOKUP = 0xFF;   // message state: key must be looked up by its owner
 static constexpr uint32_t MW_READREC = 0xFE;  // message state: read head record (m[4] >> 32) - 1 of this
                                               // rank (its run starts at the key; only sent to self)
+static constexpr uint32_t MW_ENTRY = 0xFD;    // a new walker (first round): look up its own start k-mer
+                                              // for the record covering its run; its forward
+                                              // extension is the start record's own
 static constexpr uint8_t MW_NONE = 0xFF;      // destination: walker finished this round
 
 __device__ __forceinline__ uint64_t rec_tag(uint32_t origin, bool fin, uint64_t word_no, uint32_t idx) {
@@ -58,10 +61,11 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
     };
     const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
     uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    bool active = false, probing = false;
+    bool active = false, probing = false, entry = false;
     Key k{0, 0};
-    uint64_t s = 0, buf = 0;
-    uint32_t steps = 0, idx = 0, origin = 0, st = 0, nrec = 0, nwords = 0;
+    uint64_t s = 0, buf = 0, pb = 0;          // pb: 4-slot blocks probed for the current k-mer
+    const uint64_t pb_max = (cap >> 2) + 1;   // every block once: the k-mer is absent (a full table)
+    uint32_t steps = 0, idx = 0, origin = 0, st = 0, nrec = 0, nwords = 0, efwd = 0;
     uint32_t nsucc = 0;  // the last record's successor run (head-record index + 1 in its region)
     uint64_t* rec = nullptr;
     auto finish = [&](uint64_t jj) {
@@ -80,13 +84,29 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
         // walker's next k-mer (owner + region): lanes on either path share one scan, not one each
         bool scan = false, fresh = false;
         if (!active && j < n_live) {
-            const uint64_t* m = mw.in + j * MSG_WORDS;
-            k.hi = m[0];
-            k.lo = m[1];
-            buf = m[2];
-            steps = (uint32_t)m[3];
-            idx = (uint32_t)(m[3] >> 32);
-            const uint64_t m4 = m[4];
+            uint64_t m4;
+            if (mw.in) {
+                const uint64_t* m = mw.in + j * MSG_WORDS;
+                k.hi = m[0];
+                k.lo = m[1];
+                buf = m[2];
+                steps = (uint32_t)m[3];
+                idx = (uint32_t)(m[3] >> 32);
+                m4 = m[4];
+            } else {
+                // first round: walker j is start k-mer j, then splitter j - ns (segment ids in that
+                // order, kh_mseg.hip); with chains it looks up its own k-mer first (MW_ENTRY), as the
+                // single-GPU walker does, else it steps from its own extension
+                const uint64_t* x = j < mw.ns ? mw.starts + j * W : mw.splits + (j - mw.ns) * W;
+                const uint64_t x0 = x[0], x1 = (W == 2) ? x[1] : 0;
+                k = slot_key(x0, x1, p);
+                const uint32_t f = ext_fwd(slot_ext(x0));
+                efwd = f > 4 ? EXT_BAD : f;
+                buf = 0;
+                steps = 0;
+                idx = (uint32_t)j;
+                m4 = mw.rank | ((uint64_t)(chains && efwd <= 3u ? MW_ENTRY : efwd) << 8);
+            }
             origin = (uint32_t)m4 & 0xFFu;
             st = (uint32_t)(m4 >> 8) & 0xFFu;
             rec = mw.stage + j * (MW_REC_SLOTS * 2);
@@ -94,7 +114,8 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             nwords = 0;
             nsucc = 0;
             active = true;
-            probing = st == MW_LOOKUP || st == MW_READREC;
+            entry = st == MW_ENTRY;
+            probing = st == MW_LOOKUP || st == MW_READREC || entry;
             if (st == MW_READREC) {
                 s = WQ_REC | ((m4 >> 32) - 1);
             } else if (probing) {
@@ -138,6 +159,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
         if (fresh) {
             reg = pl.r;
             s = home_of(pl, cap, p);
+            pb = 0;
         }
         if (stepped) {
             if (scan) {
@@ -163,6 +185,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                     // the record names the run that starts at k (k_rec_succ): read it, no probe
                     s = (nsucc && nwords + 3 <= MW_RUN_WORDS) ? WQ_REC | ((uint64_t)reg * mw.hcap + nsucc - 1)
                                                               : home_of(pl, cap, p);
+                    pb = 0;
                 }
             }
             nsucc = 0;
@@ -250,65 +273,33 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
                 }
                 probing = false;
             } else if (myfh < myfe) {
-                const uint32_t hidx = myext >> 7;
-                if (hidx && nwords + 3 <= MW_RUN_WORDS) {  // the run's <= 2 words fit this round
+                const uint32_t hidx = myext >> 7, tf = ext_fwd(myext & 63u);
+                // a start walks from its own record (kmer_hash.cpp:42-44): a record whose run
+                // begins with another extension (a duplicate key) is not used for it
+                if (hidx && !(entry && tf != efwd) && nwords + 3 <= MW_RUN_WORDS) {  // the run's <= 2 words fit
                     s = WQ_REC | ((uint64_t)reg * mw.hcap + hidx - 1);
                 } else {
-                    st = ext_fwd(myext & 63u);
+                    st = entry ? efwd : tf;
                     probing = false;
                 }
-            } else if (myfe < 4u) {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
-                atomicAdd(&stats[ST_MISSING], 1ull);
-                finish(j);
-                mw.nrec[j] = (uint8_t)nrec;
-                active = false;
-                j += stride;
+                entry = false;
+            } else if (myfe < 4u || ++pb > pb_max) {
+                if (entry) {  // a start k-mer need not be in this shard (kh_set_starts): step from its own
+                    st = efwd;
+                    probing = false;
+                    entry = false;
+                } else {  // find() miss: kmer_hash.cpp:47-49 throws; finish the contig here
+                    atomicAdd(&stats[ST_MISSING], 1ull);
+                    finish(j);
+                    mw.nrec[j] = (uint8_t)nrec;
+                    active = false;
+                    j += stride;
+                }
             } else {
                 const uint64_t nx = (s & ~3ull) + 4;
                 s = nx >= cap ? 0 : nx;
             }
         }
-    }
-}
-
-// Initial messages: one per start (or splitter) k-mer, state = its forward extension; with chains,
-// a walker whose k-mer's slot carries a head record whose run begins with the walker's own
-// extension (the walker's rule for a start, kmer_hash.cpp:42-44; as k_start_rec) starts by reading
-// that record instead (state MW_READREC).
-template <int W, int KT>
-__global__ __launch_bounds__(BLOCK) void k_mw_init(KParams p_in, const uint64_t* __restrict__ slots, uint64_t cap,
-                                                   uint32_t hcap, const uint64_t* starts, uint64_t n, uint32_t rank,
-                                                   uint64_t* msgs, uint64_t idx0) {
-    const KParams p = specialize<KT>(p_in);
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t x0 = starts[i * W];
-        const uint64_t x1 = (W == 2) ? starts[i * W + 1] : 0;
-        const Key k = slot_key(x0, x1, p);
-        const uint32_t f = ext_fwd(slot_ext(x0));
-        uint64_t rix = 0;
-        if (hcap && f <= 3u) {
-            const Place pl = place(k, p);
-            uint64_t sl = home_of(pl, cap, p);
-            const uint64_t want0 = (W == 1) ? k.lo : k.hi;
-            for (uint64_t probes = 0; probes < cap; ++probes) {
-                uint64_t w0, w1;
-                load_slot<W>(slots, sl, w0, w1);
-                if (w0 == EMPTY) break;
-                if (slot_keybits(w0, p) == want0 && (W == 1 || w1 == k.lo)) {
-                    const uint32_t hidx = slot_hidx(w0, p);
-                    if (hidx && ext_fwd(slot_ext(w0)) == f) rix = (uint64_t)pl.r * hcap + hidx;
-                    break;
-                }
-                sl = (sl + 1 == cap) ? 0 : sl + 1;
-            }
-        }
-        uint64_t* m = msgs + i * MSG_WORDS;
-        m[0] = k.hi;
-        m[1] = k.lo;
-        m[2] = 0;
-        m[3] = (idx0 + i) << 32;
-        m[4] = rix ? rank | ((uint64_t)MW_READREC << 8) | (rix << 32)
-                   : rank | ((uint64_t)(f > 4 ? EXT_BAD : f) << 8);
     }
 }
 
@@ -318,20 +309,47 @@ struct NrecF {
     __device__ uint64_t operator()(uint64_t i) const { return (!n_dev || i < *n_dev) ? n[i] : 0u; }
 };
 
+// The records of a wave's 64 inputs are contiguous in the store (off is their exclusive scan), so
+// the wave copies them as one run: lane t takes record t of the run (its input by a binary search
+// over the 64 offsets), one coalesced 16-B store per lane (a lane copying its own input's records
+// stored 64 inputs' records 192 B apart per instruction: 0.25 ms at C3).
 __global__ __launch_bounds__(BLOCK) void k_mw_compact(const uint64_t* stage, const uint8_t* nrec,
                                                       const uint64_t* off, uint64_t nb, uint64_t* store,
                                                       const unsigned long long* n_dev, uint64_t store_cap,
                                                       unsigned long long* stats) {
     const uint64_t n = n_dev ? min((uint64_t)*n_dev, nb) : nb;
-    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
-        const uint32_t c = nrec[j];
-        if (off[j] + c > store_cap) {  // the store's bound was wrong (a cycle?): fail, never overrun
-            atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+    const uint32_t lane = lane_id();
+    const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
+    for (uint64_t j0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / 64 * 64; j0 < n; j0 += waves * 64) {
+        const uint64_t j = j0 + lane;
+        const uint32_t c = j < n ? nrec[j] : 0u;
+        const uint64_t o = j < n ? off[j] : 0;
+        const uint64_t base = __shfl(o, 0, 64);
+        const uint32_t rel = (uint32_t)(o - base);  // < 64 * MW_REC_SLOTS
+        // inclusive end of each lane's records; the run's total from the last lane
+        const uint32_t last = (uint32_t)min<uint64_t>(n - j0, 64) - 1;
+        const uint32_t tot = __shfl(rel + c, (int)last, 64);
+        if (base + tot > store_cap) {  // the store's bound was wrong (a cycle?): fail, never overrun
+            if (lane == 0) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
             continue;
         }
-        const ulonglong2* src = reinterpret_cast<const ulonglong2*>(stage + j * (MW_REC_SLOTS * 2));
-        ulonglong2* dst = reinterpret_cast<ulonglong2*>(store + off[j] * 2);
-        for (uint32_t r = 0; r < c; ++r) dst[r] = src[r];
+        for (uint32_t t0 = 0; t0 < tot; t0 += 64) {
+            const uint32_t t = t0 + lane;
+            // the input holding record t: the last lane whose run starts at or before t (lanes
+            // with no records share their start with the next one: take the last such lane)
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t st = 32; st > 0; st >>= 1) {
+                const uint32_t v = __shfl(rel, (int)(lo + st), 64);
+                if (lo + st <= last && v <= t) lo += st;
+            }
+            const uint32_t r0 = __shfl(rel, (int)lo, 64);
+            if (t < tot) {
+                const ulonglong2* src =
+                    reinterpret_cast<const ulonglong2*>(stage + (j0 + lo) * (MW_REC_SLOTS * 2)) + (t - r0);
+                reinterpret_cast<ulonglong2*>(store)[base + t] = *src;
+            }
+        }
     }
 }
 
@@ -361,16 +379,23 @@ struct RecOp {
 };
 
 // Origin side: finish records -> contig lengths (k-mers = bases appended + 1); *fin counts them
-// (one atomic per block) so the host can check that every walker came home.
+// (one atomic per block) so the host can check that every walker came home. With chunk_data (the
+// line writer, K >= 16) the first CHUNK_WORDS words of each contig go into its word-major first
+// chunk (chunk c = contig c) in the same pass.
 __global__ __launch_bounds__(BLOCK) void k_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,
-                                                   unsigned long long* fin) {
+                                                   unsigned long long* fin, uint64_t* chunk_data) {
     uint64_t f = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t t = recs[2 * i];
-        if (!((t >> 55) & 1)) continue;
-        const uint32_t c = (uint32_t)(t & 0x7FFFFFFFull);
+        const ulonglong2 r = reinterpret_cast<const ulonglong2*>(recs)[i];
+        const uint64_t t = r.x;
+        const uint64_t c = t & 0x7FFFFFFFull;
+        if (!((t >> 55) & 1)) {
+            const uint64_t wn = (t >> 31) & 0xFFFFFFull;
+            if (chunk_data && c < nc && wn < CHUNK_WORDS) chunk_data[wn * nc + c] = r.y;
+            continue;
+        }
         if (c < nc) {
-            len[c] = (uint32_t)recs[2 * i + 1] + 1;
+            len[c] = (uint32_t)r.y + 1;
             ++f;
         }
     }
@@ -379,16 +404,17 @@ __global__ __launch_bounds__(BLOCK) void k_mw_lens(const uint64_t* recs, uint64_
     if (threadIdx.x == 0 && tot) atomicAdd(fin, (unsigned long long)tot);
 }
 
-// Origin side: word records -> characters.
+// Origin side: word records (number >= wmin) -> characters.
 __global__ __launch_bounds__(BLOCK) void k_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc,
                                                     const uint32_t* len, const uint64_t* off, char* out,
-                                                    uint64_t cap) {
+                                                    uint64_t cap, uint32_t wmin) {
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t t = recs[2 * i];
         if ((t >> 55) & 1) continue;
         const uint32_t c = (uint32_t)(t & 0x7FFFFFFFull);
         if (c >= nc) continue;
         const uint64_t wn = (t >> 31) & 0xFFFFFFull;
+        if (wn < wmin) continue;
         const uint64_t app = (uint64_t)len[c] - 1;
         const uint64_t j0 = wn * 32;
         if (j0 >= app) continue;
@@ -403,22 +429,6 @@ __global__ __launch_bounds__(BLOCK) void k_mw_words(int K, const uint64_t* recs,
 static unsigned grid_for(uint64_t n, uint64_t cap_blocks) {
     const uint64_t g = (n + BLOCK - 1) / BLOCK;
     return (unsigned)(g == 0 ? 1 : (g < cap_blocks ? g : cap_blocks));
-}
-
-hipError_t launch_mw_init(const KParams& p, TableView t, uint32_t hcap, const uint64_t* starts, uint64_t n,
-                          uint32_t rank, uint64_t* msgs, hipStream_t s, uint64_t idx0) {
-    if (n == 0) return hipSuccess;
-    if (!p.chain) hcap = 0;
-    const unsigned g = grid_for(n, 8192);
-    if (p.W == 1)
-        with_kt<1>(p.K, [&](auto kt) {
-            k_mw_init<1, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, hcap, starts, n, rank, msgs, idx0);
-        });
-    else
-        with_kt<2>(p.K, [&](auto kt) {
-            k_mw_init<2, decltype(kt)::value><<<g, BLOCK, 0, s>>>(p, t.slots, t.cap, hcap, starts, n, rank, msgs, idx0);
-        });
-    return hipGetLastError();
 }
 
 hipError_t launch_mw_run(const KParams& p, TableView t, const MWalkRound& mw, unsigned long long* stats,
@@ -444,7 +454,7 @@ hipError_t launch_mw_text_offsets(const MWalkRound& mw, uint64_t* off, uint64_t*
 hipError_t launch_mw_compact(const MWalkRound& mw, const uint64_t* off, uint64_t* store, uint64_t store_cap,
                              unsigned long long* stats, hipStream_t s) {
     if (mw.n_in == 0) return hipSuccess;
-    k_mw_compact<<<grid_for(mw.n_in, 8192), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store, mw.n_dev, store_cap,
+    k_mw_compact<<<grid_for(mw.n_in, 4096), BLOCK, 0, s>>>(mw.stage, mw.nrec, off, mw.n_in, store, mw.n_dev, store_cap,
                                                            stats);
     return hipGetLastError();
 }
@@ -455,9 +465,23 @@ hipError_t launch_mw_group(const MWalkRound& mw, uint64_t* hist, uint64_t* off, 
     return group_by_owner(MsgOp{mw.dst, mw.tmp, out}, mw.n_in, mw.P, hist, off, scratch + 1, counts, total, s);
 }
 
+// one rank: every record's origin is this rank, so grouping is a copy of the n_dev records
+__global__ __launch_bounds__(BLOCK) void k_mw_text_copy(const uint64_t* recs, uint64_t n_max,
+                                                        const unsigned long long* n_dev, uint64_t* out,
+                                                        uint64_t* counts) {
+    const uint64_t n = min((uint64_t)*n_dev, n_max);
+    if (blockIdx.x == 0 && threadIdx.x < 2) counts[threadIdx.x] = n;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK)
+        reinterpret_cast<ulonglong2*>(out)[i] = reinterpret_cast<const ulonglong2*>(recs)[i];
+}
+
 hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, uint64_t* hist, uint64_t* off,
                                 uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s,
                                 const unsigned long long* n_dev) {
+    if (P == 1 && n_dev) {  // (the histogram + scan + scatter: 0.15 ms at C3; the copy ~0.05)
+        k_mw_text_copy<<<grid_for(n, 4096), BLOCK, 0, s>>>(recs, n, n_dev, out, counts);
+        return hipGetLastError();
+    }
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
     return group_by_owner(RecOp{recs, out, n_dev}, n, P, hist, off, scratch + 1, counts, total, s);
 }
@@ -481,11 +505,16 @@ __device__ __forceinline__ uint64_t slot_prefix(const uint64_t* slots, uint32_t 
 }
 
 __global__ __launch_bounds__(BLOCK) void k_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
-                                                       unsigned long long* n, uint64_t n_max) {
+                                                       unsigned long long* n, uint64_t n_max,
+                                                       unsigned long long* stats) {
     __shared__ uint64_t pre[MAX_RANKS + 1];
-    // the list holds n_max messages (walkers never multiply; more would be a sender's bug)
-    const uint64_t tot = min(slot_prefix(slots, P, cap, pre), n_max);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *n = tot;
+    // the list holds n_max messages (walkers never multiply; more is a sender's bug: reported at
+    // kh_sync as an overflow in the round it happens, the messages past n_max are not walked)
+    const uint64_t all = slot_prefix(slots, P, cap, pre), tot = min(all, n_max);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *n = tot;
+        if (all > n_max) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+    }
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * BLOCK) {
         uint32_t q = 0;
         while (q + 1 < P && pre[q + 1] <= i) ++q;
@@ -497,8 +526,8 @@ __global__ __launch_bounds__(BLOCK) void k_slot_gather(const uint64_t* slots, ui
 }
 
 hipError_t launch_slot_gather(const uint64_t* slots, uint32_t P, uint64_t cap, uint64_t* list,
-                              unsigned long long* n, uint64_t n_max, hipStream_t s) {
-    k_slot_gather<<<grid_for((uint64_t)P * cap, 4096), BLOCK, 0, s>>>(slots, P, cap, list, n, n_max);
+                              unsigned long long* n, uint64_t n_max, hipStream_t s, unsigned long long* stats) {
+    k_slot_gather<<<grid_for((uint64_t)P * cap, 4096), BLOCK, 0, s>>>(slots, P, cap, list, n, n_max, stats);
     return hipGetLastError();
 }
 
@@ -599,17 +628,18 @@ hipError_t launch_fin_check(const unsigned long long* fin, uint64_t want, const 
 }
 
 hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len, unsigned long long* fin,
-                          hipStream_t s) {
+                          hipStream_t s, uint64_t* chunk_data) {
     if (n == 0) return hipSuccess;
-    k_mw_lens<<<grid_for(n, 1024), BLOCK, 0, s>>>(recs, n, nc, len, fin);
+    k_mw_lens<<<grid_for(n, 2048), BLOCK, 0, s>>>(recs, n, nc, len, fin, chunk_data);
     return hipGetLastError();
 }
 
 hipError_t launch_mw_words(int K, const uint64_t* recs, uint64_t n, uint64_t nc, const uint32_t* len,
-                           const uint64_t* off, char* out, uint64_t cap, hipStream_t s) {
+                           const uint64_t* off, char* out, uint64_t cap, hipStream_t s, uint32_t wmin) {
     if (n == 0) return hipSuccess;
-    k_mw_words<<<grid_for(n, 8192), BLOCK, 0, s>>>(K, recs, n, nc, len, off, out, cap);
+    k_mw_words<<<grid_for(n, 8192), BLOCK, 0, s>>>(K, recs, n, nc, len, off, out, cap, wmin);
     return hipGetLastError();
 }
+
 
 }  // namespace kh

@@ -391,6 +391,13 @@ class GpuShard:
         check(self.L.kh_counters_dev(self.h, self._p(out)))
         return out
 
+    def counters_host(self):
+        """[start k-mers, splitter k-mers] on the host (blocking; after insert_records it waits for
+        the copy made beside the build, not for the build)."""
+        v = (ctypes.c_uint64 * 2)()
+        check(self.L.kh_counters(self.h, v))
+        return [int(v[0]), int(v[1])]
+
     def route_splitters(self, nranks):
         """Splitter k-mers this rank's routes sent to each owner (device int64[P], async)."""
         out = self.zeros(nranks, torch.int64)
@@ -673,7 +680,10 @@ class DistributedKmerHashMap:
             sh.reserve(n)
             sh.insert_records(recs)
             self._begin("counts")
-            c = self._host(sh.counters())      # the walk's start / splitter counts
+            if hasattr(sh, "counters_host") and hasattr(sh.L, "kh_counters"):  # start / splitter counts
+                c = sh.counters_host()         # (the library counts this read: kh_host_syncs)
+            else:
+                c = self._host(sh.counters())
             self._ns, self._nsp = int(c[0]), int(c[1])
             self._walkers, self._splitters = self._ns + self._nsp, self._nsp
             return n
@@ -822,7 +832,7 @@ class DistributedKmerHashMap:
         limit = self.MAX_ROUNDS if self._splitters else max(self.MAX_ROUNDS, total_kmers + self.MAX_ROUNDS)
         # [in flight, largest per-destination count] of the rounds since the last check
         live = self._grow("_mw_live", 2 * max(check_at, self.CHECK_EVERY) + 2, torch.int64, dev, slack=1.0)
-        maxes, used, base = [], [], 0
+        maxes, flights, used, base = [], [], [], 0
         while True:
             cap = self._cap(self.rounds)
             used.append(cap)
@@ -861,6 +871,7 @@ class DistributedKmerHashMap:
                         raise self._err
                     raise _lib.KmerHashError(_lib.KH_ERR_FULL, "another rank failed to size its shard")
                 maxes.extend(int(x) for x in h[1:nw:2])
+                flights.extend(int(x) for x in h[0:nw:2])
                 if int(h[nw - 2]) == 0:
                     break
                 # a round whose demand passed its slots held messages back: later rounds get slots
@@ -872,9 +883,10 @@ class DistributedKmerHashMap:
                     raise _lib.KmerHashError(_lib.KH_ERR_CYCLE, f"migrating walk did not end in {limit} rounds")
                 base = self.rounds
                 check_at = self.rounds + self.CHECK_EVERY
-        # the next assemble: slots sized by what each round carried, and its first check here
+        # the next assemble: slots sized by what each round carried, and its first check at the
+        # round after which nothing was in flight (rounds past it are empty: ~60 us each)
         self._caps = [max(256, int(x) * 5 // 4 + 256) for x in maxes]
-        self._rounds_hint = self.rounds
+        self._rounds_hint = next((i + 1 for i, x in enumerate(flights) if x == 0), self.rounds)
         self._caps_walkers = self._walkers
         self._begin("text_group")
         tb = sh.mw_text_bound()

@@ -203,10 +203,9 @@ public:
             abi_check(kh_insert_dev(t_, dev_recs, n));
             inserted_ += n;
             err_.clear();
-            int64_t* c2 = pack_.words(2);
-            abi_check(kh_counters_dev(t_, c2));
             uint64_t hv[2];
-            read_host(hv, c2, 2);  // the walk's start / splitter counts
+            abi_check(kh_counters(t_, hv));  // the walk's start / splitter counts (waits for the copy
+                                             // made beside the build, not for the build)
             ns_ = hv[0];
             nsp_ = splitters_ = hv[1];
             walkers_ = ns_ + nsp_;
@@ -353,7 +352,7 @@ public:
         const uint64_t limit = splitters_ ? (uint64_t)kMaxRounds : std::max<uint64_t>(kMaxRounds, total_kmers + kMaxRounds);
         // [in flight, largest per-destination count] of the rounds since the last check
         int64_t* live = live_.words(2 * (uint64_t)std::max(check_at, kCheckEvery) + 2);
-        std::vector<uint64_t> maxes, used;
+        std::vector<uint64_t> maxes, flights, used;
         int base = 0;
         for (;;) {
             const uint64_t cap = slot_cap(rounds_), sw = KH_SLOT_WORDS(cap);
@@ -392,6 +391,7 @@ public:
                     for (uint64_t i = 0; i < w; ++i) mx[i] = std::max(mx[i], h[q * w + i]);
                 if (mx[w - 1]) throw std::runtime_error(failed ? err_ : "another rank failed to size its shard");
                 for (uint64_t i = 1; i < nw; i += 2) maxes.push_back(mx[i]);
+                for (uint64_t i = 0; i < nw; i += 2) flights.push_back(mx[i]);
                 if (mx[nw - 2] == 0) break;
                 // a round whose demand passed its slots held messages back: later rounds get
                 // slots for that demand, so the surplus drains in a few rounds, not thousands
@@ -402,10 +402,16 @@ public:
                 check_at = rounds_ + kCheckEvery;
             }
         }
-        // the next assemble: slots sized by what each round carried, and its first check here
+        // the next assemble: slots sized by what each round carried, and its first check at the
+        // round after which nothing was in flight (rounds past it are empty)
         caps_.assign(maxes.size(), 0);
         for (size_t r = 0; r < maxes.size(); ++r) caps_[r] = std::max<uint64_t>(256, maxes[r] * 5 / 4 + 256);
         rounds_hint_ = rounds_;
+        for (size_t r = 0; r < flights.size(); ++r)
+            if (flights[r] == 0) {
+                rounds_hint_ = (int)r + 1;
+                break;
+            }
         caps_walkers_ = walkers_;
         uint64_t tb = 0;
         abi_check(kh_mwalk_text_bound(t_, &tb));

@@ -166,6 +166,10 @@ int kh_route_splitters_dev(kh_table* t, void* dev_out, int nranks);
 /* Async copy of {start k-mers collected, splitter k-mers collected} (2 uint64) into device memory,
  * for hosts that read them together with their own counts (one host round trip). */
 int kh_counters_dev(kh_table* t, void* dev_out);
+/* The same two counts read on the host (blocking). After kh_insert_dev they come from the copy
+ * made beside the region build, so the read waits for the start / splitter compaction, not for the
+ * build (the one-rank sharded step reads them without idling the device). */
+int kh_counters(kh_table* t, uint64_t* out2);
 /* Migrating-walker rounds. The table is sharded by a hash of each k-mer's minimizer, so
  * consecutive k-mers of a contig mostly share an owner; a walker walks the local shard until its
  * next k-mer is owned elsewhere and is then sent there. Nothing below reads the device on the host:

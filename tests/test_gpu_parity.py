@@ -119,6 +119,44 @@ def test_overlapping_walks_redo(k, L, every):
     assert got_nc == nc and got == want
 
 
+def _split_hash(kmer):
+    """kh_codec.hpp split_hash of a k-mer string (V = 2-bit bases, first base most significant)."""
+    v = 0
+    for ch in kmer:
+        v = (v << 2) | "ACGT".index(ch)
+    lo = v & ((1 << 62) - 1)
+    return (((lo & 0xFFFFFFFF) ^ (lo >> 32)) * 0x9E3779B1) & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("k", [19, 51])
+def test_walk_into_start_that_passes_split_test(monkeypatch, k):
+    """Malformed input: a chain k-mer C_j that passes split_test (so the segmented walk stops
+    before it) also carries bwd 'F' (so it is a start, not a collected splitter). The reference
+    walks C_0's contig on through C_j (kmer_hash.cpp:44 checks only the forward extension) and
+    walks C_j's own contig too. The segmented walk cannot link to C_j; it reports an overlap and
+    kh_assemble redoes the walk unsegmented: the text equals the oracle's."""
+    monkeypatch.setenv("KH_SPLIT_BITS", "4")  # splitters 1 in 16, and walked at that density
+    rng = np.random.default_rng(31 + k)
+    L = 300
+    seq = "".join("ACGT"[x] for x in rng.integers(0, 4, L + k - 1))
+    chain = [seq[i:i + k] for i in range(L)]
+    js = [j for j in range(2, L - 2) if _split_hash(chain[j]) < (1 << 28)]
+    assert js, "no chain k-mer passes split_test at 4 bits"
+    j = js[len(js) // 2]
+    lines = []
+    for i in range(L):
+        bwd = "F" if i in (0, j) else seq[i - 1]
+        fwd = "F" if i == L - 1 else seq[i + k]
+        lines.append(f"{chain[i]} {bwd}{fwd}\n")
+    lines += [f"{x} FF\n" for x in ("".join("ACGT"[b] for b in rng.integers(0, 4, k)) for _ in range(5))]
+    order = rng.permutation(len(lines))
+    recs = kh.pack_text(k, "".join(lines[i] for i in order).encode())
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0 and nc == 7
+    _, got, got_nc = run(k, recs)
+    assert got_nc == nc and got == want
+
+
 def test_empty_table():
     t = kh.KmerHashTable(19, 0)
     assert t.assemble() == (0, 0)
