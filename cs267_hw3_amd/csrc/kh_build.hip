@@ -663,39 +663,56 @@ __global__ __launch_bounds__(BUILD_THREADS) void k_part_build(KParams p, const u
 // comparing with the earlier keys of the same home.
 // Thread t scans the slots [t*E, t*E + E) of the slice: returns through hist[i] the first slot of
 // home i (C(i-1) + M(i)); wsum / wmax: TB / 64 words of LDS scratch.
+// The count prefix C and the prefix max M come from ONE block scan over pairs (s, m) = (keys of a
+// stretch of homes, max over its homes i of i - (keys before i within the stretch)), combined as
+// (s1, m1) . (s2, m2) = (s1 + s2, max(m1, m2 - s1)) (associative): one barrier per region instead
+// of a sum scan and a max scan with a barrier each.
 template <int TB>
 __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t& total, uint32_t* wsum);
 template <int TB>
 __device__ __forceinline__ void sorted_starts(uint32_t* hist, uint32_t S, uint32_t* wsum, int32_t* wmax) {
     const uint32_t E = (S + TB - 1) / TB;
     const uint32_t i0 = min(threadIdx.x * E, S), i1 = min(i0 + E, S);
-    uint32_t tot = 0;
-    for (uint32_t i = i0; i < i1; ++i) tot += hist[i];
-    uint32_t all;
-    const uint32_t base = block_scan_u32<TB>(tot, all, wsum);  // C(i0 - 1)
-    // prefix max of v(i) = i - C(i - 1): this thread's run, then across threads (exclusive)
-    int32_t run = INT32_MIN;
-    uint32_t c = base;
+    uint32_t s = 0;
+    int32_t mr = INT32_MIN / 2;  // (far below any i - C: no slot)
     for (uint32_t i = i0; i < i1; ++i) {
-        run = max(run, (int32_t)i - (int32_t)c);
-        c += hist[i];
+        mr = max(mr, (int32_t)i - (int32_t)s);
+        s += hist[i];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int32_t x = run;
+    uint32_t xs = s;
+    int32_t xm = mr;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x = max(x, y);
+    for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scan of the pairs
+        const uint32_t ys = __shfl_up(xs, o, 64);
+        const int32_t ym = __shfl_up(xm, o, 64);
+        if (lane >= o) {
+            xm = max(ym, xm - (int32_t)ys);
+            xs += ys;
+        }
     }
-    if (lane == 63) wmax[w] = x;
+    if (lane == 63) {
+        wsum[w] = xs;
+        wmax[w] = xm;
+    }
     lds_barrier();
-    int32_t pre = INT32_MIN;
+    uint32_t ps = 0;             // the waves before this one
+    int32_t pm = INT32_MIN / 2;
 #pragma unroll
     for (int k = 0; k < TB / 64; ++k)
-        if (k < w) pre = max(pre, wmax[k]);
-    const int32_t xin = __shfl_up(x, 1, 64);
-    int32_t m = max(pre, lane ? xin : INT32_MIN);  // max over the slots before i0
-    c = base;
+        if (k < w) {
+            pm = max(pm, wmax[k] - (int32_t)ps);
+            ps += wsum[k];
+        }
+    const uint32_t es = __shfl_up(xs, 1, 64);  // the lanes before this one in the wave
+    const int32_t em = __shfl_up(xm, 1, 64);
+    if (lane) {
+        pm = max(pm, em - (int32_t)ps);
+        ps += es;
+    }
+    const uint32_t base = ps;      // C(i0 - 1)
+    int32_t m = pm;                // max over the homes before i0 of i - C(i - 1)
+    uint32_t c = base;
     for (uint32_t i = i0; i < i1; ++i) {
         const uint32_t ci = hist[i];
         m = max(m, (int32_t)i - (int32_t)c);
