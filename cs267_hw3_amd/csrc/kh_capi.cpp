@@ -132,6 +132,8 @@ struct kh_table {
     uint64_t mw_wg = 0;        // walkers of every rank (bound of a round's input / held-back messages)
     uint64_t mw_store_n = 0;   // text records in mw_store (valid when mw_store_known)
     uint64_t mw_store_bound = 0;  // upper bound of the store's records (its device count: mw_misc[2])
+    bool mw_seg_off = false;      // kh_mwalk_redo: the next walk runs without splitter segments
+    uint64_t mw_store_min = 0;    // ... with a text store of at least this many records
     bool mw_store_known = true;
     uint32_t mw_P = 0, mw_rank = 0;
     bool mw_live = false, mw_stepped = false;
@@ -1421,7 +1423,7 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     uint64_t nsp = 0;
     // splitter segments: every splitter this shard owns seeds a walker too (kh_mseg.hip), on or
     // off the same way on every rank (walkers stop before splitters owned anywhere)
-    t->ms_on = mseg_enabled(t) && t->words_split;
+    t->ms_on = mseg_enabled(t) && t->words_split && !t->mw_seg_off;
     if (t->ms_on) {
         nsp = n_splitters;
         if ((rc = ensure_list(t, t->splits, t->splits_cap, nsp))) return rc;
@@ -1434,7 +1436,10 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     // text store: a walker appends each k-mer of this shard once, 32 bases per full word record,
     // and leaves at most a partial word, its finish record and a 2-record link where it ends
     // (held-back walkers flush nothing extra): shard / 32 + 4 per walker of every rank, doubled
-    const uint64_t store_cap = 2 * (t->n_inserted / 32 + 4 * t->mw_wg) + 4096;
+    uint64_t store_cap = 2 * (t->n_inserted / 32 + 4 * t->mw_wg) + 4096;
+    if (store_cap < t->mw_store_min) store_cap = t->mw_store_min;  // a redo sized by the last attempt
+    t->mw_seg_off = false;
+    t->mw_store_min = 0;
     if ((rc = t->mw_misc.ensure(64)) || (rc = t->mw_store.ensure(store_cap * 16)))
         return rc;
     t->ms_ns = ns;
@@ -1576,6 +1581,28 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
                                  t->route_scratch.as<uint64_t>(), t->stream));
     t->mw_cur = nxt;
     t->mw_stepped = true;
+    return KH_OK;
+}
+
+int kh_mwalk_flags_dev(kh_table* t, void* dev_out) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (!dev_out) return fail(KH_ERR_ARG, "null output");
+    if (int rc = set_device(t)) return rc;
+    KH_HIP(kh::launch_mw_flags(t->stats.as<unsigned long long>() + kh::ST_CHUNK_OVF, mw_word(t, 2), (uint64_t*)dev_out,
+                               t->stream));
+    return KH_OK;
+}
+
+int kh_mwalk_redo(kh_table* t, uint64_t store_records) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
+    // the overlap / overflow this walk reported is answered by the redo, not an error
+    KH_HIP(hipMemsetAsync(t->stats.as<unsigned long long>() + kh::ST_CHUNK_OVF, 0, 8, t->stream));
+    t->mw_seg_off = true;
+    t->mw_store_min = store_records;
+    t->mw_live = false;
+    t->assembled = false;
     return KH_OK;
 }
 

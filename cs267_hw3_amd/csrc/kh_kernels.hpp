@@ -270,6 +270,8 @@ hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, ui
                                 uint64_t* scratch, uint64_t* out, uint64_t* counts, hipStream_t s,
                                 const unsigned long long* n_dev = nullptr);
 // *fin != want (+ *want_dev) -> stats[ST_MISSING] (walkers that never came home)
+hipError_t launch_mw_flags(const unsigned long long* ovf, const unsigned long long* store_n, uint64_t* out,
+                           hipStream_t s);
 hipError_t launch_fin_check(const unsigned long long* fin, uint64_t want, const unsigned long long* want_dev,
                             uint64_t want_max, unsigned long long* stats, hipStream_t s);
 hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,

@@ -217,8 +217,10 @@ __global__ __launch_bounds__(BLOCK) void k_mseg_pred(const uint64_t* msgs, uint6
             }
             s = (s + 1 == cap2) ? 0 : s + 1;
         }
-        if (!found) {
-            atomicAdd(&stats[ST_MISSING], 1ull);
+        if (!found) {  // not a collected splitter: a start reached by another walk (overlapping walks,
+                       // malformed input) or a missing k-mer; the host redoes the walk unsegmented,
+                       // which walks through a start and reports a k-mer that is really missing
+            atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
             continue;
         }
         const uint64_t g = ns + id[s];

@@ -603,6 +603,18 @@ hipError_t launch_slot_round(const SlotRound& r, uint64_t* hist, uint64_t* off, 
     return hipGetLastError();
 }
 
+// [walks' overflow / overlap reports (ST_CHUNK_OVF), text records the store needed]
+__global__ void k_mw_flags(const unsigned long long* ovf, const unsigned long long* store_n, uint64_t* out) {
+    out[0] = *ovf;
+    out[1] = *store_n;
+}
+
+hipError_t launch_mw_flags(const unsigned long long* ovf, const unsigned long long* store_n, uint64_t* out,
+                           hipStream_t s) {
+    k_mw_flags<<<1, 1, 0, s>>>(ovf, store_n, out);
+    return hipGetLastError();
+}
+
 __global__ void k_add_count(unsigned long long* out, uint64_t a, const unsigned long long* b, uint64_t bmax) {
     const uint64_t v = b ? (uint64_t)*b : 0;
     *out = a + (v < bmax ? v : bmax);

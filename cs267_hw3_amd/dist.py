@@ -438,6 +438,15 @@ class GpuShard:
     def mw_end(self, recs, n):
         check(self.L.kh_mwalk_end_dev(self.h, self._p(recs), n))
 
+    def mw_flags(self):
+        """Device int64[2] (async): [overlap / overflow reports of this walk, store records needed]."""
+        out = self.zeros(2, torch.int64)
+        check(self.L.kh_mwalk_flags_dev(self.h, self._p(out)))
+        return out
+
+    def mw_redo(self, store_records):
+        check(self.L.kh_mwalk_redo(self.h, int(store_records)))
+
     # splitter segments of the migrating walk (kh_mseg.hip)
     LINK_WORDS = _lib.LINK_WORDS
     PRED_WORDS = _lib.PRED_WORDS
@@ -656,7 +665,8 @@ class DistributedKmerHashMap:
         nsp = int(host[1, :, nch + 1].sum())                  # splitters routed to this rank
         walkers = int(host[1, :, nch + 2].sum() + host[1, :, nch + 3].sum())
         splitters = int(host[1, :, nch + 3].sum())
-        return send_c, recv_c, gmax, int(host[0, 0, nch + 2]), nsp, walkers, splitters
+        starts = int(host[1, :, nch + 2].sum())
+        return send_c, recv_c, gmax, int(host[0, 0, nch + 2]), nsp, walkers, splitters, starts
 
     def insert_all(self, recs):
         """Route every record to its owner (+ this block's start k-mers), learn the per-chunk
@@ -686,6 +696,7 @@ class DistributedKmerHashMap:
                 c = self._host(sh.counters())
             self._ns, self._nsp = int(c[0]), int(c[1])
             self._walkers, self._splitters = self._ns + self._nsp, self._nsp
+            self._starts_all = self._ns
             return n
         nch = 1
         if exchange and self.INSERT_CHUNKS > 1 and n >= self.PIPELINE_MIN:
@@ -727,7 +738,7 @@ class DistributedKmerHashMap:
         spl = sh.route_splitters(P)
         cnt = sh.counters()
         mine = torch.stack([cnt[0], spl[:P].sum()])
-        send_c, recv_c, gmax, self._ns, self._nsp, self._walkers, self._splitters = \
+        send_c, recv_c, gmax, self._ns, self._nsp, self._walkers, self._splitters, self._starts_all = \
             self._exchange_count_matrix(counts, spl, mine)
         m = sum(sum(r) for r in recv_c)
         ok = True
@@ -778,8 +789,41 @@ class DistributedKmerHashMap:
         return m
 
     def assemble(self, total_kmers):
-        """Walk this rank's start k-mers (collective); returns the number of rounds."""
+        """Walk this rank's start k-mers (collective); returns the number of rounds. Walks that
+        overlap (malformed input) are redone unsegmented (see _redo)."""
+        self._seg_off = False
         return self._assemble_migrate(total_kmers)
+
+    REDO_MAX = 2  # unsegmented with the default store, then with the store the last attempt needed
+
+    def _flag(self):
+        """This walk's overlap / overflow report as a device int64 scalar (shards without it: 0)."""
+        sh = self.shard
+        if hasattr(sh, "mw_flags") and hasattr(getattr(sh, "L", None), "kh_mwalk_flags_dev"):
+            self._flags = sh.mw_flags()
+            return self._flags[:1]
+        self._flags = None
+        return None
+
+    def _redo(self, total_kmers, attempt):
+        """Some rank's walk reported overlapping walks (a splitter segment with two predecessors, a
+        start k-mer met as a splitter) or outgrew its text store: every rank walks again without
+        splitter segments — each start to its own end, as kmer_hash.cpp:41-53 does — with a store
+        sized from the last attempt's need. Every rank takes this branch together (the report
+        travelled with a count exchange)."""
+        if attempt >= self.REDO_MAX:
+            raise _lib.KmerHashError(_lib.KH_ERR_NOMEM, "migrating walk: overlapping walks or text store overflow "
+                                                        f"after {attempt} redo(s)")
+        sh = self.shard
+        need = int(self._host(self._flags)[1]) if attempt else 0
+        sh.mw_redo(need * 5 // 4 + 4096 if need else 0)
+        saved = self._splitters, self._walkers
+        self._splitters, self._walkers = 0, self._starts_all
+        self._seg_off = True
+        try:
+            return self._assemble_migrate(total_kmers, attempt + 1)
+        finally:
+            self._splitters, self._walkers = saved
 
     def _grow(self, name, n, dtype, device, slack=1.25):
         t = getattr(self, name, None)
@@ -806,7 +850,7 @@ class DistributedKmerHashMap:
 
     SLOT_CAP_MAX = 1 << 40  # tests: tiny slots (messages held back), set on the class
 
-    def _assemble_migrate(self, total_kmers):
+    def _assemble_migrate(self, total_kmers, attempt=0):
         """Walkers move to the rank owning their next k-mer (minimizer sharding keeps runs of
         consecutive k-mers on one rank). A round = local walk -> one all-to-all of fixed-size
         slots: no host read per round; the host reads the global in-flight count only at checks
@@ -892,7 +936,13 @@ class DistributedKmerHashMap:
         tb = sh.mw_text_bound()
         tout = self._grow("_mw_tout", max(tb, 1) * T, torch.int64, dev)
         counts = sh.mw_text(tout)
-        send_splits, recv_splits, _, gmax, _ = self._exchange_counts(counts)
+        segmented = bool(self._splitters) and hasattr(sh, "mw_segments")
+        # unsegmented walks report their store overflow (overlapping walks) with this exchange;
+        # segmented ones with the retag exchange (_segments_end), after the segment links
+        flag = None if segmented else self._flag()
+        send_splits, recv_splits, _, gmax, over = self._exchange_counts(counts, flag)
+        if flag is not None and any(int(x) for x in over):
+            return self._redo(total_kmers, attempt)
         r = sum(recv_splits)
         if local:
             trecv = tout
@@ -902,8 +952,9 @@ class DistributedKmerHashMap:
             self._all_to_all(trecv[:r * T], tout[:sum(send_splits) * T], [c * T for c in recv_splits],
                              [c * T for c in send_splits], gmax * T)
         # every rank takes the same branch (a rank without splitters still links and answers)
-        if self._splitters and hasattr(sh, "mw_segments"):
-            self._segments_end(trecv, r, self._ns + self._nsp)
+        if segmented:
+            if not self._segments_end(trecv, r, self._ns + self._nsp):
+                return self._redo(total_kmers, attempt)
         else:
             self._begin("materialize")
             sh.mw_end(trecv, r)
@@ -956,7 +1007,10 @@ class DistributedKmerHashMap:
         self._begin("seg_retag")
         tout = self._grow("_ms_t", max(r + nseg, 1) * S, torch.int64, dev)
         counts = sh.mw_retag(trecv, r, tout)
-        send_splits, recv_splits, _, gmax, _ = self._exchange_counts(counts)
+        flag = self._flag()  # overlapping walks (links, predecessors) or a store overflow, any rank
+        send_splits, recv_splits, _, gmax, over = self._exchange_counts(counts, flag)
+        if flag is not None and any(int(x) for x in over):
+            return False
         m = sum(recv_splits)
         if local:
             tin = tout
@@ -966,6 +1020,7 @@ class DistributedKmerHashMap:
                              [c * S for c in send_splits], gmax * S)
         self._begin("materialize")
         sh.mw_end_seg(trecv, r, tin, m)
+        return True
 
     def contigs_text(self):
         """This rank's contig text (D2H; outside the timed region)."""

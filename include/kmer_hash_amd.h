@@ -213,6 +213,15 @@ int kh_mwalk_end_dev(kh_table* t, const void* dev_recs, uint64_t n);
 #define KH_PRED_WORDS 2
 #define KH_SEG_REC_WORDS 3
 int kh_mwalk_segments(kh_table* t, uint64_t* n_splitter_segments);
+/* Malformed input whose start walks overlap (a k-mer reached by two walks): a segmented walk
+ * cannot give one splitter segment two contigs, and an unsegmented one may outgrow its text store.
+ * kh_mwalk_flags_dev writes 2 uint64 to device memory (async): [overlap / overflow reports of this
+ * walk, text records the store needed]; hosts exchange the first with a count exchange they make
+ * anyway, and when any rank reports one, every rank calls kh_mwalk_redo (ends this walk, clears the
+ * report) and walks again from kh_mwalk_begin: without splitter segments (each start walked to its
+ * end, as kmer_hash.cpp:41-53 does) and with a store of at least store_records records. */
+int kh_mwalk_flags_dev(kh_table* t, void* dev_out2);
+int kh_mwalk_redo(kh_table* t, uint64_t store_records);
 int kh_mwalk_link_dev(kh_table* t, const void* dev_recs, uint64_t n, void* dev_links_out, void* dev_counts_out);
 int kh_mwalk_pred_dev(kh_table* t, const void* dev_links, uint64_t m, void* dev_preds_out, uint64_t stride);
 int kh_mwalk_resolve_dev(kh_table* t, const void* dev_all_preds, uint64_t stride);

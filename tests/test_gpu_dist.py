@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import cs267_hw3_amd as kh
+import oracle_bind as ob
 
 pytestmark = pytest.mark.gpu
 
@@ -212,13 +213,18 @@ def test_sharded_small_then_large_input(P):
     check_ranks(gs, texts[2], P)
 
 
-def test_sharded_overlapping_walks_fail_loudly():
-    """Walks that run into each other (malformed input: a k-mer with two predecessors) make a
-    splitter segment two walks' successor; the sharded walk cannot write one segment into two
-    contigs, so it fails with an error on every rank instead of returning wrong text (the
-    single-GPU kh_assemble redoes such a walk unsegmented: test_overlapping_walks_redo)."""
+@pytest.mark.parametrize("k,L,every,P", [(19, 3000, 1, 2), (51, 1500, 3, 2), (19, 2000, 2, 3)])
+def test_sharded_overlapping_walks(k, L, every, P):
+    """Walks that run into each other (malformed input: a k-mer with several predecessors, every
+    start walking the shared tail again, kmer_hash.cpp:41-53) make a splitter segment two walks'
+    successor: the segmented walk reports the overlap with its retag count exchange and every rank
+    walks again without splitter segments (then once more with the text store the first redo
+    needed). The ranks' texts, concatenated in rank order, equal the oracle's byte for byte (as the
+    single-GPU kh_assemble's redo does, test_overlapping_walks_redo)."""
     from cs267_hw3_amd.dist import run_threaded
     from test_gpu_parity import merging_walks
-    recs = merging_walks(19, 3000, seed=26)
-    with pytest.raises(kh.KmerHashError):
-        run_threaded(19, recs, 2)
+    recs = merging_walks(k, L, seed=26 + k, every=every)
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0 and len(want) > 4 * len(recs)
+    texts = run_threaded(k, recs, P)
+    assert b"".join(texts) == want
