@@ -57,6 +57,7 @@ SEG_REC_WORDS = 3  # KH_SEG_REC_WORDS
 
 _SIGS = {
     "kh_abi_version": (ctypes.c_int, []),
+    "kh_device_bytes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "kh_packed_size": (ctypes.c_int, [ctypes.c_int]),
     "kh_record_size": (ctypes.c_int, [ctypes.c_int]),
     "kh_last_error": (ctypes.c_char_p, []),

@@ -5,6 +5,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <string>
@@ -46,14 +47,23 @@ int fail(int code, const char* fmt, ...) {
     } while (0)
 
 // Grow-only device buffer.
+// device bytes held by every table's buffers in this process, and their high-water mark
+// (kh_device_bytes: checks tools/mem_model.py against what the sharded path really allocates)
+std::atomic<uint64_t> g_dev_bytes{0}, g_dev_peak{0};
+
+void dev_account(int64_t delta) {
+    const uint64_t now = g_dev_bytes.fetch_add((uint64_t)delta) + (uint64_t)delta;
+    uint64_t pk = g_dev_peak.load();
+    while (now > pk && !g_dev_peak.compare_exchange_weak(pk, now)) {
+    }
+}
+
 struct DevBuf {
     void* p = nullptr;
     uint64_t bytes = 0;
     int ensure(uint64_t want) {
         if (want <= bytes && p) return KH_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
+        release();
         if (want == 0) want = 16;
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) {
@@ -62,10 +72,14 @@ struct DevBuf {
                         hipGetErrorString(e));
         }
         bytes = want;
+        dev_account((int64_t)want);
         return KH_OK;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            dev_account(-(int64_t)bytes);
+        }
         p = nullptr;
         bytes = 0;
     }
@@ -340,6 +354,13 @@ static_assert(KH_MSG_WORDS == kh::MSG_WORDS, "message layout");
 extern "C" {
 
 int kh_abi_version(void) { return KH_ABI_VERSION; }
+
+int kh_device_bytes(uint64_t* now, uint64_t* peak, int reset_peak) {
+    if (now) *now = g_dev_bytes.load();
+    if (peak) *peak = g_dev_peak.load();
+    if (reset_peak) g_dev_peak.store(g_dev_bytes.load());
+    return KH_OK;
+}
 int kh_packed_size(int k) { return (k >= 1 && k <= KH_K_MAX) ? (k + 3) / 4 : KH_ERR_ARG; }
 int kh_record_size(int k) { return (k >= 1 && k <= KH_K_MAX) ? (k + 3) / 4 + 2 : KH_ERR_ARG; }
 const char* kh_last_error(void) { return g_err.c_str(); }
@@ -804,6 +825,9 @@ int kh_assemble_dev(kh_table* t) {
     wb.chunk_seq = t->chunk_seq.as<uint32_t>();
     wb.chunk_cap = chunk_cap;
     wb.max_steps = n;
+    // short contigs (C5: ~9 k-mers each): 32 queue batches per atomic (C5 walk 3.27 -> 2.99 ms at
+    // round 5); long ones keep 8 (C3 1.18 -> 1.85 ms at 32: a wave's batches wait for a straggler)
+    wb.batches = (ns && n / ns < 24) ? 32u : 0u;
     wb.headrec = t->headrec.as<uint64_t>();
     wb.hcap = t->headrec.p ? t->hcap : 0u;
     kh::SegBuffers sb{};
@@ -811,7 +835,7 @@ int kh_assemble_dev(kh_table* t) {
         // walkers may stop before a splitter k-mer even when none was collected (then the link
         // step reports it missing), so the segment arrays exist whenever splitting is on
         const uint64_t cap2 = 2 * nsp + 64;
-        if ((rc = t->seg_next.ensure((nseg + 1) * 4)) || (rc = t->seg_key.ensure((nseg + 1) * 16)) ||
+        if ((rc = t->seg_next.ensure((nseg + 4) * 4)) || (rc = t->seg_key.ensure((nseg + 1) * 16)) ||
             (rc = t->seg_contig.ensure((nseg + 1) * 4)) || (rc = t->seg_off.ensure((nseg + 1) * 4)) ||
             (rc = t->clen.ensure((ns + 1) * 4)) || (rc = t->stab.ensure(cap2 * 16)) ||
             (rc = t->stab_id.ensure(cap2 * 4)) || (rc = t->seg_jump.ensure((nseg + 1) * 4)) ||

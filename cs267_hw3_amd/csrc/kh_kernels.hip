@@ -336,6 +336,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
     const bool chains = p.chain && wb.hcap != 0;
     uint64_t bbase = 0, rbase = 0;
     uint32_t bused = WALK_GRAB, rleft = 0;  // rleft: walkers left in the wave's reservation
+    const uint32_t grab_all = WALK_GRAB * (wb.batches ? wb.batches : (uint32_t)WALK_BATCHES);
     bool bdry = false;
     uint64_t bw0 = 0, bw1 = 0;
 
@@ -369,9 +370,9 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                         if (rleft == 0) {  // reserve WALK_BATCHES batches with one atomic
                             unsigned long long g = 0;
                             if (lane == 0)
-                                g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)WALK_GRAB * WALK_BATCHES);
+                                g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)grab_all);
                             rbase = __shfl(g, 0, 64);
-                            rleft = WALK_GRAB * WALK_BATCHES;
+                            rleft = grab_all;
                         }
                         bbase = rbase;
                         rbase += WALK_GRAB;
@@ -1133,7 +1134,12 @@ __global__ __launch_bounds__(BLOCK) void k_stab_build(KParams p, WalkBuffers wb,
 __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
     const uint64_t cap2 = stab_cap(wb, sb.cap2);
-    for (uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; g < nseg; g += (uint64_t)gridDim.x * BLOCK) {
+    // most segments end at 'F' (C5: 21M of 21.8M): a thread tests 4 with one 16-B load (seg_next
+    // is 16-B aligned, its allocation rounded up to 4 entries)
+    for (uint64_t g4 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; 4 * g4 < nseg; g4 += (uint64_t)gridDim.x * BLOCK) {
+        const uint4 v = reinterpret_cast<const uint4*>(wb.seg_next)[g4];
+        if (v.x != SEG_AT_SPLIT && v.y != SEG_AT_SPLIT && v.z != SEG_AT_SPLIT && v.w != SEG_AT_SPLIT) continue;
+        for (uint64_t g = 4 * g4; g < min(4 * g4 + 4, nseg); ++g) {
         if (wb.seg_next[g] != SEG_AT_SPLIT) continue;
         const Key k{wb.seg_key[2 * g], wb.seg_key[2 * g + 1]};
         uint64_t s = mulhi64(fmix64(key_hash(k)), cap2);
@@ -1154,6 +1160,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, SegBuffers s
         // walker steps through the start and reports a k-mer that is really missing.
         if (nx == SEG_NONE) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
         wb.seg_next[g] = nx;
+        }
     }
 }
 
@@ -1180,11 +1187,11 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers 
             // segment text would be written once, so kh_assemble redoes the walk unsegmented.
             // Segment links lead to splitter segments only, so the contig's own start segment is
             // reached by this thread alone: a plain store (C5: 21M atomics fewer)
-            if (hops == 0)
-                sb.seg_contig[g] = (uint32_t)c;
-            else if (atomicExch(&sb.seg_contig[g], (uint32_t)c) != SEG_NONE)
-                atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
-            sb.seg_off[g] = (uint32_t)off;
+            // (segment c < n_starts is contig c's own start segment at offset 0: not stored)
+            if (hops) {
+                if (atomicExch(&sb.seg_contig[g], (uint32_t)c) != SEG_NONE) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+                sb.seg_off[g] = (uint32_t)off;
+            }
             off += wb.contig_len[g] - 1;
             g = wb.seg_next[g];
             if (g == SEG_NONE) break;
@@ -1203,10 +1210,13 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers 
     }
 }
 
+// (jump pointers and anchors are splitter segments' only: a long chain continues past its start
+// segment through splitter segments, and k_seg_chain_jump starts at one)
 __global__ __launch_bounds__(BLOCK) void k_seg_jump(WalkBuffers wb, SegBuffers sb) {
     if (!*sb.long_flag) return;
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg; i += (uint64_t)gridDim.x * BLOCK) {
+    for (uint64_t i = wb.n_starts + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg;
+         i += (uint64_t)gridDim.x * BLOCK) {
         uint32_t g = (uint32_t)i, sum = 0;
         for (uint32_t h = 0; h < SEG_JUMP && g != SEG_NONE; ++h) {
             sum += wb.contig_len[g] - 1;
@@ -1244,7 +1254,8 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain_jump(WalkBuffers wb, SegBuf
 __global__ __launch_bounds__(BLOCK) void k_seg_fill(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     if (!*sb.long_flag) return;
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg; i += (uint64_t)gridDim.x * BLOCK) {
+    for (uint64_t i = wb.n_starts + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nseg;
+         i += (uint64_t)gridDim.x * BLOCK) {
         if (!sb.anchor[i]) continue;
         uint32_t g = (uint32_t)i;
         const uint32_t c = sb.seg_contig[g];
@@ -1293,7 +1304,9 @@ hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBu
     if (nseg == 0) return hipSuccess;
     k_stab_init<<<(unsigned)hmin((sb.cap2 + BLOCK - 1) / BLOCK, 2048), BLOCK, 0, s>>>(wb, sb.stab, sb.cap2);
     hipError_t e;
-    if ((e = hipMemsetAsync(sb.seg_contig, 0xff, nseg * 4, s)) != hipSuccess) return e;
+    // splitter segments' contigs (a start segment's is itself, never stored)
+    if (wb.n_splits && (e = hipMemsetAsync(sb.seg_contig + wb.n_starts, 0xff, wb.n_splits * 4, s)) != hipSuccess)
+        return e;
     if (wb.n_splits)
         k_stab_build<<<(unsigned)hmin((wb.n_splits + BLOCK - 1) / BLOCK, 4096), BLOCK, 0, s>>>(
             p, wb, sb.stab, sb.stab_id, sb.cap2);
@@ -1308,7 +1321,7 @@ hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuf
     if (nseg == 0) return hipSuccess;
     hipError_t e;
     const unsigned gs = (unsigned)hmin((nseg + BLOCK - 1) / BLOCK, 8192);
-    k_seg_link<<<gs, BLOCK, 0, s>>>(wb, sb, stats);
+    k_seg_link<<<(unsigned)hmin((nseg / 4 + BLOCK) / BLOCK, 8192), BLOCK, 0, s>>>(wb, sb, stats);
     if (wb.n_starts == 0) return hipGetLastError();
     const unsigned gc = (unsigned)hmin((wb.n_starts + BLOCK - 1) / BLOCK, 8192);
     if ((e = hipMemsetAsync(sb.long_flag, 0, 4, s)) != hipSuccess) return e;
@@ -1339,14 +1352,16 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
         const uint64_t ch = t / WC_TPC;
         const uint32_t q = (uint32_t)(t % WC_TPC);
         const uint32_t g = ch < nseg ? (uint32_t)ch : owner[ch];
-        const uint32_t c = seg_contig[g];
+        const bool own = g < n_starts;  // a contig's start segment: contig g, offset 0
+        const uint32_t c = own ? g : seg_contig[g];
         if (c == SEG_NONE) continue;  // a segment no contig reached
         const uint64_t cb = ch < nseg ? 0ull : (uint64_t)seq[ch] * CHUNK_BASES;
         const uint64_t app = (uint64_t)seg_len[g] - 1;
         if (cb + 32 * q >= app) continue;
         const uint32_t cnt = (uint32_t)min<uint64_t>(CHUNK_BASES, app - cb);
-        if (off[c] + K + seg_off[g] + cb + cnt > cap) continue;  // past the buffer: not written
-        char* o = out + off[c] + K + seg_off[g] + cb;
+        const uint64_t so = own ? 0ull : (uint64_t)seg_off[g];
+        if (off[c] + K + so + cb + cnt > cap) continue;  // past the buffer: not written
+        char* o = out + off[c] + K + so + cb;
         for (uint32_t w = q; 32 * w < cnt; w += WC_TPC) {
             const uint64_t word = chunk_data[chunk_word(ch, w, chunk_cap)];
             store_chars(o + 32 * w, min(32u, cnt - 32 * w),

@@ -93,6 +93,9 @@ struct WalkBuffers {
     // bytes of the text buffer the materialisation writes into (0: sized from the scanned total);
     // a contig that would pass it is not written (the caller compares the total with it)
     uint64_t text_cap = 0;
+    // work-queue batches a wave reserves per atomic (0: WALK_BATCHES); kh_assemble_dev takes 32
+    // for short contigs (C5: 21M contigs of ~9 k-mers), where the queue's one counter is the limit
+    uint32_t batches = 0;
 };
 
 // Persistent per-lane walker (single GPU): every lane walks whole contigs, pulling start k-mers

@@ -320,6 +320,7 @@ class GpuShard:
         self.W = self.L.kh_word_count(k)
         self.h = self.table._h
         self.n_kmers = n_kmers
+        self.n_table = n_kmers  # the table's sizing (kh_create, grown by reserve)
         self.stream = torch.cuda.Stream(device=self.dev)
         self.table.set_stream(self.stream.cuda_stream)
         self.inserted = 0  # k-mers the shard holds since the last clear
@@ -365,6 +366,7 @@ class GpuShard:
         """Room for m more k-mers: an empty shard grows to them (kh_reserve); a non-empty one must
         already have the room (kh_reserve fails otherwise: the caller's ranks agree on it)."""
         check(self.L.kh_reserve(self.h, int(self.inserted + m)))
+        self.n_table = max(self.n_table, int(self.inserted + m))
 
     def insert_records(self, recs):
         """One rank: the route is the identity, so the block's records go straight through the
@@ -511,6 +513,7 @@ class DistributedKmerHashMap:
         self._cur = None
         self.timer = None       # a PhaseTimer: per-phase stream time of the step (bench)
         self.xbytes = 0         # bytes this rank sent to other ranks in the step (all exchanges)
+        self.text_records = self.seg_records = 0  # text / retag records received by the last walk
 
     # tests: stall this rank when it begins phase HANG_AT[0] (HANG_AT[1] = the rank) — a rank that
     # never reaches the next collective, as a crashed or diverged peer would look to the others
@@ -944,6 +947,7 @@ class DistributedKmerHashMap:
         if flag is not None and any(int(x) for x in over):
             return self._redo(total_kmers, attempt)
         r = sum(recv_splits)
+        self.text_records = r  # text records this origin received (tools/mem_model.py checks)
         if local:
             trecv = tout
         else:
@@ -1012,6 +1016,7 @@ class DistributedKmerHashMap:
         if flag is not None and any(int(x) for x in over):
             return False
         m = sum(recv_splits)
+        self.seg_records = m
         if local:
             tin = tout
         else:
@@ -1091,6 +1096,11 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
                     info.setdefault("stats", {})[r] = shard.stats()
                     info.setdefault("syncs", {})[r] = syncs
                     info.setdefault("checks", {})[r] = dm.checks
+                    # the counts tools/mem_model.py sizes a rank's buffers from
+                    info.setdefault("counts", {})[r] = dict(
+                        n_ins=shard.inserted, n_table=shard.n_table, ns=dm._ns, nsp=dm._nsp,
+                        walkers_all=dm._walkers, recv_text=dm.text_records, recv_seg=dm.seg_records,
+                        cap_slot=max(dm._caps) if dm._caps else 0)
             shard.table.close()
         except BaseException as ex:  # surface thread failures
             errs.append(ex)

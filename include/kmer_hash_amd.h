@@ -75,6 +75,9 @@ typedef struct kh_stats {
 
 /* ---- sizes / info --------------------------------------------------------------------------*/
 int kh_abi_version(void);
+/* Device bytes the library's buffers hold now in this process (every table) and their high-water
+ * mark since the last reset (reset_peak != 0 restarts it at `now` after reading). */
+int kh_device_bytes(uint64_t* now, uint64_t* peak, int reset_peak);
 int kh_packed_size(int k);   /* sizeof(pkmer_t)   */
 int kh_record_size(int k);   /* sizeof(kmer_pair) */
 const char* kh_last_error(void);

@@ -230,3 +230,99 @@ def test_c5_hot_bucket_1b_8_ranks(load):
     ranks (logical, one GPU), loads 0.5 and 0.85; every rank's text equals its block's truth."""
     info = _sharded(_gen(C5H, 1_000_000_000), 8, load_factor=load)
     assert sum(s["n_inserted"] for s in info["stats"].values()) == 1_000_000_000
+
+
+def _mem_model():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "mem_model", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "mem_model.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _dev_bytes():
+    """Device bytes held now: the library's buffers (every table) + torch's allocated tensors."""
+    import ctypes
+    from cs267_hw3_amd import _lib
+    now = ctypes.c_uint64(0)
+    _lib.lib().kh_device_bytes(ctypes.byref(now), None, 0)
+    torch.cuda.synchronize()
+    return now.value, torch.cuda.memory_allocated()
+
+
+def test_mem_model_matches_measured_c3_routed_one_rank():
+    """tools/mem_model.py (the sizing formulas of the library's buffers and the Python host's)
+    against what the sharded step holds after a step: C3 200M through the one-pass route at one
+    rank (the step P > 1 runs), the model fed with the step's own counts. Within 15 %."""
+    import gc
+    from cs267_hw3_amd.dist import DistributedKmerHashMap, GpuShard, ThreadComm
+    gc.collect()
+    torch.cuda.empty_cache()
+    lib0, tor0 = _dev_bytes()
+    n = 200_000_000
+    g = _gen(C3, n)
+    recs = g.records_dev(0, n, device=0)
+    shard = GpuShard(51, int(n * 1.02) + 4096, device=0)
+    with torch.cuda.stream(shard.stream):
+        dm = DistributedKmerHashMap(ThreadComm.group(1)[0], shard)
+        dm.ROUTE_ONE_RANK = True
+        for step in range(2):
+            if step:
+                shard.clear()
+            dm.insert_all(recs)
+            dm.assemble(n)
+    lib1, tor1 = _dev_bytes()
+    assert dm.contigs_text() == g.truth(0, n)
+    mm = _mem_model()
+    items = mm.rank_model(P=1, n_rec=n, n_ins=n, n_table=int(n * 1.02) + 4096, ns=dm._ns, nsp=dm._nsp,
+                          walkers_all=dm._walkers, routed=True, windows=True, exchange=False,
+                          recv_text=dm.text_records, recv_seg=dm.seg_records)
+    lib_m, tor_m = mm.totals(items)
+    got_lib, got_tor = lib1 - lib0, tor1 - tor0
+    print(f"model lib {lib_m / 1e9:.2f} torch {tor_m / 1e9:.2f} GB; measured lib {got_lib / 1e9:.2f} "
+          f"torch {got_tor / 1e9:.2f} GB", file=sys.stderr)
+    assert abs(lib_m + tor_m - got_lib - got_tor) <= 0.15 * (got_lib + got_tor)
+    assert abs(lib_m - got_lib) <= 0.15 * got_lib
+    shard.table.close()
+    del recs, dm, shard
+
+
+def test_mem_model_matches_measured_c5_8_ranks():
+    """The same for C5 (walker skew: rank 0 holds every start k-mer) at 200M over 8 logical ranks
+    on one GPU: the model fed with each rank's own counts, and the model fed with the counts
+    workload_ranks() derives from the generator's parameters (as the 1B claim of DESIGN.md §6 is):
+    both totals over the 8 ranks within 15 % of what the ranks hold after the step."""
+    import gc
+    import threading
+    from cs267_hw3_amd.dist import run_threaded
+    gc.collect()
+    torch.cuda.empty_cache()
+    lib0, tor0 = _dev_bytes()
+    n, P = 200_000_000, 8
+    g = _gen(C5, n)
+    seen = {}
+    bar = threading.Barrier(P)
+
+    def check(r, text):
+        bar.wait()          # every rank's walk is done, no shard closed yet
+        if r == 0:
+            seen["bytes"] = _dev_bytes()
+        bar.wait()
+        b, e = g.block(P, r)
+        assert text == g.truth(b, e)
+
+    info = {}
+    run_threaded(51, g, P, check=check, info=info, shard_kmers=int(n / P * 1.02) + 4096)
+    lib1, tor1 = seen["bytes"]
+    got = (lib1 - lib0) + (tor1 - tor0)
+    mm = _mem_model()
+    exact = 0
+    for r in range(P):
+        b, e = g.block(P, r)
+        exact += sum(mm.totals(mm.rank_model(P=P, n_rec=e - b, **info["counts"][r])))
+    derived = sum(sum(mm.totals(mm.rank_model(**rk))) for rk in mm.workload_ranks("c5", n, P))
+    print(f"model {exact / 1e9:.2f} GB (rank counts), {derived / 1e9:.2f} GB (workload counts); measured "
+          f"{got / 1e9:.2f} GB (library {(lib1 - lib0) / 1e9:.2f})", file=sys.stderr)
+    assert abs(exact - got) <= 0.15 * got
+    assert abs(derived - got) <= 0.15 * got
