@@ -825,9 +825,9 @@ int kh_assemble_dev(kh_table* t) {
     wb.chunk_seq = t->chunk_seq.as<uint32_t>();
     wb.chunk_cap = chunk_cap;
     wb.max_steps = n;
-    // short contigs (C5: ~9 k-mers each): 32 queue batches per atomic (C5 walk 3.27 -> 2.99 ms at
-    // round 5); long ones keep 8 (C3 1.18 -> 1.85 ms at 32: a wave's batches wait for a straggler)
-    wb.batches = (ns && n / ns < 24) ? 32u : 0u;
+    // (32 queue batches per atomic for short contigs measured slower at C5 in round 6: walk kernel
+    // 2.745 -> 2.87 ms; round 5's 3.27 -> 2.99 predates the single place() site)
+    wb.batches = 0;
     wb.headrec = t->headrec.as<uint64_t>();
     wb.hcap = t->headrec.p ? t->hcap : 0u;
     kh::SegBuffers sb{};
