@@ -1166,22 +1166,32 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
 
     for _ in range(args.warmup):
         step()
+    # the contract's bracket: barrier + synchronize on both sides of the K steps (round 5 put a
+    # barrier inside every step: ~0.2 ms of a one-rank step was that closing barrier). Each step
+    # still ends in a synchronize, as the single-GPU bench's steps do, for its wall time and the
+    # phase events; the steps' own collectives keep the ranks in step.
     times, phases, ptimes, xbytes, syncs = [], [], [], [], []
+    dist.barrier()
+    torch.cuda.synchronize()
+    t_all = time.perf_counter()
     for _ in range(args.steps):
-        dist.barrier()
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
         s0 = dm.host_syncs()
         step()
         torch.cuda.synchronize()
-        dist.barrier()
         times.append(time.perf_counter() - t0)
         phases.append(shard.stats())
         ptimes.append(dm.timer.totals())
         xbytes.append(dm.xbytes)
         syncs.append(dm.host_syncs() - s0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t_all = time.perf_counter() - t_all
     print(f"[rank {rank}] step ms: " + " ".join(f"{1e3 * x:.2f}" for x in times), file=sys.stderr, flush=True)
-    mine = sum(times) / len(times)
+    for i in (0, len(ptimes) - 1):
+        print(f"[rank {rank}] step {i} phases ms: " + " ".join(f"{nm} {v:.3f}" for nm, v in ptimes[i].items()),
+              file=sys.stderr, flush=True)
+    mine = t_all / args.steps
     tmax = comm.all_reduce_max(mine)
     # per-rank phase times (mean over the timed steps) -> max / min over ranks, in PHASES order
     names = list(DistributedKmerHashMap.PHASES)
@@ -1271,7 +1281,8 @@ def bench_main(args, w, world, rank, cpu_baseline=None, load_traffic=None):
             "phases_ms": {"insert_pipeline_rank0": ins_ms, "build_rank0": build_ms},
             # per-rank stream time of each driver phase (HIP events), max / min over the ranks
             "rank_phases_ms": rank_phases,
-            "rank_step_ms": {"max": tmax * 1e3, "mean_rank0": mine * 1e3},
+            "rank_step_ms": {"max": tmax * 1e3, "mean_rank0": mine * 1e3,
+                             "median_step_rank0": 1e3 * sorted(times)[len(times) // 2]},
             "exchange_bytes_per_step": {"max": hi[nph], "min": lo[nph]},
             "host_syncs_per_step": {"max": hi[nph + 1], "min": lo[nph + 1]},
             "build_ms": {"max": hi[nph + 2], "min": lo[nph + 2]},
