@@ -350,7 +350,7 @@ hipError_t launch_mseg_check(uint64_t ns, uint64_t nseg, const MSegState& st, co
 // 3-word record: [origin << 56 | type << 48 | contig, type 0: pos | count << 48, type 1: end; word]
 struct RetagOp {
     const uint64_t* recs;
-    uint64_t n, ns;
+    uint64_t n, ns, nsp;
     MSegState st;
     uint64_t* out;
     __device__ bool seg_rec(uint64_t i, uint64_t& c) const {
@@ -358,7 +358,7 @@ struct RetagOp {
         const uint64_t t = recs[2 * i];
         if ((t >> 55) & 1) return false;
         c = t & 0x7FFFFFFFull;
-        return c >= ns && st.done[c];
+        return c >= ns && c < ns + nsp && st.done[c];  // (a walker id past the segments: not ours)
     }
     __device__ int owner(uint64_t i) const {
         uint64_t c;
@@ -392,7 +392,7 @@ hipError_t launch_mseg_retag(const uint64_t* recs, uint64_t n, uint64_t ns, uint
                              uint32_t P, uint64_t* hist, uint64_t* off, uint64_t* scratch, uint64_t* out,
                              uint64_t* counts, hipStream_t s) {
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    return group_by_owner(RetagOp{recs, n, ns, st, out}, n + nsp, P, hist, off, scratch + 1, counts, total, s);
+    return group_by_owner(RetagOp{recs, n, ns, nsp, st, out}, n + nsp, P, hist, off, scratch + 1, counts, total, s);
 }
 
 // ---- origin: lengths and characters ----------------------------------------------------------------

@@ -329,10 +329,11 @@ __global__ __launch_bounds__(BLOCK) void k_mw_compact(const uint64_t* stage, con
         // inclusive end of each lane's records; the run's total from the last lane
         const uint32_t last = (uint32_t)min<uint64_t>(n - j0, 64) - 1;
         const uint32_t tot = __shfl(rel + c, (int)last, 64);
-        if (base + tot > store_cap) {  // the store's bound was wrong (a cycle?): fail, never overrun
-            if (lane == 0) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
-            continue;
-        }
+        // past the store's bound (malformed input: overlapping walks): the records that fit are
+        // written, so every record below the bound is real (the text grouping reads up to it), and
+        // the overflow is reported (the walk is redone with a larger store)
+        if (base + tot > store_cap && lane == 0) atomicAdd(&stats[ST_CHUNK_OVF], 1ull);
+        if (base >= store_cap) continue;
         for (uint32_t t0 = 0; t0 < tot; t0 += 64) {
             const uint32_t t = t0 + lane;
             // the input holding record t: the last lane whose run starts at or before t (lanes
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(BLOCK) void k_mw_compact(const uint64_t* stage, con
                 if (lo + st <= last && v <= t) lo += st;
             }
             const uint32_t r0 = __shfl(rel, (int)lo, 64);
-            if (t < tot) {
+            if (t < tot && base + t < store_cap) {
                 const ulonglong2* src =
                     reinterpret_cast<const ulonglong2*>(stage + (j0 + lo) * (MW_REC_SLOTS * 2)) + (t - r0);
                 reinterpret_cast<ulonglong2*>(store)[base + t] = *src;
@@ -371,7 +372,12 @@ struct RecOp {
     const uint64_t* recs;
     uint64_t* out;
     const unsigned long long* n_dev;  // records past the live count do not exist (null: all)
-    __device__ int owner(uint64_t i) const { return (n_dev && i >= *n_dev) ? -1 : (int)(recs[2 * i] >> 56); }
+    uint32_t P;
+    __device__ int owner(uint64_t i) const {
+        if (n_dev && i >= *n_dev) return -1;
+        const uint32_t q = (uint32_t)(recs[2 * i] >> 56);
+        return q < P ? (int)q : -1;  // (a record's origin is a rank: anything else is not sent)
+    }
     __device__ void emit(uint64_t i, int q, uint64_t d) const {
         if (q < 0) return;  // past the live count
         reinterpret_cast<ulonglong2*>(out)[d] = reinterpret_cast<const ulonglong2*>(recs)[i];
@@ -483,7 +489,7 @@ hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, ui
         return hipGetLastError();
     }
     unsigned long long* total = reinterpret_cast<unsigned long long*>(scratch);
-    return group_by_owner(RecOp{recs, out, n_dev}, n, P, hist, off, scratch + 1, counts, total, s);
+    return group_by_owner(RecOp{recs, out, n_dev, P}, n, P, hist, off, scratch + 1, counts, total, s);
 }
 
 // ---- fixed-size exchange slots ---------------------------------------------------------------------

@@ -213,6 +213,18 @@ def test_sharded_small_then_large_input(P):
     check_ranks(gs, texts[2], P)
 
 
+def _dirty_device_memory(gib=4):
+    """Fill free device memory with 0xFF bytes and hand it back to the driver, so buffers the next
+    step allocates start as garbage (a fresh box hands out zeros, which hid round 6's store-overflow
+    bug: text records past the store's end read as rank 255)."""
+    import torch
+    t = torch.empty(gib << 30, dtype=torch.uint8, device="cuda")
+    t.fill_(0xFF)
+    torch.cuda.synchronize()
+    del t
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("k,L,every,P", [(19, 3000, 1, 2), (51, 1500, 3, 2), (19, 2000, 2, 3)])
 def test_sharded_overlapping_walks(k, L, every, P):
     """Walks that run into each other (malformed input: a k-mer with several predecessors, every
@@ -226,5 +238,6 @@ def test_sharded_overlapping_walks(k, L, every, P):
     recs = merging_walks(k, L, seed=26 + k, every=every)
     rc, want, nc, _, _, _ = ob.assemble(k, recs)
     assert rc == 0 and len(want) > 4 * len(recs)
+    _dirty_device_memory()
     texts = run_threaded(k, recs, P)
     assert b"".join(texts) == want
