@@ -840,7 +840,7 @@ int kh_assemble_dev(kh_table* t) {
             (rc = t->clen.ensure((ns + 1) * 4)) || (rc = t->stab.ensure(cap2 * 16)) ||
             (rc = t->stab_id.ensure(cap2 * 4)) || (rc = t->seg_jump.ensure((nseg + 1) * 4)) ||
             (rc = t->seg_jsum.ensure((nseg + 1) * 4)) || (rc = t->seg_anchor.ensure(nseg + 1)) ||
-            (rc = t->seg_pend.ensure((ns + 2) * 4)))
+            (rc = t->seg_pend.ensure((ns + 4) * 4)))
             return rc;
         wb.splits = splits;
         wb.n_splits = nsp;
@@ -858,6 +858,14 @@ int kh_assemble_dev(kh_table* t) {
         sb.anchor = t->seg_anchor.as<uint8_t>();
         sb.pend = t->seg_pend.as<uint32_t>();
         sb.long_flag = sb.pend + ns + 1;
+        // deferred splitter segments (k_walk_q): a contig's walker stops at a splitter only past
+        // the walk density's spacing, so contigs shorter than it (C3: all) need no splitter segment
+        // and the splitter walkers are skipped; KH_DEBUG=seg_eager stops at every splitter
+        // (not where the mean contig is longer than the splitter spacing, C2: most walkers stop
+        // anyway and phase 1 would only run after the start walkers instead of beside them)
+        wb.seg_long = sb.pend + ns + 2;  // [0] a contig's walker stopped at a splitter, [1] splitter walkers deferred
+        const bool short_mean = ns && n / ns <= (1ull << kp.split_bits);
+        wb.split_min = (kh::debug_flag("seg_eager") || !short_mean) ? 0u : (1u << kp.split_bits);
         KH_HIP(hipMemsetAsync(wb.seg_next, 0xff, nseg * 4, t->stream));
     }
     unsigned long long* ctr = t->ctr.as<unsigned long long>();
@@ -879,6 +887,10 @@ int kh_assemble_dev(kh_table* t) {
     }
     for (int attempt = 0;; ++attempt) {
         KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
+        if (wb.split_min) {
+            KH_HIP(hipMemsetAsync(wb.seg_long, 0, 8, t->stream));
+            KH_HIP(hipMemsetAsync(wb.contig_len + ns, 0, nsp * 4, t->stream));  // phase 1: not walked yet
+        }
         KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
         // Successor runs of the head records (k_rec_succ). A record read before its successor is
         // resolved still says 0 (the walker probes, as without), so the resolve runs on the side
@@ -908,7 +920,14 @@ int kh_assemble_dev(kh_table* t) {
         if (succ_side) KH_HIP(hipEventRecord(t->ev_conv, t->side));
         // three walker blocks per CU for 16-B slots at load <= 0.6, else two (kh_kernels.hip)
         // (round 5, after the single place() site: 4 / 5 blocks per CU C3 walk 1.40 / 1.43 ms vs 1.16)
-        KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, (kp.W == 2 && t->load <= 0.6) ? -3 : -2, t->stream));
+        const int wgrid = (kp.W == 2 && t->load <= 0.6) ? -3 : -2;
+        KH_HIP(kh::launch_walk(kp, view(t), wb, ctr, stats, wgrid, t->stream));
+        if (wb.split_min && wb.n_splits) {  // the splitter walkers, if some contig was long
+            kh::WalkBuffers wb1 = wb;
+            wb1.phase = 1;
+            KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8, t->stream));
+            KH_HIP(kh::launch_walk(kp, view(t), wb1, ctr, stats, wgrid, t->stream));
+        }
         if (succ_side) KH_HIP(hipStreamWaitEvent(t->stream, t->ev_conv, 0));
         KH_HIP(hipEventRecord(t->ev_wk1, t->stream));
         t->wk_timed = true;

@@ -331,8 +331,22 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
     const KParams p = specialize<KT>(p_in);
     const uint32_t lane = lane_id();
     const uint32_t q = lane & 3, ql = lane & ~3u;
-    const uint64_t n = wb.n_starts + walk_splits(wb);
-    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n};
+    const uint64_t n_all = wb.n_starts + walk_splits(wb);
+    // Deferred splitter segments (wb.split_min): the splitter walkers follow the start walkers in
+    // the queue. A wave that reaches them before any contig has stopped at a splitter (seg_long[0],
+    // read once per reservation) defers them all: it moves the queue head past the end
+    // (atomicMax), sets seg_long[1] and stops taking walkers. Phase 1 then walks the splitter
+    // walkers that were not walked (contig_len still 0), and returns at once unless some contig
+    // stopped at a splitter after all (plain loads: phase 0 wrote the flags in an earlier kernel).
+    // C3 (contigs shorter than the splitter spacing): no splitter walker runs; C5: the long chains
+    // stop early, so the splitter walkers run in phase 0 beside the short contigs as before.
+    if (wb.phase == 1 && !(wb.seg_long[0] && wb.seg_long[1])) return;
+    const uint64_t q_first = wb.phase == 1 ? wb.n_starts : 0;
+    uint64_t n = n_all;  // wave-uniform: the last walker this wave may take (+1)
+    // the flags are read and written at most once per wave (agent-scope accesses pass the per-XCD
+    // L2 and serialise on one address: one per lane cost C3 10 ms)
+    bool long_known = wb.phase == 1;
+    const LaneOut o{wb.contig_len, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, wb.chunk_cap, n_all};
     const bool chains = p.chain && wb.hcap != 0;
     uint64_t bbase = 0, rbase = 0;
     uint32_t bused = WALK_GRAB, rleft = 0;  // rleft: walkers left in the wave's reservation
@@ -355,6 +369,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
     while (true) {
         while (true) {
             const bool need = !active && !done;
+            bool skipped = false;  // phase 1: took a walker phase 0 walked: take another
             const uint64_t m = __ballot(need);
             if (m) {
                 const uint32_t cnt = (uint32_t)__popcll(m);
@@ -370,9 +385,20 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                         if (rleft == 0) {  // reserve WALK_BATCHES batches with one atomic
                             unsigned long long g = 0;
                             if (lane == 0)
-                                g = atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)grab_all);
+                                g = q_first + atomicAdd(&ctr[CT_WALK_NEXT], (unsigned long long)grab_all);
                             rbase = __shfl(g, 0, 64);
                             rleft = grab_all;
+                            // (a reservation past the end, after some wave deferred: nothing to check)
+                            if (wb.split_min && !long_known && rbase + grab_all > wb.n_starts && rbase < n_all) {
+                                long_known = __hip_atomic_load(wb.seg_long, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT) != 0;
+                                if (!long_known) {  // defer every splitter walker to phase 1
+                                    if (lane == 0 && atomicMax(&ctr[CT_WALK_NEXT], (unsigned long long)n_all) < n_all)
+                                        __hip_atomic_store(wb.seg_long + 1, 1u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                                    n = wb.n_starts;
+                                }
+                            }
                         }
                         bbase = rbase;
                         rbase += WALK_GRAB;
@@ -405,7 +431,10 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                         x0 = n0;
                         x1 = n1;
                     }
-                    if (cc < n) {
+                    // phase 1: a splitter walker phase 0 walked (its length is set) is not taken
+                    const bool take = cc < n && (wb.phase == 0 || wb.contig_len[cc] == 0);
+                    skipped = cc < n && !take;
+                    if (take) {
                         c = cc;
                         k = slot_key(x0, x1, p);
                         fwd = ext_fwd(slot_ext(x0));
@@ -416,7 +445,7 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                         entry = chains;
                         resolved = !chains;  // with chains: its own slot tells whether a record covers its run
                         do_place = chains;
-                    } else {
+                    } else if (!skipped) {
                         done = true;
                     }
                 }
@@ -427,13 +456,15 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
                 finish_contig(o, c, steps, chunk, buf);
                 active = false;
             }
-            if (!__any(fin)) break;
+            if (!__any(fin || skipped)) break;
         }
         if (!__any(active)) break;
+        bool stop_long = false;
         if (active && resolved) {
             append_base(o, c, fwd, steps, chunk, buf, ctr, stats);
             k = key_next(k, fwd, p);
-            if (is_splitter(k, p)) {
+            if (is_splitter(k, p) && (c >= wb.n_starts || steps >= wb.split_min)) {
+                stop_long = c < wb.n_starts;  // a long contig: splitter segments are needed
                 finish_contig(o, c, steps, chunk, buf);
                 wb.seg_next[c] = SEG_AT_SPLIT;
                 wb.seg_key[2 * c] = k.hi;
@@ -442,6 +473,10 @@ __global__ __launch_bounds__(BLOCK) void k_walk_q(KParams p_in, const uint64_t* 
             } else {
                 do_place = true;
             }
+        }
+        if (wb.split_min && !long_known && __any(stop_long)) {  // once per wave
+            if (lane == 0) __hip_atomic_store(wb.seg_long, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            long_known = true;
         }
         if (do_place) {
             const Place pl = place(k, p);
@@ -720,10 +755,19 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     const int bpc = grid_blocks < 0 ? -grid_blocks : 2;
     const unsigned grid = (unsigned)hmin((nw + BLOCK - 1) / BLOCK,
                                          (uint64_t)(grid_blocks > 0 ? grid_blocks : bpc * cu_count()));
+    // queue batches per reservation: WALK_BATCHES where every wave gets many reservations, fewer
+    // where a reservation of 8 x 64 walkers would leave most waves idle (the start walkers of a few
+    // long contigs, C2: 12.7K of them, took 25 waves)
+    WalkBuffers w = wb;
+    if (w.batches == 0) {
+        const uint64_t nq = !wb.split_min ? nw : wb.phase == 0 ? wb.n_starts : wb.n_splits;
+        const uint64_t per = nq / ((uint64_t)WALK_GRAB * grid * (BLOCK / 64) * 4);
+        w.batches = (uint32_t)(per < 1 ? 1 : hmin(per, (uint64_t)WALK_BATCHES));
+    }
     if (p.W == 1)
-        with_kt<1>(p.K, [&](auto kt) { k_walk_q<1, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); });
+        with_kt<1>(p.K, [&](auto kt) { k_walk_q<1, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, w, ctr, stats); });
     else
-        with_kt<2>(p.K, [&](auto kt) { k_walk_q<2, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, wb, ctr, stats); });
+        with_kt<2>(p.K, [&](auto kt) { k_walk_q<2, decltype(kt)::value><<<grid, BLOCK, 0, s>>>(p, t.slots, t.cap, w, ctr, stats); });
     return hipGetLastError();
 }
 
@@ -1132,6 +1176,7 @@ __global__ __launch_bounds__(BLOCK) void k_stab_build(KParams p, WalkBuffers wb,
 // lookup per hop on the contig's serial path) measured C3 -0.03 ms but C2 (~80 segments per
 // contig) 0.60 -> 1.00 ms walk bracket (profiles/r05/ab/ab_seg_lazy_link.txt).
 __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
+    if (wb.split_min && !*wb.seg_long) return;  // no walker stopped at a splitter
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
     const uint64_t cap2 = stab_cap(wb, sb.cap2);
     // most segments end at 'F' (C5: 21M of 21.8M): a thread tests 4 with one 16-B load (seg_next
@@ -1343,13 +1388,18 @@ __global__ __launch_bounds__(BLOCK) void k_write_chunks_seg(int K, const uint64_
                                                             const unsigned long long* nsp_dev, uint64_t nsp,
                                                             const uint32_t* seg_len, const uint32_t* seg_contig,
                                                             const uint32_t* seg_off, const uint64_t* off,
-                                                            char* out, uint64_t cap, uint64_t ch_begin = 0) {
-    const uint64_t nseg = n_starts + (nsp_dev ? (uint64_t)*nsp_dev : nsp);
+                                                            char* out, uint64_t cap, uint64_t ch_begin,
+                                                            const uint32_t* seg_long) {
+    const uint64_t ns_w = nsp_dev ? (uint64_t)*nsp_dev : nsp;
+    const uint64_t nseg = n_starts + ns_w;
     const uint64_t nchunks = min(nseg + (uint64_t)ctr[CT_CHUNK_NEXT], chunk_cap);
-    const uint64_t nt = nchunks * WC_TPC;
+    // no contig reached a splitter segment (deferred segments, k_walk_q): their chunks are skipped
+    const uint64_t gap = (seg_long && !*seg_long && ch_begin <= n_starts) ? ns_w : 0;
+    const uint64_t nt = (nchunks - min(gap, nchunks)) * WC_TPC;
     for (uint64_t t = ch_begin * WC_TPC + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < nt;
          t += (uint64_t)gridDim.x * BLOCK) {
-        const uint64_t ch = t / WC_TPC;
+        uint64_t ch = t / WC_TPC;
+        if (ch >= n_starts) ch += gap;
         const uint32_t q = (uint32_t)(t % WC_TPC);
         const uint32_t g = ch < nseg ? (uint32_t)ch : owner[ch];
         const bool own = g < n_starts;  // a contig's start segment: contig g, offset 0
@@ -1390,7 +1440,7 @@ hipError_t launch_materialize_seg(const KParams& p, const WalkBuffers& wb, const
     const unsigned gc = (unsigned)hmin(((wb.chunk_cap - min(cb, wb.chunk_cap)) * WC_TPC + BLOCK - 1) / BLOCK + 1, 8192);
     k_write_chunks_seg<<<gc, BLOCK, 0, s>>>(p.K, wb.chunk_data, wb.chunk_owner, wb.chunk_seq, ctr, wb.chunk_cap,
                                             nc, wb.n_splits_dev, wb.n_splits, wb.contig_len, sb.seg_contig,
-                                            sb.seg_off, offsets, out, cap, cb);
+                                            sb.seg_off, offsets, out, cap, cb, wb.split_min ? wb.seg_long : nullptr);
     return hipGetLastError();
 }
 

@@ -96,6 +96,15 @@ struct WalkBuffers {
     // work-queue batches a wave reserves per atomic (0: WALK_BATCHES); kh_assemble_dev takes 32
     // for short contigs (C5: 21M contigs of ~9 k-mers), where the queue's one counter is the limit
     uint32_t batches = 0;
+    // Deferred splitter segments (split_min > 0): a contig's walker stops before a splitter only
+    // once it has appended split_min bases, and then sets seg_long[0]; splitter walkers reached in
+    // the queue before that are deferred (seg_long[1]) to a second launch (phase 1), which walks
+    // them only if some contig did stop at a splitter (k_walk_q). Contigs shorter than split_min
+    // (C3: all) then need no splitter segment at all. The splitter segments' contig_len must be 0
+    // before phase 0 (phase 1 walks those still 0).
+    uint32_t split_min = 0;
+    uint32_t* seg_long = nullptr;  // 2 words
+    uint32_t phase = 0;
 };
 
 // Persistent per-lane walker (single GPU): every lane walks whole contigs, pulling start k-mers

@@ -107,6 +107,18 @@ def merging_walks(k, L, seed, every=1):
     return kh.pack_text(k, merging_walks_text(k, L, seed, every))
 
 
+def dirty_device_memory(gib=4):
+    """Fill free device memory with 0xFF bytes and hand it back to the driver, so buffers the next
+    step allocates start as garbage (a fresh box hands out zeros, which hid round 6's store-overflow
+    bug: text records past the store's end read as rank 255)."""
+    import torch
+    t = torch.empty(gib << 30, dtype=torch.uint8, device="cuda")
+    t.fill_(0xFF)
+    torch.cuda.synchronize()
+    del t
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("k,L,every", [(19, 3000, 1), (51, 2000, 3)])
 def test_overlapping_walks_redo(k, L, every):
     """Walks that overlap (malformed input) pass the pre-walk text bound and exhaust the walker
@@ -115,6 +127,7 @@ def test_overlapping_walks_redo(k, L, every):
     recs = merging_walks(k, L, seed=7 + k, every=every)
     rc, want, nc, _, _, _ = ob.assemble(k, recs)
     assert rc == 0 and len(want) > 4 * len(recs)
+    dirty_device_memory()
     _, got, got_nc = run(k, recs)
     assert got_nc == nc and got == want
 
@@ -153,6 +166,7 @@ def test_walk_into_start_that_passes_split_test(monkeypatch, k):
     recs = kh.pack_text(k, "".join(lines[i] for i in order).encode())
     rc, want, nc, _, _, _ = ob.assemble(k, recs)
     assert rc == 0 and nc == 7
+    dirty_device_memory()
     _, got, got_nc = run(k, recs)
     assert got_nc == nc and got == want
 
@@ -448,6 +462,33 @@ def test_gpu_skewed_c5(k, n, n_long, long_len):
     g = kh.SyntheticKmers(k, n, 2, 16, 0, seed=k + n_long, n_long=n_long, long_len=long_len, front_starts=True)
     t, got, nc = run(k, g.records())
     assert nc == g.num_contigs and got == g.truth()
+
+
+@pytest.mark.parametrize("k,long_last", [(51, True), (51, False), (19, True)])
+def test_deferred_splitter_segments(monkeypatch, k, long_last):
+    """Deferred splitter segments (k_walk_q, wb.split_min): contigs mostly shorter than the splitter
+    spacing, so the walkers reaching the splitter walkers in the queue defer them, plus a few long
+    chains that do stop at splitters. long_last puts the long chains' start records after every
+    other record (their walkers start last: the splitter walkers are deferred first and walked by
+    the second launch); otherwise they sit anywhere among the starts. Byte-equal to the oracle, and
+    to the eager walk (KH_DEBUG=seg_eager: every walker stops at every walked splitter)."""
+    # contigs of 2-16 k-mers (mean 9: below the walk's splitter spacing, 16 at this size)
+    g = kh.SyntheticKmers(k, 2_000_000, 2, 16, 0, seed=61 + k, n_long=3, long_len=60_000)
+    recs = g.records()
+    if long_last:
+        P = kh.packed_size(k)
+        heads = {kh.pack_kmer(k, line[:k]).tobytes() for line in g.truth().split(b"\n") if len(line) > 10_000}
+        rows = recs[:, :P]
+        is_long = np.array([rows[i].tobytes() in heads for i in range(len(recs))])
+        assert is_long.sum() == 3
+        recs = np.concatenate([recs[~is_long], recs[is_long]])
+    rc, want, nc, _, _, _ = ob.assemble(k, recs)
+    assert rc == 0
+    _, got, got_nc = run(k, recs)
+    assert got_nc == nc and got == want
+    monkeypatch.setenv("KH_DEBUG", "seg_eager")
+    _, got2, _ = run(k, recs)
+    assert got2 == want
 
 
 # ---- C5 hot-bucket half: many k-mers sharing a few minimizer windows (BASELINE configs[4]) -------
