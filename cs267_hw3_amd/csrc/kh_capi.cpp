@@ -840,7 +840,7 @@ int kh_assemble_dev(kh_table* t) {
             (rc = t->clen.ensure((ns + 1) * 4)) || (rc = t->stab.ensure(cap2 * 16)) ||
             (rc = t->stab_id.ensure(cap2 * 4)) || (rc = t->seg_jump.ensure((nseg + 1) * 4)) ||
             (rc = t->seg_jsum.ensure((nseg + 1) * 4)) || (rc = t->seg_anchor.ensure(nseg + 1)) ||
-            (rc = t->seg_pend.ensure((ns + 4) * 4)))
+            (rc = t->seg_pend.ensure((ns + 6) * 4)))
             return rc;
         wb.splits = splits;
         wb.n_splits = nsp;
@@ -888,7 +888,7 @@ int kh_assemble_dev(kh_table* t) {
     for (int attempt = 0;; ++attempt) {
         KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
         if (wb.split_min) {
-            KH_HIP(hipMemsetAsync(wb.seg_long, 0, 8, t->stream));
+            KH_HIP(hipMemsetAsync(wb.seg_long, 0, 16, t->stream));
             KH_HIP(hipMemsetAsync(wb.contig_len + ns, 0, nsp * 4, t->stream));  // phase 1: not walked yet
         }
         KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
@@ -929,6 +929,8 @@ int kh_assemble_dev(kh_table* t) {
             KH_HIP(kh::launch_walk(kp, view(t), wb1, ctr, stats, wgrid, t->stream));
         }
         if (succ_side) KH_HIP(hipStreamWaitEvent(t->stream, t->ev_conv, 0));
+        // the splitter table, if the walk found it needed and it was not built beside the walk
+        if (kp.split_bits && wb.split_min) KH_HIP(kh::launch_seg_table(kp, wb, sb, t->stream, true));
         KH_HIP(hipEventRecord(t->ev_wk1, t->stream));
         t->wk_timed = true;
         if (kp.split_bits) KH_HIP(kh::launch_segments(kp, wb, sb, stats, t->stream));

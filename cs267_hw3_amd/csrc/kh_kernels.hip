@@ -1144,13 +1144,27 @@ hipError_t launch_materialize(const KParams& p, const WalkBuffers& wb, uint64_t*
 __device__ __forceinline__ uint64_t stab_cap(const WalkBuffers& wb, uint64_t cap2) {
     return min(cap2, 2 * walk_splits(wb) + 64);
 }
+// Deferred splitter segments (wb.split_min): the table is needed only if some contig stopped at a
+// splitter (seg_long[0]). Beside the walk it is built when that is already known (C5: the long
+// chains stop early), else after the walk if it turned out so (seg_long[2]: built beside; [3]: this
+// launch builds it). C3 never builds it (it was the critical path of the walk phase: resolve 0.98
+// + table 0.09 ms beside a 0.99-ms walk).
+__global__ void k_stab_gate(uint32_t* seg_long, int after) {
+    if (threadIdx.x || blockIdx.x) return;
+    const uint32_t f = __hip_atomic_load(seg_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t go = after ? (f && !seg_long[2]) : f;
+    if (!after) seg_long[2] = go;
+    seg_long[3] = go;
+}
 __global__ __launch_bounds__(BLOCK) void k_stab_init(WalkBuffers wb, uint64_t* stab, uint64_t cap2_max) {
+    if (wb.split_min && !wb.seg_long[3]) return;
     const uint64_t cap2 = stab_cap(wb, cap2_max);
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < cap2; i += (uint64_t)gridDim.x * BLOCK)
         stab[2 * i] = EMPTY;
 }
 __global__ __launch_bounds__(BLOCK) void k_stab_build(KParams p, WalkBuffers wb, uint64_t* stab, uint32_t* id,
                                                       uint64_t cap2_max) {
+    if (wb.split_min && !wb.seg_long[3]) return;
     const uint64_t* splits = wb.splits;
     const uint64_t nsp = walk_splits(wb);
     const uint64_t cap2 = stab_cap(wb, cap2_max);
@@ -1344,13 +1358,17 @@ hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64
 
 // The splitter table (key -> segment id) and the segment owners' reset: they read only the walked
 // splitter list, so they run before or beside the walk (on the resolve's side stream).
-hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb, hipStream_t s) {
+hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb, hipStream_t s,
+                            bool after) {
     const uint64_t nseg = wb.n_starts + wb.n_splits;
     if (nseg == 0) return hipSuccess;
+    if (wb.split_min) k_stab_gate<<<1, 64, 0, s>>>(wb.seg_long, after ? 1 : 0);
+    else if (after) return hipSuccess;  // built beside the walk
     k_stab_init<<<(unsigned)hmin((sb.cap2 + BLOCK - 1) / BLOCK, 2048), BLOCK, 0, s>>>(wb, sb.stab, sb.cap2);
     hipError_t e;
     // splitter segments' contigs (a start segment's is itself, never stored)
-    if (wb.n_splits && (e = hipMemsetAsync(sb.seg_contig + wb.n_starts, 0xff, wb.n_splits * 4, s)) != hipSuccess)
+    if (!after && wb.n_splits &&
+        (e = hipMemsetAsync(sb.seg_contig + wb.n_starts, 0xff, wb.n_splits * 4, s)) != hipSuccess)
         return e;
     if (wb.n_splits)
         k_stab_build<<<(unsigned)hmin((wb.n_splits + BLOCK - 1) / BLOCK, 4096), BLOCK, 0, s>>>(

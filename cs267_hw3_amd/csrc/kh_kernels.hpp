@@ -103,7 +103,7 @@ struct WalkBuffers {
     // (C3: all) then need no splitter segment at all. The splitter segments' contig_len must be 0
     // before phase 0 (phase 1 walks those still 0).
     uint32_t split_min = 0;
-    uint32_t* seg_long = nullptr;  // 2 words
+    uint32_t* seg_long = nullptr;  // 4 words (k_walk_q, k_stab_gate)
     uint32_t phase = 0;
 };
 
@@ -139,7 +139,10 @@ struct SegBuffers {
 // splits with (hash & (2^bits - 1)) == 0 -> out (count to *count)
 hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64_t n, int bits, uint64_t* off,
                                 uint64_t* scratch, uint64_t* out, unsigned long long* count, hipStream_t s);
-hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb, hipStream_t s);
+// after: the second launch of deferred splitter segments (builds the table only if the first,
+// beside the walk, did not and some contig stopped at a splitter)
+hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb, hipStream_t s,
+                            bool after = false);
 hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
                            unsigned long long* stats, hipStream_t s);
 // phases: MAT_SCAN = offsets + ctr[CT_OUT_BYTES]; MAT_WRITE = the text (out must hold the
