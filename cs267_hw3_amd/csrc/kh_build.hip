@@ -2050,8 +2050,12 @@ hipError_t launch_hot_prepass(const KParams& p, const uint8_t* recs, const uint6
                               uint64_t cap, uint32_t* rcnt, uint32_t* hot, uint32_t* hot_list,
                               unsigned long long* ctr, hipStream_t s, uint64_t total) {
     hipError_t e;
-    if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 16, s)) != hipSuccess) return e;
+    {
+        FillSet f;
+        f.add(rcnt, (uint64_t)nreg(p) * 4, 0);
+        f.add(ctr + CT_HOT, 16, 0);
+        if ((e = launch_fill(f, s)) != hipSuccess) return e;
+    }
     if (n) {
         const unsigned grid = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
         if (p.W == 2) {
@@ -2118,7 +2122,11 @@ static hipError_t sample_mark(const KParams& p, uint64_t cap, uint64_t n, uint32
     if ((e = hipMemsetAsync(ctr + CT_HOT, 0, 16, s)) != hipSuccess) return e;  // CT_HOT, CT_HOTNEW
     k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot, B.hot_list, ctr, 1, 0,
                                                      balanced_T(p, cap, n));
-    return hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s);
+    // the region counts for level 2 (sample_level2, always next) and its counter
+    FillSet f;
+    f.add(B.rcnt, (uint64_t)nreg(p) * 4, 0);
+    f.add(ctr + CT_HOT2, 8, 0);
+    return launch_fill(f, s);
 }
 
 // Level 2 of the bitmap (kh_codec.hpp remap_region): a 1-in-256 sample of the batch counted by its
@@ -2172,7 +2180,7 @@ static hipError_t sample_level2(const KParams& p, const uint8_t* recs, const uin
              return hipGetLastError();
          })) != hipSuccess)
         return e;
-    if ((e = hipMemsetAsync(ctr + CT_HOT2, 0, 8, s)) != hipSuccess) return e;
+    // (ctr[CT_HOT2] was zeroed by sample_mark)
     k_hot_mark<<<(nreg(p) + 255) / 256, 256, 0, s>>>(q, cap, RC, 0, 8, B.rcnt, B.hot + HOT_WORDS, B.hot_list, ctr, 1, 0,
                                                      balanced_T(p, cap, total), CT_HOT2);
     return hipMemsetAsync(B.rcnt, 0, (size_t)nreg(p) * 4, s);
@@ -2196,9 +2204,13 @@ static hipError_t part_insert(const KParams& p, const uint8_t* recs, const uint6
     const uint32_t CAP1 = part_win1_cap(n), RC = part_region_cap(p, n);
     uint32_t* wcnt = B.wcnt;
     uint32_t* rcnt = B.rcnt;
-    if ((e = hipMemsetAsync(ctr + CT_OVF, 0, 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(wcnt, 0, (size_t)NW1 * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(rcnt, 0, (size_t)nreg(p) * 4, s)) != hipSuccess) return e;
+    {
+        FillSet f;
+        f.add(ctr + CT_OVF, 8, 0);
+        f.add(wcnt, (uint64_t)NW1 * 4, 0);
+        f.add(rcnt, (uint64_t)nreg(p) * 4, 0);
+        if ((e = launch_fill(f, s)) != hipSuccess) return e;
+    }
     // records of a compiled shape (k=51 / k=19 packed sizes): pass 1 reads them itself, no
     // record -> word copy (other shapes: the convert pass + pass 1 on its words)
     const bool rec_pass = REC && rec_pass_ok<W>(p);

@@ -499,10 +499,12 @@ int kh_clear(kh_table* t) {
     if (int rc = set_device(t)) return rc;
     if (int rc = join_succ(t)) return rc;
     t->slots_stale = true;
-    KH_HIP(hipMemsetAsync(t->ctr.p, 0, kh::CT_NUM * 8, t->stream));
-    KH_HIP(hipMemsetAsync(t->stats.p, 0, kh::ST_NUM * 8, t->stream));
-    KH_HIP(hipMemsetAsync(t->hot.p, 0, 2 * kh::HOT_WORDS * 4, t->stream));  // placement by minimizer again
-    KH_HIP(hipMemsetAsync(t->route_spl.p, 0, kh::MAX_RANKS * 8, t->stream));
+    kh::FillSet f;
+    f.add(t->ctr.p, kh::CT_NUM * 8, 0);
+    f.add(t->stats.p, kh::ST_NUM * 8, 0);
+    f.add(t->hot.p, 2 * kh::HOT_WORDS * 4, 0);  // placement by minimizer again
+    f.add(t->route_spl.p, kh::MAX_RANKS * 8, 0);
+    KH_HIP(kh::launch_fill(f, t->stream));
     t->n_inserted = 0;
     t->assembled = false;
     t->split_ok = true;
@@ -866,7 +868,6 @@ int kh_assemble_dev(kh_table* t) {
         wb.seg_long = sb.pend + ns + 2;  // [0] a contig's walker stopped at a splitter, [1] splitter walkers deferred
         const bool short_mean = ns && n / ns <= (1ull << kp.split_bits);
         wb.split_min = (kh::debug_flag("seg_eager") || !short_mean) ? 0u : (1u << kp.split_bits);
-        KH_HIP(hipMemsetAsync(wb.seg_next, 0xff, nseg * 4, t->stream));
     }
     unsigned long long* ctr = t->ctr.as<unsigned long long>();
     unsigned long long* stats = t->stats.as<unsigned long long>();
@@ -886,10 +887,15 @@ int kh_assemble_dev(kh_table* t) {
         wb.text_cap = t->text.bytes;
     }
     for (int attempt = 0;; ++attempt) {
-        KH_HIP(hipMemsetAsync(ctr + kh::CT_WALK_NEXT, 0, 8 * 3, t->stream));  // WALK, CHUNK, OUT
-        if (wb.split_min) {
-            KH_HIP(hipMemsetAsync(wb.seg_long, 0, 16, t->stream));
-            KH_HIP(hipMemsetAsync(wb.contig_len + ns, 0, nsp * 4, t->stream));  // phase 1: not walked yet
+        {
+            kh::FillSet f;
+            f.add(ctr + kh::CT_WALK_NEXT, 8 * 3, 0);  // WALK, CHUNK, OUT
+            if (kp.split_bits) f.add(wb.seg_next, nseg * 4, 0xff);
+            if (wb.split_min) {
+                f.add(wb.seg_long, 16, 0);
+                f.add(wb.contig_len + ns, nsp * 4, 0);  // phase 1: not walked yet
+            }
+            KH_HIP(kh::launch_fill(f, t->stream));
         }
         KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
         // Successor runs of the head records (k_rec_succ). A record read before its successor is
@@ -957,8 +963,7 @@ int kh_assemble_dev(kh_table* t) {
             wb.chunk_owner = t->chunk_owner.as<uint32_t>();
             wb.chunk_seq = t->chunk_seq.as<uint32_t>();
             KH_HIP(hipMemsetAsync(stats + kh::ST_CHUNK_OVF, 0, 8, t->stream));
-            if (kp.split_bits) KH_HIP(hipMemsetAsync(wb.seg_next, 0xff, nseg * 4, t->stream));
-            continue;
+            continue;  // (seg_next is reset at the top of the attempt)
         }
         if ((rc = t->text.ensure(hv[1] + 64))) return rc;
         break;

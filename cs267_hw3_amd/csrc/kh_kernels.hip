@@ -771,6 +771,27 @@ hipError_t launch_walk(const KParams& p, TableView t, const WalkBuffers& wb, uns
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(BLOCK) void k_fill(FillSet f) {
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    for (int j = 0; j < f.n; ++j) {
+        uint32_t* q = reinterpret_cast<uint32_t*>(f.p[j]);
+        const uint64_t words = f.bytes[j] / 4;
+        const uint32_t v = f.byte[j] * 0x01010101u;
+        for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < words; i += stride) q[i] = v;
+    }
+}
+
+hipError_t launch_fill(const FillSet& f, hipStream_t s) {
+    uint64_t most = 0;
+    for (int j = 0; j < f.n; ++j) {
+        if (f.bytes[j] % 4 || (reinterpret_cast<uintptr_t>(f.p[j]) & 3)) return hipErrorInvalidValue;
+        most = f.bytes[j] > most ? f.bytes[j] : most;
+    }
+    if (!most) return hipSuccess;
+    k_fill<<<(unsigned)hmin((most / 4 + BLOCK - 1) / BLOCK, 2048), BLOCK, 0, s>>>(f);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------------
 // Materialisation: contig c occupies bytes [off[c], off[c] + K + len[c]) =
 //   K chars of the start k-mer, len[c]-1 appended forward bases, '\n'.

@@ -41,6 +41,23 @@ enum CtrIdx : int {
     CT_NUM = 12
 };
 
+// Several fills in one launch (each hipMemsetAsync is a ~5 us dispatch of its own): up to
+// FILL_MAX buffers of whole 4-byte words, each set to a byte value. Null / empty entries are skipped.
+static constexpr int FILL_MAX = 6;
+struct FillSet {
+    void* p[FILL_MAX] = {};
+    uint64_t bytes[FILL_MAX] = {};
+    uint32_t byte[FILL_MAX] = {};
+    int n = 0;
+    void add(void* ptr, uint64_t nbytes, uint32_t value) {
+        p[n] = ptr;
+        bytes[n] = nbytes;
+        byte[n] = value & 0xFFu;
+        ++n;
+    }
+};
+hipError_t launch_fill(const FillSet& f, hipStream_t s);
+
 // Chunk of appended bases: 8 words x 32 bases (2 bits each) = 256 bases.
 static constexpr int CHUNK_WORDS = 8;
 static constexpr uint32_t WMIN_ERR = 0xFFFFFFFFu;  // origin_lines (kh_capi.cpp): no memory
