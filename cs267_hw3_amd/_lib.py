@@ -104,6 +104,8 @@ _SIGS = {
     "kh_mwalk_segments": (ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "kh_mwalk_flags_dev": (ctypes.c_int, [c_vp, c_vp]),
     "kh_mwalk_redo": (ctypes.c_int, [c_vp, c_u64]),
+    "kh_mwalk_short": (ctypes.c_int, [c_vp, c_u64, c_u64, ctypes.POINTER(ctypes.c_int)]),
+    "kh_mwalk_abandon": (ctypes.c_int, [c_vp]),
     "kh_mwalk_link_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp]),
     "kh_mwalk_pred_dev": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_u64]),
     "kh_mwalk_resolve_dev": (ctypes.c_int, [c_vp, c_vp, c_u64]),

@@ -147,6 +147,8 @@ struct kh_table {
     uint64_t mw_store_n = 0;   // text records in mw_store (valid when mw_store_known)
     uint64_t mw_store_bound = 0;  // upper bound of the store's records (its device count: mw_misc[2])
     bool mw_seg_off = false;      // kh_mwalk_redo: the next walk runs without splitter segments
+    uint64_t mw_soft_next = 0;    // kh_mwalk_short: the next walk's soft step limit (0: none)
+    uint64_t mw_soft = 0;         // this walk's
     uint64_t mw_store_min = 0;    // ... with a text store of at least this many records
     bool mw_store_known = true;
     uint32_t mw_P = 0, mw_rank = 0;
@@ -1490,6 +1492,8 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     if (store_cap < t->mw_store_min) store_cap = t->mw_store_min;  // a redo sized by the last attempt
     t->mw_seg_off = false;
     t->mw_store_min = 0;
+    t->mw_soft = t->mw_soft_next;
+    t->mw_soft_next = 0;
     if ((rc = t->mw_misc.ensure(64)) || (rc = t->mw_store.ensure(store_cap * 16)))
         return rc;
     t->ms_ns = ns;
@@ -1518,7 +1522,7 @@ int kh_mwalk_begin(kh_table* t, int nranks, int rank, uint64_t total_kmers, uint
     t->mw_store_bound = store_cap;
     t->mw_store_known = false;
     t->mw_cur = 0;
-    KH_HIP(hipMemsetAsync(mw_word(t, 2), 0, 8 * 4, t->stream));  // store count, walkers, carries
+    KH_HIP(hipMemsetAsync(mw_word(t, 2), 0, 8 * 6, t->stream));  // store count, walkers, carries, long walks
     KH_HIP(hipEventRecord(t->ev_walk0, t->stream));
     t->wk_timed = false;
     // chain records: the first round's walkers read the start and splitter lists themselves and
@@ -1590,6 +1594,8 @@ int kh_mwalk_round_dev(kh_table* t, const void* in_slots, uint64_t in_cap, void*
     mw.headrec = t->headrec.as<uint64_t>();
     mw.hcap = t->headrec.p ? t->hcap : 0u;
     mw.max_steps = t->rw_total;
+    mw.soft_steps = t->mw_soft;
+    mw.long_ctr = mw_word(t, 6);
     mw.in = src;
     mw.starts = t->starts.as<uint64_t>();
     mw.splits = t->splits.as<uint64_t>();
@@ -1639,7 +1645,32 @@ int kh_mwalk_flags_dev(kh_table* t, void* dev_out) {
     if (!dev_out) return fail(KH_ERR_ARG, "null output");
     if (int rc = set_device(t)) return rc;
     KH_HIP(kh::launch_mw_flags(t->stats.as<unsigned long long>() + kh::ST_CHUNK_OVF, mw_word(t, 2), (uint64_t*)dev_out,
-                               t->stream));
+                               t->stream, t->mw_soft ? mw_word(t, 6) : nullptr));
+    return KH_OK;
+}
+
+int kh_mwalk_short(kh_table* t, uint64_t total_kmers, uint64_t total_starts, int* armed) {
+    if (!t || !armed) return fail(KH_ERR_ARG, "null argument");
+    *armed = 0;
+    // splitter segments cut the rounds of long contigs; where the mean contig (every rank's k-mers
+    // over every rank's starts) is shorter than the splitter spacing (C3: 104 < 256) the walk goes
+    // without them first, and a walker past 4 spacings ends it (the hosts then walk segmented)
+    if (!mseg_enabled(t) || !t->words_split || t->mw_seg_off || !total_starts) return KH_OK;
+    const int sb = mseg_params(t).split_bits;
+    if (sb <= 0 || total_kmers / total_starts > (1ull << sb)) return KH_OK;
+    t->mw_seg_off = true;
+    t->mw_soft_next = 4ull << sb;
+    *armed = 1;
+    return KH_OK;
+}
+
+int kh_mwalk_abandon(kh_table* t) {
+    if (!t || !t->mw_live) return fail(KH_ERR_STATE, "kh_mwalk_begin first");
+    if (int rc = set_device(t)) return rc;
+    if (int rc = join_succ(t)) return rc;
+    KH_HIP(hipMemsetAsync(t->stats.as<unsigned long long>() + kh::ST_CHUNK_OVF, 0, 8, t->stream));
+    t->mw_live = false;
+    t->assembled = false;
     return KH_OK;
 }
 

@@ -209,6 +209,10 @@ struct MWalkRound {
     uint8_t* nrec;        // n_in
     const uint64_t* headrec = nullptr;  // chain head records of this shard's build (hcap 0 = none)
     uint32_t hcap = 0;
+    // short walk (kh_mwalk_short): a walker past soft_steps bases ends, counted in *long_ctr (the
+    // hosts then walk again with splitter segments)
+    uint64_t soft_steps = 0;
+    unsigned long long* long_ctr = nullptr;
 };
 
 // ---- splitter segments of the migrating walk (kh_mseg.hip) ----------------------------------
@@ -303,7 +307,7 @@ hipError_t launch_mw_group_text(const uint64_t* recs, uint64_t n, uint32_t P, ui
                                 const unsigned long long* n_dev = nullptr);
 // *fin != want (+ *want_dev) -> stats[ST_MISSING] (walkers that never came home)
 hipError_t launch_mw_flags(const unsigned long long* ovf, const unsigned long long* store_n, uint64_t* out,
-                           hipStream_t s);
+                           hipStream_t s, const unsigned long long* long_ctr = nullptr);
 hipError_t launch_fin_check(const unsigned long long* fin, uint64_t want, const unsigned long long* want_dev,
                             uint64_t want_max, unsigned long long* stats, hipStream_t s);
 hipError_t launch_mw_lens(const uint64_t* recs, uint64_t n, uint64_t nc, uint32_t* len,

@@ -129,6 +129,9 @@ __global__ __launch_bounds__(BLOCK) void k_mw_run(KParams p_in, const uint64_t* 
             if (st > 3) {
                 if (st != EXT_F) atomicAdd(&stats[ST_BAD_EXT], 1ull);
                 fin = true;
+            } else if (mw.soft_steps && steps > mw.soft_steps) {  // a long contig: walk again segmented
+                atomicAdd(mw.long_ctr, 1ull);
+                fin = true;
             } else if (steps > mw.max_steps) {
                 atomicAdd(&stats[ST_CYCLE], 1ull);
                 fin = true;
@@ -610,14 +613,16 @@ hipError_t launch_slot_round(const SlotRound& r, uint64_t* hist, uint64_t* off, 
 }
 
 // [walks' overflow / overlap reports (ST_CHUNK_OVF), text records the store needed]
-__global__ void k_mw_flags(const unsigned long long* ovf, const unsigned long long* store_n, uint64_t* out) {
-    out[0] = *ovf;
+// out[0]: overlap / overflow reports, + 2^40 when a short walk met a long contig
+__global__ void k_mw_flags(const unsigned long long* ovf, const unsigned long long* store_n, uint64_t* out,
+                           const unsigned long long* long_ctr) {
+    out[0] = *ovf + ((long_ctr && *long_ctr) ? (1ull << 40) : 0ull);
     out[1] = *store_n;
 }
 
 hipError_t launch_mw_flags(const unsigned long long* ovf, const unsigned long long* store_n, uint64_t* out,
-                           hipStream_t s) {
-    k_mw_flags<<<1, 1, 0, s>>>(ovf, store_n, out);
+                           hipStream_t s, const unsigned long long* long_ctr) {
+    k_mw_flags<<<1, 1, 0, s>>>(ovf, store_n, out, long_ctr);
     return hipGetLastError();
 }
 

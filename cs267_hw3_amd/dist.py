@@ -449,6 +449,18 @@ class GpuShard:
     def mw_redo(self, store_records):
         check(self.L.kh_mwalk_redo(self.h, int(store_records)))
 
+    def mw_short(self, total_kmers, total_starts):
+        """Arm the next walk as a short walk (no splitter segments, long contigs reported) where the
+        mean contig is shorter than the splitter spacing; True when armed."""
+        if not hasattr(self.L, "kh_mwalk_short"):
+            return False
+        armed = ctypes.c_int(0)
+        check(self.L.kh_mwalk_short(self.h, int(total_kmers), int(total_starts), ctypes.byref(armed)))
+        return bool(armed.value)
+
+    def mw_abandon(self):
+        check(self.L.kh_mwalk_abandon(self.h))
+
     # splitter segments of the migrating walk (kh_mseg.hip)
     LINK_WORDS = _lib.LINK_WORDS
     PRED_WORDS = _lib.PRED_WORDS
@@ -793,9 +805,34 @@ class DistributedKmerHashMap:
 
     def assemble(self, total_kmers):
         """Walk this rank's start k-mers (collective); returns the number of rounds. Walks that
-        overlap (malformed input) are redone unsegmented (see _redo)."""
+        overlap (malformed input) are redone unsegmented (see _redo).
+
+        Short walk first (round 6): splitter segments bound the rounds of long contigs (C5's 10^6-k-mer
+        chains), but where contigs are short (C3: <= 200 k-mers) they add a walker per splitter and
+        the link / pointer-jumping / retag phase for nothing. Where every rank's mean contig is
+        shorter than the splitter spacing the walk goes without segments first; a walker past 4
+        spacings ends it (reported with the text count exchange) and every rank walks again,
+        segmented, as it then does for the rest of this input's steps."""
         self._seg_off = False
+        sh = self.shard
+        if self._short_key != (self._walkers, total_kmers):  # another input: try short again
+            self._short_key, self._needs_seg = (self._walkers, total_kmers), False
+        if not self._needs_seg and hasattr(sh, "mw_short") and sh.mw_short(total_kmers, self._starts_all):
+            saved = self._splitters, self._walkers
+            self._splitters, self._walkers = 0, self._starts_all
+            self._seg_off = True
+            try:
+                r = self._assemble_migrate(total_kmers, short=True)
+            finally:
+                self._splitters, self._walkers = saved
+                self._seg_off = False
+            if r is not None:
+                return r
+            self._needs_seg = True
         return self._assemble_migrate(total_kmers)
+
+    _short_key = None
+    _needs_seg = False
 
     REDO_MAX = 2  # unsegmented with the default store, then with the store the last attempt needed
 
@@ -853,7 +890,7 @@ class DistributedKmerHashMap:
 
     SLOT_CAP_MAX = 1 << 40  # tests: tiny slots (messages held back), set on the class
 
-    def _assemble_migrate(self, total_kmers, attempt=0):
+    def _assemble_migrate(self, total_kmers, attempt=0, short=False):
         """Walkers move to the rank owning their next k-mer (minimizer sharding keeps runs of
         consecutive k-mers on one rank). A round = local walk -> one all-to-all of fixed-size
         slots: no host read per round; the host reads the global in-flight count only at checks
@@ -944,6 +981,9 @@ class DistributedKmerHashMap:
         # segmented ones with the retag exchange (_segments_end), after the segment links
         flag = None if segmented else self._flag()
         send_splits, recv_splits, _, gmax, over = self._exchange_counts(counts, flag)
+        if short and flag is not None and any(int(x) >> 40 for x in over):
+            sh.mw_abandon()  # a long contig somewhere: every rank walks again, segmented
+            return None
         if flag is not None and any(int(x) for x in over):
             return self._redo(total_kmers, attempt)
         r = sum(recv_splits)

@@ -225,6 +225,14 @@ int kh_mwalk_segments(kh_table* t, uint64_t* n_splitter_segments);
  * end, as kmer_hash.cpp:41-53 does) and with a store of at least store_records records. */
 int kh_mwalk_flags_dev(kh_table* t, void* dev_out2);
 int kh_mwalk_redo(kh_table* t, uint64_t store_records);
+/* Short walk first (round 6): splitter segments only pay for long contigs. Called before
+ * kh_mwalk_begin with every rank's k-mer and start counts: where the mean contig is shorter than
+ * the splitter spacing, *armed = 1 and the next walk runs without splitter segments; a walker that
+ * passes 4 spacings ends and adds 2^40 to the first word kh_mwalk_flags_dev reports. When any rank
+ * reports it, every rank calls kh_mwalk_abandon and walks again from kh_mwalk_begin, segmented
+ * (hosts keep walking segmented on the same input). */
+int kh_mwalk_short(kh_table* t, uint64_t total_kmers, uint64_t total_starts, int* armed);
+int kh_mwalk_abandon(kh_table* t);
 int kh_mwalk_link_dev(kh_table* t, const void* dev_recs, uint64_t n, void* dev_links_out, void* dev_counts_out);
 int kh_mwalk_pred_dev(kh_table* t, const void* dev_links, uint64_t m, void* dev_preds_out, uint64_t stride);
 int kh_mwalk_resolve_dev(kh_table* t, const void* dev_all_preds, uint64_t stride);
