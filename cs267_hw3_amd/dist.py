@@ -1136,6 +1136,7 @@ def run_threaded(k, recs, nranks, device=0, info=None, insert_chunks=None, shard
                     info.setdefault("stats", {})[r] = shard.stats()
                     info.setdefault("syncs", {})[r] = syncs
                     info.setdefault("checks", {})[r] = dm.checks
+                    info.setdefault("segmented", {})[r] = dm._needs_seg  # the short walk met a long contig
                     # the counts tools/mem_model.py sizes a rank's buffers from
                     info.setdefault("counts", {})[r] = dict(
                         n_ins=shard.inserted, n_table=shard.n_table, ns=dm._ns, nsp=dm._nsp,

@@ -213,18 +213,6 @@ def test_sharded_small_then_large_input(P):
     check_ranks(gs, texts[2], P)
 
 
-def _dirty_device_memory(gib=4):
-    """Fill free device memory with 0xFF bytes and hand it back to the driver, so buffers the next
-    step allocates start as garbage (a fresh box hands out zeros, which hid round 6's store-overflow
-    bug: text records past the store's end read as rank 255)."""
-    import torch
-    t = torch.empty(gib << 30, dtype=torch.uint8, device="cuda")
-    t.fill_(0xFF)
-    torch.cuda.synchronize()
-    del t
-    torch.cuda.empty_cache()
-
-
 @pytest.mark.parametrize("k,L,every,P", [(19, 3000, 1, 2), (51, 1500, 3, 2), (19, 2000, 2, 3)])
 def test_sharded_overlapping_walks(k, L, every, P):
     """Walks that run into each other (malformed input: a k-mer with several predecessors, every
@@ -234,10 +222,26 @@ def test_sharded_overlapping_walks(k, L, every, P):
     needed). The ranks' texts, concatenated in rank order, equal the oracle's byte for byte (as the
     single-GPU kh_assemble's redo does, test_overlapping_walks_redo)."""
     from cs267_hw3_amd.dist import run_threaded
-    from test_gpu_parity import merging_walks
+    from test_gpu_parity import dirty_device_memory, merging_walks
     recs = merging_walks(k, L, seed=26 + k, every=every)
     rc, want, nc, _, _, _ = ob.assemble(k, recs)
     assert rc == 0 and len(want) > 4 * len(recs)
-    _dirty_device_memory()
+    dirty_device_memory()
     texts = run_threaded(k, recs, P)
     assert b"".join(texts) == want
+
+
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("n_long", [0, 2])
+def test_sharded_short_walk_first(P, n_long):
+    """Short walk first (dist.py assemble): contigs shorter than the splitter spacing walk without
+    splitter segments; two long chains make every rank walk again segmented (and keep doing so for
+    this input: the second step goes straight to the segmented walk). Ground truth either way."""
+    from cs267_hw3_amd.dist import run_threaded
+    g = kh.SyntheticKmers(51, 1_500_000, 2, 12, 0, seed=71 + n_long, n_long=n_long, long_len=40_000)
+    info = {}
+    texts = run_threaded(51, [g.records(), g.records()], P, info=info)
+    for t in texts:
+        check_ranks(g, t, P)
+    assert all(v == bool(n_long) for v in info["segmented"].values())
+
