@@ -1255,7 +1255,11 @@ __global__ __launch_bounds__(BLOCK) void k_seg_link(WalkBuffers wb, SegBuffers s
 // chain_jump 0.27 ms); 128 serial + jumps of 64 (~sqrt of the chain) + 64-hop jump and fill passes: ~320
 // (32 / 64 serial hops: C5 -0.08 / 0 ms but C2 1.24 -> 1.44 / 1.46 ms: C2's ~100-segment contigs then
 // take the jump passes; profiles/r05/ab/ab_misc.txt)
-static constexpr uint32_t SEG_SERIAL = 128, SEG_JUMP = 64;
+// Round 6: the serial prefix is SegBuffers::serial — SEG_SERIAL where contigs average many
+// segments (C2: ~50 walked splitters per start), SEG_SERIAL_FEW where long chains are rare
+// outliers among single-segment contigs (C5: 0.04 per start), whose few chains take the jump
+// passes anyway: 128 + 61 + 64 dependent hops become 32 + 61 + 64.
+static constexpr uint32_t SEG_SERIAL = 128, SEG_SERIAL_FEW = 32, SEG_JUMP = 64;
 __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers sb, unsigned long long* stats) {
     const uint64_t nseg = wb.n_starts + walk_splits(wb);
     for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < wb.n_starts; c += (uint64_t)gridDim.x * BLOCK) {
@@ -1279,7 +1283,7 @@ __global__ __launch_bounds__(BLOCK) void k_seg_chain(WalkBuffers wb, SegBuffers 
                 atomicAdd(&stats[ST_CYCLE], 1ull);
                 break;
             }
-            if (hops == SEG_SERIAL) {  // a long chain: the rest goes over jump pointers
+            if (hops == sb.serial) {  // a long chain: the rest goes over jump pointers
                 pend = g;
                 *sb.long_flag = 1u;
                 break;
@@ -1398,9 +1402,11 @@ hipError_t launch_seg_table(const KParams& p, const WalkBuffers& wb, const SegBu
 }
 
 // After the walk (and launch_seg_table): links, chains, offsets.
-hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb,
+hipError_t launch_segments(const KParams& p, const WalkBuffers& wb, const SegBuffers& sb_in,
                            unsigned long long* stats, hipStream_t s) {
     (void)p;
+    SegBuffers sb = sb_in;
+    sb.serial = wb.n_splits >= 16 * wb.n_starts ? SEG_SERIAL : SEG_SERIAL_FEW;
     const uint64_t nseg = wb.n_starts + wb.n_splits;
     if (nseg == 0) return hipSuccess;
     hipError_t e;

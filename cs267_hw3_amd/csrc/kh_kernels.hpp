@@ -151,7 +151,8 @@ struct SegBuffers {
     uint32_t* jsum;        // nseg: bases of the SEG_JUMP segments from this one
     uint8_t* anchor;       // nseg: a contig's walk over jump pointers visited this segment
     uint32_t* pend;        // n_starts: segment where a contig's serial walk stopped (SEG_NONE: done)
-    uint32_t* long_flag;   // one word: some contig has more than SEG_SERIAL segments
+    uint32_t* long_flag;   // one word: some contig has more than `serial` segments
+    uint32_t serial = 0;   // segments a contig's thread follows before the jump passes (launch_segments)
 };
 // splits with (hash & (2^bits - 1)) == 0 -> out (count to *count)
 hipError_t launch_filter_splits(const KParams& p, const uint64_t* splits, uint64_t n, int bits, uint64_t* off,
