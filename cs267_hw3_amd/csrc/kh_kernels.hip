@@ -980,6 +980,133 @@ __global__ __launch_bounds__(BLOCK) void k_write_lines(KParams p_in, const uint6
     }
 }
 
+// 64 bits of the 128-bit value (h:l) from bit s on, -64 < s < 64; s < 0 shifts left (zeros come in)
+__device__ __forceinline__ uint64_t bits64(uint64_t h, uint64_t l, int s) {
+    if (s < 0) return l << (-s);
+    return s == 0 ? l : (l >> s) | (h << (64 - s));
+}
+
+// The line writer at K >= 32: a wave owns 2 KiB of the text and a lane 32 contiguous bytes (two
+// 16-B stores). Contigs then hold >= 33 bytes, so a lane's 32 bytes still touch at most two
+// contigs (c, and the head of c + 1) and the <= 63 contigs that start in the wave's 2 KiB fit the
+// wave's 64 lanes. Per byte this halves what the 16-byte version repeats per lane — the contig
+// search, the key unpacks, the record loads — which is what bound it: VALU-bound at C5's
+// 60-byte lines (~280 VALU per 16-B lane store). line_first is the 1-KiB table (entry 2b).
+static constexpr uint32_t LINE2_BYTES = 2048;
+static constexpr int LINE2_KMIN = 32;
+
+template <int W, int KT>
+__global__ __launch_bounds__(BLOCK) void k_write_lines32(KParams p_in, const uint64_t* __restrict__ starts, uint64_t nc,
+                                                         const uint32_t* __restrict__ clen,
+                                                         const uint32_t* __restrict__ slen,
+                                                         const uint64_t* __restrict__ chunk_data, uint64_t chunk_cap,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ first,
+                                                         const unsigned long long* ctr, char* __restrict__ out,
+                                                         uint64_t cap, int slen_add) {
+    const KParams p = specialize<KT>(p_in);
+    const uint64_t lim = min((uint64_t)ctr[CT_OUT_BYTES], cap);
+    const uint32_t lane = lane_id();
+    const uint64_t nblk = (lim + LINE2_BYTES - 1) / LINE2_BYTES;
+    const uint64_t waves = (uint64_t)gridDim.x * (BLOCK / 64);
+    const int K = p.K;
+    const uint32_t xr = 32u * lane;  // the lane's first byte, relative to the block
+    constexpr int U = 2;
+    for (uint64_t blk0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / 64; blk0 < nblk; blk0 += U * waves) {
+        uint64_t c0[U], oj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c0[u] = first[2 * min(blk0 + u * waves, nblk - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) oj[u] = c0[u] + lane < nc ? off[c0[u] + lane] : ~0ull;
+        uint64_t x0[U], c[U];
+        int64_t rc[U];
+        uint32_t nb[U], hb[U];
+        bool live[U], two[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t blk = blk0 + u * waves, B = blk * LINE2_BYTES;
+            x0[u] = B + xr;
+            // offsets relative to the block as 32-bit (contig c0 starts at or before B: 0; past
+            // the contigs: the maximum), so the search shuffles and compares 32-bit values
+            const uint64_t rel = oj[u] - B;
+            const uint32_t r32 = oj[u] <= B ? 0u : rel > 0x7fffffffull ? 0x7fffffffu : (uint32_t)rel;
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t st = 32; st > 0; st >>= 1) {
+                const uint32_t v = (uint32_t)__shfl((int)r32, (int)(lo + st), 64);
+                if (v <= xr) lo += st;
+            }
+            const uint32_t rn = (uint32_t)__shfl((int)r32, (int)min(lo + 1, 63u), 64);
+            const uint64_t oc0 = __shfl(oj[u], 0, 64);
+            const uint32_t rl = (uint32_t)__shfl((int)r32, (int)lo, 64);
+            live[u] = blk < nblk && x0[u] < lim;
+            c[u] = c0[u] + lo;
+            two[u] = lo < 63 && rn < xr + 32 && c[u] + 1 < nc;  // the next contig starts inside these 32 bytes
+            rc[u] = lo ? (int64_t)(xr - rl) : (int64_t)(x0[u] - oc0);
+            nb[u] = two[u] ? rn - xr : 32u;  // bytes of contig c
+            hb[u] = rc[u] >= K ? 0u : min((uint32_t)(K - rc[u]), nb[u]);
+        }
+        auto head64 = [&](uint64_t w0, uint64_t w1, int rel0) {  // head base rel0 + b at bits 2b
+            const Key k = slot_key(w0, w1, p);
+            const uint64_t vl = k.lo | (k.hi << 62), vh = k.hi >> 2;  // V as 128 bits
+            return rev2_64(bits64(vh, vl, 2 * (K - 32 - rel0)));
+        };
+        uint64_t kc0[U], kc1[U], kn0[U], kn1[U], d0[U], d1[U];
+        uint32_t cl[U], sl[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // every load of both blocks before any use
+            const uint64_t cc = live[u] ? c[u] : 0, cn = live[u] && two[u] ? c[u] + 1 : cc;
+            kc0[u] = starts[cc * W];
+            kc1[u] = W == 2 ? starts[cc * W + 1] : 0;
+            kn0[u] = starts[cn * W];
+            kn1[u] = W == 2 ? starts[cn * W + 1] : 0;
+            cl[u] = clen[cc];
+            sl[u] = slen[cc];
+            const int64_t j0 = rc[u] - K;
+            const uint32_t w = j0 > 0 ? (uint32_t)min<int64_t>(j0 / 32, CHUNK_WORDS - 1) : 0u;
+            const bool need = live[u] && hb[u] < nb[u] && j0 < CHUNK_BASES;
+            d0[u] = need ? chunk_data[chunk_word(cc, w, chunk_cap)] : 0ull;
+            d1[u] = need && w + 1 < CHUNK_WORDS ? chunk_data[chunk_word(cc, w + 1, chunk_cap)] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;
+            // the head (rc < K, so rel0 >= 0 and hb >= 1 bytes of it)
+            uint64_t codes = hb[u] ? head64(kc0[u], kc1[u], (int)rc[u]) : 0ull;
+            if (hb[u] < nb[u]) {  // first-chunk bases j0 + b
+                const int64_t A = min<int64_t>((int64_t)sl[u] + slen_add - 1, CHUNK_BASES), j0 = rc[u] - K;
+                if (j0 + 32 > 0 && j0 < A) {
+                    const uint32_t w = j0 > 0 ? (uint32_t)(j0 / 32) : 0u;
+                    const uint64_t bw = bits64(d1[u], d0[u], (int)(2 * (j0 - 32 * (int64_t)w)));
+                    const uint64_t mh = hb[u] ? ~0ull >> (64 - 2 * hb[u]) : 0ull;
+                    codes = (codes & mh) | (bw & ~mh);
+                }
+            }
+            if (two[u]) {  // 32 - nb < 32 <= K: all of them head bases of contig c + 1
+                const uint64_t mn = ~0ull << (2 * nb[u]);
+                codes = (codes & ~mn) | ((head64(kn0[u], kn1[u], 0) << (2 * nb[u])) & mn);
+            }
+            const int64_t nl64 = (int64_t)K + cl[u] - 1 - rc[u];
+            const int nl = (nl64 >= 0 && nl64 < (int64_t)nb[u]) ? (int)nl64 : -1;
+            uint32_t v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t x = (uint32_t)(codes >> (8 * i)) & 0xFFu;
+                uint32_t sel = (x & 3u) | ((x << 6) & 0x300u) | ((x << 12) & 0x30000u) | ((x << 18) & 0x3000000u);
+                if (nl >= 4 * i && nl < 4 * i + 4)
+                    sel = (sel & ~(0xFFu << (8 * (nl - 4 * i)))) | (4u << (8 * (nl - 4 * i)));
+                v[i] = __builtin_amdgcn_perm(0x0A0A0A0Au, 0x54474341u, sel);
+            }
+            if (x0[u] + 32 <= lim) {
+                *reinterpret_cast<uint4*>(out + x0[u]) = make_uint4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<uint4*>(out + x0[u] + 16) = make_uint4(v[4], v[5], v[6], v[7]);
+            } else {
+                for (uint32_t b = 0; x0[u] + b < lim; ++b) out[x0[u] + b] = (char)(v[b >> 2] >> (8 * (b & 3)));
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_write_chunks(int K, const uint64_t* chunk_data,
                                                         const uint32_t* owner, const uint32_t* seq,
                                                         const unsigned long long* ctr,
@@ -1101,6 +1228,23 @@ static bool launch_lines(const KParams& p, const WalkBuffers& wb, const uint32_t
     if (!line_first || p.K < (int)LINE_KMIN) return false;
     const unsigned gf = (unsigned)hmin((nc + BLOCK - 1) / BLOCK, 8192);
     k_line_first<<<gf, BLOCK, 0, s>>>(p.K, clen, nc, offsets, ctr, cap, line_first);
+    if (p.K >= LINE2_KMIN) {
+        const uint64_t waves2 = (min(out_bytes, cap) + LINE2_BYTES - 1) / LINE2_BYTES;
+        const unsigned g2 = (unsigned)hmin((waves2 + BLOCK / 64 - 1) / (BLOCK / 64) + 1, 8192);
+        if (p.W == 1)
+            with_kt<1>(p.K, [&](auto kt) {
+                k_write_lines32<1, decltype(kt)::value><<<g2, BLOCK, 0, s>>>(
+                    p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data, wb.chunk_cap, offsets, line_first, ctr, out,
+                    cap, slen_add);
+            });
+        else
+            with_kt<2>(p.K, [&](auto kt) {
+                k_write_lines32<2, decltype(kt)::value><<<g2, BLOCK, 0, s>>>(
+                    p, wb.starts, nc, clen, wb.contig_len, wb.chunk_data, wb.chunk_cap, offsets, line_first, ctr, out,
+                    cap, slen_add);
+            });
+        return true;
+    }
     const uint64_t waves = (min(out_bytes, cap) + LINE_BYTES - 1) / LINE_BYTES;
     const unsigned gl = (unsigned)hmin((waves + BLOCK / 64 - 1) / (BLOCK / 64) + 1, 8192);
     if (p.W == 1)
