@@ -1087,14 +1087,16 @@ __global__ __launch_bounds__(BLOCK) void k_write_lines32(KParams p_in, const uin
                 codes = (codes & ~mn) | ((head64(kn0[u], kn1[u], 0) << (2 * nb[u])) & mn);
             }
             const int64_t nl64 = (int64_t)K + cl[u] - 1 - rc[u];
-            const int nl = (nl64 >= 0 && nl64 < (int64_t)nb[u]) ? (int)nl64 : -1;
+            // '\n' as selector bit 2 (selector 4 | code picks a byte of 0x0A0A0A0A): one bit per byte
+            const uint32_t nlm = (nl64 >= 0 && nl64 < (int64_t)nb[u]) ? 1u << (uint32_t)nl64 : 0u;
             uint32_t v[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
+                // 4 codes (2 bits each) spread to the low bits of 4 selector bytes
                 const uint32_t x = (uint32_t)(codes >> (8 * i)) & 0xFFu;
-                uint32_t sel = (x & 3u) | ((x << 6) & 0x300u) | ((x << 12) & 0x30000u) | ((x << 18) & 0x3000000u);
-                if (nl >= 4 * i && nl < 4 * i + 4)
-                    sel = (sel & ~(0xFFu << (8 * (nl - 4 * i)))) | (4u << (8 * (nl - 4 * i)));
+                const uint32_t t = (x | (x << 12)) & 0x000F000Fu;
+                const uint32_t nib = (nlm >> (4 * i)) & 0xFu;
+                const uint32_t sel = ((t | (t << 6)) & 0x03030303u) | (((nib * 0x00204081u) & 0x01010101u) << 2);
                 v[i] = __builtin_amdgcn_perm(0x0A0A0A0Au, 0x54474341u, sel);
             }
             if (x0[u] + 32 <= lim) {
